@@ -1,0 +1,159 @@
+/*
+ * mrbo.h -- C ABI of the MI355X rollout-acquisition evaluator (libmrbo.so).
+ *
+ * Drop-in boundary for the reference's Monte-Carlo rollout path.  The reference is pure
+ * Julia and has no FFI; each entry point below replaces one Julia function (file:line in
+ * /root/reference) and is what a `ccall` shim binds (INTEGRATION.md shows the shim):
+ *
+ *   mrbo_simulate_mc       simulate_trajectory_mc(T, tp; inner_solve_xstarts, resolutions,
+ *                          spatial_gradients_container, hyperparameter_gradients_container)
+ *                          rollout.jl:279-340 -- batched over R restarts (the x0 batch of the
+ *                          outer ascent, utils.jl:97-106 / stochastic_solve utils.jl:235-265)
+ *   mrbo_eto_reduce        the mean / std(n-1) tail of simulate_trajectory_mc, rollout.jl:328-339
+ *   mrbo_eval_base         eval(s::Surrogate, x, θ) radial_basis_surrogates.jl:224-310 (μ, σ, ∇, Hα)
+ *   mrbo_rnstream          gen_low_discrepancy_sequence utils.jl:65-74 (Sobol→Box–Muller(log10))
+ *   mrbo_initial_guesses   generate_initial_guesses utils.jl:145-153
+ *
+ * Conventions
+ *   - Plain pointers and sizes; matrices are column-major with the reference's (Julia) shapes.
+ *   - Arrays passed to mrbo_simulate_mc / mrbo_eto_reduce / mrbo_eval_base are DEVICE pointers
+ *     (hipMalloc'd or from a framework allocator) unless MRBO_FLAG_HOST_POINTERS is set, in
+ *     which case the library stages them through device memory (PCIe-inclusive).
+ *   - The plan owns the device copy of the base surrogate and all workspace; a call never
+ *     allocates (graph-capturable) and is re-entrant per (plan, stream) pair.
+ *   - Return value: 0 on success, negative mrbo_err_t on argument/launch errors (message via
+ *     mrbo_last_error()).  Per-trajectory numerical failures -- the reference's Julia
+ *     exceptions -- are reported in status[] (MRBO_ST_*), never as a return code.
+ */
+#ifndef MRBO_H
+#define MRBO_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MRBO_ABI_VERSION 1
+
+typedef enum {
+  MRBO_OK = 0,
+  MRBO_ERR_ARG = -1,      /* invalid argument (dimension, size, null pointer)            */
+  MRBO_ERR_UNSUPPORTED = -2, /* shape outside the compiled kernels (d > 8, N > 128, h > 5) */
+  MRBO_ERR_HIP = -3,      /* HIP runtime error                                          */
+  MRBO_ERR_NOMEM = -4
+} mrbo_err_t;
+
+typedef enum {
+  MRBO_KERNEL_MATERN52 = 0, /* radial_basis_functions.jl:60-68  */
+  MRBO_KERNEL_MATERN32 = 1, /* :70-78 */
+  MRBO_KERNEL_MATERN12 = 2, /* :80-88 */
+  MRBO_KERNEL_SE = 3        /* :90-96 */
+} mrbo_kernel_t;
+
+typedef enum { MRBO_RULE_EI = 0 /* decision_rules.jl:84-99 */ } mrbo_rule_t;
+
+/* per-trajectory status bits: the reference's exceptions (SURVEY.md §8b "Errors") */
+enum {
+  MRBO_ST_OK = 0,
+  MRBO_ST_SIGMA_NEG = 1,   /* DomainError sqrt(negative variance)   r_b_s.jl:528 */
+  MRBO_ST_DRAW_NOT_PD = 2, /* PosDefException, gp_draw covariance    r_b_s.jl:537 */
+  MRBO_ST_COND_NOT_PD = 4, /* PosDefException, update_cholesky!      r_b_s.jl:412 */
+  MRBO_ST_ALL_NAN = 8,     /* findmin on an empty candidate list     rbf_optim.jl:96 */
+  MRBO_ST_SINGULAR = 16    /* singular Hessian in solve_dual_x       rollout.jl:188 */
+};
+
+enum {
+  MRBO_FLAG_HOST_POINTERS = 1, /* arrays are host memory; stage through the device  */
+  MRBO_FLAG_NO_GRADIENT = 2    /* skip gradient(T): containers == nothing branch    */
+};
+
+/* Base GP surrogate (Surrogate struct, radial_basis_surrogates.jl:30-41), HOST memory. */
+typedef struct {
+  int32_t d;            /* input dimension                                        */
+  int32_t N;            /* observed points (get_observed)                         */
+  int32_t kernel;       /* mrbo_kernel_t                                          */
+  double lengthscale;   /* ψ.θ[1]                                                 */
+  double sigma_n2;      /* σn2                                                    */
+  double fmini;         /* minimum(s.y) over the whole capacity buffer (Q3)       */
+  const double* X;      /* d×N, column-major, leading dim d                       */
+  const double* L;      /* N×N lower Cholesky factor of K, column-major, ld = ldL */
+  int32_t ldL;
+  const double* c;      /* N coefficients L'\(L\y)                                */
+  const double* y;      /* N observations                                        */
+} mrbo_surrogate_t;
+
+/* TrajectoryParameters (trajectory.jl:43-94) + inner-solve options (rbf_optim.jl:24-30). */
+typedef struct {
+  int32_t h;            /* horizon (≤ 5)                                         */
+  int32_t M;            /* MC samples per restart (tp.mc_iters)                  */
+  int32_t R;            /* restarts (x0 batch)                                   */
+  int32_t nstarts;      /* inner starts = columns of inner_solve_xstarts         */
+  int32_t rule;         /* mrbo_rule_t                                           */
+  double theta;         /* T.θ[1]: decision-rule hyperparameter (Q12: T.θ, not tp.θ) */
+  const double* lbs;    /* d, HOST */
+  const double* ubs;    /* d, HOST */
+  int32_t max_iters;    /* inner Newton iterations per start      */
+  int32_t max_ls;       /* backtracking steps                                    */
+  double x_tol;         /* Optim x_tol (rbf_optim.jl:27) = 1e-3                  */
+  double f_tol;         /* Optim f_tol = 1e-3                                    */
+  double g_tol;         /* Optim default g_tol = 1e-8                            */
+  double htol;          /* solve_dual_x det threshold (rollout.jl:156) = 1e-4    */
+  double sigma_tol;     /* EI σtol (decision_rules.jl:84) = 1e-8                 */
+  uint64_t seed;        /* δx for solve_dual_y (rollout.jl:133) when dual_y_dx == NULL */
+} mrbo_params_t;
+
+typedef struct mrbo_plan mrbo_plan_t;
+
+const char* mrbo_version(void);
+const char* mrbo_last_error(void);
+int mrbo_device_count(void);
+
+/* Build the device state for (surrogate, params): copies X, L⁻¹ (packed), c; sizes the
+ * persistent-wave grid and workspace.  `device` is a HIP ordinal.                         */
+int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t device, mrbo_plan_t** out);
+int mrbo_plan_destroy(mrbo_plan_t* plan);
+
+/* simulate_trajectory_mc for the R×M trajectories of the plan.
+ *   x0s        d×R          start of each restart (tp.x0 / set_start!, rollout.jl:287)
+ *   rnstream   M×(d+1)×(h+1) tp.rnstream_sequence (trajectory.jl:52-68), shared by restarts
+ *   xstarts    d×nstarts    inner_solve_xstarts
+ *   dual_y_dx  d×h×M×R or NULL: δx of solve_dual_y call j (column j-1); NULL → counter RNG(seed)
+ *   replay_x   d×h×M×R or NULL: inject policy points x_1..x_h instead of the inner solve
+ *   values     M×R          resolutions
+ *   grad_x     d×M×R        spatial_gradients_container          (may be NULL with NO_GRADIENT)
+ *   grad_theta 1×M×R        hyperparameter_gradients_container   (may be NULL with NO_GRADIENT)
+ *   status     M×R          MRBO_ST_* bits
+ *   policy_x   d×(h+1)×M×R or NULL: x_0..x_h of every trajectory (fs.X[:, N+1:N+h+1])
+ *   obs        (h+1)×M×R or NULL:   sampled observations y_0..y_h
+ *   evals      M×R or NULL:         full surrogate evaluations spent in the inner solves
+ * Launches on `stream` (hipStream_t, may be NULL) and returns without synchronising.       */
+int mrbo_simulate_mc(mrbo_plan_t* plan, const double* x0s, const double* rnstream, const double* xstarts,
+                     const double* dual_y_dx, const double* replay_x, double* values, double* grad_x,
+                     double* grad_theta, int32_t* status, double* policy_x, double* obs, int64_t* evals,
+                     uint32_t flags, void* stream);
+
+/* ExpectedTrajectoryOutput per restart: eto R×W (row-major per restart, W = 2+2d+2):
+ * [μxθ, σ_μxθ, ∇μx(d), σ_∇μx(d), ∇μθ, σ_∇μθ]; std uses n-1 (Q14).                     */
+int mrbo_eto_reduce(mrbo_plan_t* plan, const double* values, const double* grad_x, const double* grad_theta,
+                    double* eto, uint32_t flags, void* stream);
+
+/* Partial sums for the multi-GPU allreduce: sums R×(2+2d+2) = [Σα, Σα², Σ∇x(d), Σ∇x²(d), Σ∇θ, Σ∇θ²]
+ * over the M_local samples of this rank (rollout.jl:328-339 in two-pass-free form).     */
+int mrbo_partial_sums(mrbo_plan_t* plan, const double* values, const double* grad_x, const double* grad_theta,
+                      int32_t M_local, double* sums, uint32_t flags, void* stream);
+
+/* eval(s, x, θ) of the base surrogate at P points xs (d×P); out stride 3+4d+d²:
+ * [μ, σ, α, ∇μ(d), ∇σ(d), ∇α(d), Hα(d×d col-major), d2α/dxdθ(d)].                       */
+int mrbo_eval_base(mrbo_plan_t* plan, int32_t P, const double* xs, double* out, uint32_t flags, void* stream);
+
+/* Host helpers (HOST memory). */
+int mrbo_rnstream(int32_t M, int32_t d, int32_t H, double* out);                 /* M×(d+1)×H */
+int mrbo_initial_guesses(int32_t n, int32_t d, const double* lbs, const double* ubs, double* out); /* d×(n+2) */
+double mrbo_dual_uniform(uint64_t seed, int64_t traj, int32_t j, int32_t k);
+
+/* Timing of the last mrbo_simulate_mc kernel on its stream (HIP events), milliseconds. */
+double mrbo_last_kernel_ms(mrbo_plan_t* plan);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

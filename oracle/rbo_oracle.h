@@ -1,0 +1,109 @@
+/*
+ * rbo_oracle.h -- CPU restatement of the Rollout-Bayesian-Optimization hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the parity checker for the MI355X
+ * product (libmrbo.so).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it.  The product never links or calls it.
+ *
+ * It restates, in plain C and in the reference's own (column-major, Julia) layout:
+ *   rollout.jl:39-340            rollout!, resolve, gradient (adjoint), simulate_trajectory_mc
+ *   radial_basis_surrogates.jl   Surrogate/FantasySurrogate eval, condition!, gp_draw,
+ *                                Spatial/DataPerturbationSurrogate (dense δK, as written)
+ *   radial_basis_functions.jl    Matern52/32/12, SquaredExponential and their ρ-derivatives
+ *   decision_rules.jl:84-99      EI and its partials (closed forms of the ForwardDiff partials)
+ *   observables.jl:83-124        StochasticObservable (gp_draw with gradient)
+ *   utils.jl:4-74,145-153        Sobol uniforms, Box–Muller(log10), rnstream reshape, inner starts
+ *   low_discrepancy.jl:7-28      kronecker_quasirand
+ * The inner policy solve (rbf_optim.jl:1-101, Optim.jl IPNewton -- absent, unpinned) is
+ * replaced by the build's deterministic projected Newton spec; the GPU
+ * implements the same spec.
+ *
+ * Parity status: UNPINNED against the Julia reference (julia is not installed, the
+ * reference ships no golden vectors).  Cross-checked against an independent NumPy
+ * restatement (tests/golden), scipy's Sobol, closed forms and the reference's own
+ * finite-difference methodology (runtests.jl:11-157).
+ */
+#ifndef RBO_ORACLE_H
+#define RBO_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { RBO_K_MATERN52 = 0, RBO_K_MATERN32 = 1, RBO_K_MATERN12 = 2, RBO_K_SE = 3 };
+
+/* per-trajectory status bits (reference: Julia exceptions, see SURVEY.md §8b "Errors") */
+enum {
+  RBO_ST_OK = 0,
+  RBO_ST_SIGMA_NEG = 1,      /* DomainError: sqrt of negative posterior variance (r_b_s.jl:528) */
+  RBO_ST_DRAW_NOT_PD = 2,    /* PosDefException in gp_draw covariance (r_b_s.jl:537)          */
+  RBO_ST_COND_NOT_PD = 4,    /* PosDefException in update_cholesky! (r_b_s.jl:412)            */
+  RBO_ST_ALL_NAN = 8,        /* findmin on empty candidate list (rbf_optim.jl:96-97)          */
+  RBO_ST_SINGULAR = 16       /* singular Hessian in solve_dual_x (rollout.jl:188)             */
+};
+
+typedef struct {
+  int32_t d, N;            /* dimension, base observations                       */
+  int32_t kernel;          /* RBO_K_*                                            */
+  double ell;              /* kernel lengthscale θ[1]                            */
+  double sigma_n2;         /* σn2                                                */
+  double fmini;            /* minimum(s.y) over the capacity buffer (Q3)         */
+  const double* X;         /* d×N column-major                                   */
+  const double* L;         /* N×N lower Cholesky of K, column-major, ld = N      */
+  const double* c;         /* N, L'\(L\y)                                        */
+  const double* y;         /* N                                                  */
+} rbo_surrogate;
+
+typedef struct {
+  int32_t h, M, R, nstarts;
+  double theta;            /* decision-rule hyperparameter T.θ[1] (EI ξ)         */
+  const double* lbs;       /* d */
+  const double* ubs;       /* d */
+  int32_t max_iters, max_ls;
+  double x_tol, f_tol, g_tol;
+  double htol;             /* det threshold in solve_dual_x (rollout.jl:156)     */
+  double sigma_tol;        /* EI σtol (decision_rules.jl:84)                     */
+  uint64_t seed;           /* counter-based δx for solve_dual_y when dual_y_dx==NULL */
+  int32_t with_gradient;
+  int32_t nthreads;        /* OpenMP threads for the (restart, sample) loop      */
+} rbo_params;
+
+/* utils.jl:4-13: D×samples Sobol uniforms (zero point skipped), column-major. */
+int rbo_gen_uniform(int32_t samples, int32_t dim, double* out);
+/* utils.jl:65-74: M×(d+1)×H rnstream, Julia column-major layout. */
+int rbo_gen_low_discrepancy_sequence(int32_t M, int32_t d, int32_t H, double* out);
+/* utils.jl:145-153: d×(n+2) inner starts. */
+int rbo_generate_initial_guesses(int32_t n, int32_t d, const double* lbs, const double* ubs, double* out);
+/* low_discrepancy.jl:7-28 */
+int rbo_kronecker_quasirand(int32_t d, int32_t N, int32_t start, double* out);
+/* counter-based uniform used for solve_dual_y's δx when the caller supplies none */
+double rbo_dual_uniform(uint64_t seed, int64_t traj, int32_t j, int32_t k);
+
+/* Evaluate the base surrogate (fantasy_index = -1) at P points: per point writes
+ * out[0]=μ, [1]=σ, [2]=α, [3..3+d)=∇μ, [3+d..3+2d)=∇σ, [3+2d..3+3d)=∇α,
+ * [3+3d..3+3d+d²)=Hα (col-major), then d2α/dxdθ (d).  stride = 3+4d+d². */
+int rbo_eval_base(const rbo_surrogate* s, double theta, double sigma_tol, int32_t P,
+                  const double* xs, double* out);
+
+/* simulate_trajectory_mc (rollout.jl:279-340) for R restarts x0s (d×R).
+ * Outputs (caller-allocated, Julia layout):
+ *   values   M×R, grad_x d×M×R, grad_theta 1×M×R, status M×R,
+ *   policy_x d×(h+1)×M×R (optional), obs (h+1)×M×R (optional).
+ * dual_y_dx: optional d×h×M×R uniforms (δx of solve_dual_y call j at column j-1).
+ * replay_x:  optional d×h×M×R policy points injected instead of the inner solve.
+ * eto: optional R×(2+2d+2) rows [μ, σ, ∇μx(d), σ∇x(d), ∇μθ, σ∇θ].
+ * newton_evals: optional M×R count of full surrogate evaluations performed. */
+int rbo_simulate_mc(const rbo_surrogate* s, const rbo_params* p, const double* x0s,
+                    const double* rnstream, const double* xstarts,
+                    const double* dual_y_dx, const double* replay_x,
+                    double* values, double* grad_x, double* grad_theta, int32_t* status,
+                    double* policy_x, double* obs, double* eto, int64_t* evals);
+
+/* Test functions (testfns.jl) used to make base data y. id: 0 GramacyLee, 1 BraninHoo,
+ * 2 Hartmann6D, 3 Ackley(d), 4 Rosenbrock, 5 Rastrigin(d). */
+double rbo_testfn(int32_t id, int32_t d, const double* x);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,539 @@
+// mrbo_api.hip -- C ABI (include/mrbo.h) of the MI355X rollout evaluator: plans, launches,
+// ETO reductions and host helpers.  Single translation unit with the device code.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mrbo.h"
+#include "mrbo_rollout.hip"
+#include "sobol_table.h"
+
+using namespace mrbo;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) return fail(MRBO_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+}  // namespace
+
+struct mrbo_plan {
+  int device = 0;
+  int d = 0, N = 0, RPL = 1, NR = 64, Npad = 64;
+  mrbo_params_t p{};
+  std::vector<double> lbs, ubs;
+  int kernel = 0;
+  double ell = 1, cK = 1, psi0 = 1, d2psi0 = -1, sn2 = 1e-6;
+  double fmin_base = 0, fmini = 0;
+  // device state
+  double* dX0 = nullptr;    // [d][NR]
+  double* dc0 = nullptr;    // [NR]
+  double* dLinv = nullptr;  // packed
+  double* dlbs = nullptr;
+  double* dubs = nullptr;
+  double* dwork = nullptr;
+  long long work_stride = 0;
+  int* dqueue = nullptr;
+  int wpg = 4, blocks = 0;
+  size_t smem = 0;
+  int ewpg = 4, eblocks = 0;
+  size_t esmem = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+};
+
+namespace {
+
+// ---- kernel dispatch tables -----------------------------------------------------------
+typedef void (*kfun_t)(KParams);
+
+template <int D, int RPL>
+size_t wave_lds_bytes() { return sizeof(double) * Lay<D, RPL>::WAVE_LDS; }
+
+struct KernelSet {
+  const void* rollout;
+  const void* evalb;
+  size_t wave_bytes;
+};
+
+template <int D, int RPL>
+KernelSet kset() {
+  return KernelSet{(const void*)&rollout_kernel<D, RPL>, (const void*)&eval_base_kernel<D, RPL>, wave_lds_bytes<D, RPL>()};
+}
+
+bool get_kset(int d, int rpl, KernelSet& ks) {
+#define CASE(DD)                                        \
+  case DD:                                              \
+    ks = (rpl == 1) ? kset<DD, 1>() : kset<DD, 2>();    \
+    return true;
+  switch (d) {
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+    default: return false;
+  }
+#undef CASE
+}
+
+void launch_rollout(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
+#define CASE(DD)                                                                           \
+  case DD:                                                                                 \
+    if (rpl == 1) hipLaunchKernelGGL((rollout_kernel<DD, 1>), g, b, sm, st, kp);           \
+    else hipLaunchKernelGGL((rollout_kernel<DD, 2>), g, b, sm, st, kp);                    \
+    break;
+  switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) }
+#undef CASE
+}
+void launch_evalb(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
+#define CASE(DD)                                                                           \
+  case DD:                                                                                 \
+    if (rpl == 1) hipLaunchKernelGGL((eval_base_kernel<DD, 1>), g, b, sm, st, kp);         \
+    else hipLaunchKernelGGL((eval_base_kernel<DD, 2>), g, b, sm, st, kp);                  \
+    break;
+  switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) }
+#undef CASE
+}
+
+// choose waves per workgroup maximising resident waves per CU (LDS + register limits)
+int pick_grid(const void* fn, size_t linv_bytes, size_t wave_bytes, int ncu, int& wpg, int& blocks, size_t& smem) {
+  int best_w = 0;
+  for (int w = 1; w <= 4; ++w) {
+    const size_t sm = linv_bytes + w * wave_bytes;
+    if (sm > 160 * 1024) break;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, w * WAVE, sm) != hipSuccess) continue;
+    const int waves = nb * w;
+    if (waves > best_w) { best_w = waves; wpg = w; blocks = nb * ncu; smem = sm; }
+  }
+  return best_w;
+}
+
+// ---- reductions: per (restart, component) block, deterministic tree order --------------
+// comp 0: values, 1..d: grad_x[a], d+1: grad_theta.  mode 0: ETO (mean, std n-1) -> eto;
+// mode 1: partial sums (Σ, Σ²) -> sums.
+__global__ void __launch_bounds__(256) reduce_kernel(const double* values, const double* grad_x,
+                                                     const double* grad_theta, int M, int d, int mode,
+                                                     double* out) {
+  __shared__ double sh[256];
+  const int r = blockIdx.x, comp = blockIdx.y, tid = threadIdx.x;
+  const int W = 2 + 2 * d + 2;
+  auto elem = [&](int m) -> double {
+    const long long idx = (long long)m + (long long)M * r;
+    if (comp == 0) return values[idx];
+    if (comp <= d) return grad_x ? grad_x[idx * d + (comp - 1)] : 0.0;
+    return grad_theta ? grad_theta[idx] : 0.0;
+  };
+  auto block_sum = [&](double v) -> double {
+    sh[tid] = v;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+      if (tid < s) sh[tid] += sh[tid + s];
+      __syncthreads();
+    }
+    const double t = sh[0];
+    __syncthreads();
+    return t;
+  };
+  double s = 0.0;
+  for (int m = tid; m < M; m += 256) s += elem(m);
+  const double tot = block_sum(s);
+  double s2 = 0.0;
+  if (mode == 0) {
+    const double mu = tot / M;
+    for (int m = tid; m < M; m += 256) { const double dv = elem(m) - mu; s2 += dv * dv; }
+  } else {
+    for (int m = tid; m < M; m += 256) { const double v = elem(m); s2 += v * v; }
+  }
+  const double tot2 = block_sum(s2);
+  if (tid == 0) {
+    int c0, c1;
+    if (comp == 0) { c0 = 0; c1 = 1; }
+    else if (comp <= d) { c0 = 2 + (comp - 1); c1 = 2 + d + (comp - 1); }
+    else { c0 = 2 + 2 * d; c1 = 3 + 2 * d; }
+    if (mode == 0) {
+      out[(long long)W * r + c0] = tot / M;
+      out[(long long)W * r + c1] = sqrt(tot2 / (M - 1));
+    } else {
+      out[(long long)W * r + c0] = tot;
+      out[(long long)W * r + c1] = tot2;
+    }
+  }
+}
+
+// ---- host Sobol (Joe-Kuo directions, Gray code, zero point skipped) ---------------------
+struct Sobol {
+  int dim;
+  std::vector<uint32_t> v;  // dim × 32
+  std::vector<uint32_t> x;
+  uint64_t n = 0;
+  explicit Sobol(int dim_) : dim(dim_), v((size_t)dim_ * 32), x(dim_, 0u) {
+    for (int j = 0; j < dim; ++j) {
+      const int s = mrbo_sobol_table[j].s, a = mrbo_sobol_table[j].a;
+      uint32_t m[33];
+      for (int k = 1; k <= 32; ++k) {
+        if (s == 0) m[k] = 1;
+        else if (k <= s) m[k] = mrbo_sobol_table[j].m[k - 1];
+        else {
+          uint32_t mk = m[k - s] ^ (m[k - s] << s);
+          for (int l = 1; l < s; ++l)
+            if ((a >> (s - 1 - l)) & 1) mk ^= m[k - l] << l;
+          m[k] = mk;
+        }
+      }
+      for (int k = 1; k <= 32; ++k) v[(size_t)j * 32 + k - 1] = m[k] << (32 - k);
+    }
+  }
+  void next(double* u) {
+    int c = 0;
+    while ((n >> c) & 1ULL) ++c;
+    for (int j = 0; j < dim; ++j) {
+      x[j] ^= v[(size_t)j * 32 + c];
+      u[j] = (double)x[j] * (1.0 / 4294967296.0);
+    }
+    ++n;
+  }
+};
+
+}  // namespace
+
+static void fill_common(const mrbo_plan_t* P, KParams& kp) {
+  memset(&kp, 0, sizeof kp);
+  kp.d = P->d; kp.N = P->N; kp.Npad = P->Npad; kp.h = P->p.h; kp.M = P->p.M; kp.R = P->p.R;
+  kp.nstarts = P->p.nstarts;
+  kp.kernel = P->kernel; kp.ell = P->ell; kp.cK = P->cK; kp.psi0 = P->psi0; kp.d2psi0 = P->d2psi0; kp.sn2 = P->sn2;
+  kp.fmin_base = P->fmin_base; kp.fmini = P->fmini; kp.theta = P->p.theta;
+  kp.max_iters = P->p.max_iters; kp.max_ls = P->p.max_ls;
+  kp.x_tol = P->p.x_tol; kp.f_tol = P->p.f_tol; kp.g_tol = P->p.g_tol; kp.htol = P->p.htol;
+  kp.sigma_tol = P->p.sigma_tol; kp.seed = P->p.seed;
+  kp.X0 = P->dX0; kp.c0 = P->dc0; kp.Linv = P->dLinv; kp.lbs = P->dlbs; kp.ubs = P->dubs;
+  kp.work = P->dwork; kp.work_stride = P->work_stride; kp.queue = P->dqueue;
+}
+
+// staging helper for MRBO_FLAG_HOST_POINTERS
+struct Stage {
+  std::vector<void*> bufs;
+  ~Stage() { for (void* b : bufs) (void)hipFree(b); }
+  template <class T>
+  int in(const T* h, size_t n, const T** dptr) {
+    if (!h) { *dptr = nullptr; return 0; }
+    void* d = nullptr;
+    if (hipMalloc(&d, sizeof(T) * n) != hipSuccess) return -1;
+    bufs.push_back(d);
+    if (hipMemcpy(d, h, sizeof(T) * n, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    *dptr = (const T*)d;
+    return 0;
+  }
+  template <class T>
+  int out(size_t n, T* h, T** dptr) {
+    if (!h) { *dptr = nullptr; return 0; }
+    void* d = nullptr;
+    if (hipMalloc(&d, sizeof(T) * n) != hipSuccess) return -1;
+    bufs.push_back(d);
+    *dptr = (T*)d;
+    return 0;
+  }
+};
+
+static int reduce_common(mrbo_plan_t* P, const double* values, const double* grad_x, const double* grad_theta,
+                         int M, double* out, int mode, uint32_t flags, void* stream) {
+  if (!P || !values || !out) return fail(MRBO_ERR_ARG, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  const int d = P->d, R = P->p.R;
+  const size_t T = (size_t)M * R, W = 2 + 2 * d + 2;
+  Stage sg;
+  const double *dv = values, *dg = grad_x, *dt = grad_theta;
+  double* dout = out;
+  if (flags & MRBO_FLAG_HOST_POINTERS) {
+    if (sg.in(values, T, &dv) || sg.in(grad_x, (size_t)d * T, &dg) || sg.in(grad_theta, T, &dt) ||
+        sg.out(W * R, out, &dout))
+      return fail(MRBO_ERR_NOMEM, "staging allocation failed");
+  }
+  hipLaunchKernelGGL(reduce_kernel, dim3(R, d + 2), dim3(256), 0, st, dv, dg, dt, M, d, mode, dout);
+  HIP_TRY(hipGetLastError());
+  if (flags & MRBO_FLAG_HOST_POINTERS) {
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipMemcpy(out, dout, sizeof(double) * W * R, hipMemcpyDeviceToHost));
+  }
+  return MRBO_OK;
+}
+
+// =========================================================================================
+extern "C" {
+
+const char* mrbo_version(void) { return "mrbo 0.1.0 (gfx950, fp64, ABI 1)"; }
+const char* mrbo_last_error(void) { return g_err.c_str(); }
+
+int mrbo_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t device, mrbo_plan_t** out) {
+  if (!s || !p || !out) return fail(MRBO_ERR_ARG, "null argument");
+  *out = nullptr;
+  const int d = s->d, N = s->N;
+  if (d < 1 || N < 1 || !s->X || !s->L || !s->c || !s->y) return fail(MRBO_ERR_ARG, "bad surrogate (d=%d N=%d)", d, N);
+  if (d > 8) return fail(MRBO_ERR_UNSUPPORTED, "d=%d > 8 not compiled", d);
+  if (N > 128) return fail(MRBO_ERR_UNSUPPORTED, "N=%d > 128 not supported (LDS-resident L0^-1)", N);
+  if (p->h < 0 || p->h > FMAX - 1) return fail(MRBO_ERR_UNSUPPORTED, "h=%d outside [0,%d]", p->h, FMAX - 1);
+  if (p->M < 1 || p->R < 1 || p->nstarts < 1 || !p->lbs || !p->ubs) return fail(MRBO_ERR_ARG, "bad params");
+  if (p->rule != MRBO_RULE_EI) return fail(MRBO_ERR_UNSUPPORTED, "only the EI base rule is compiled");
+  if (s->kernel < 0 || s->kernel > 3) return fail(MRBO_ERR_ARG, "kernel id %d", s->kernel);
+  const int ldL = s->ldL > 0 ? s->ldL : N;
+
+  mrbo_plan* P = new mrbo_plan();
+  P->device = device;
+  P->d = d;
+  P->N = N;
+  P->RPL = (N <= 64) ? 1 : 2;
+  P->NR = 64 * P->RPL;
+  P->Npad = P->NR;
+  P->p = *p;
+  P->lbs.assign(p->lbs, p->lbs + d);
+  P->ubs.assign(p->ubs, p->ubs + d);
+  P->p.lbs = nullptr;
+  P->p.ubs = nullptr;
+  P->kernel = s->kernel;
+  P->ell = s->lengthscale;
+  P->sn2 = s->sigma_n2;
+  P->fmini = s->fmini;
+  P->fmin_base = s->y[0];
+  for (int i = 1; i < N; ++i) P->fmin_base = std::min(P->fmin_base, s->y[i]);
+  const double ell = s->lengthscale;
+  switch (s->kernel) {
+    case 0: P->cK = std::sqrt(5.0) / ell; P->d2psi0 = -P->cK * P->cK / 3.0; break;
+    case 1: P->cK = std::sqrt(3.0) / ell; P->d2psi0 = -P->cK * P->cK; break;
+    case 2: P->cK = 1.0 / ell; P->d2psi0 = P->cK * P->cK; break;
+    default: P->cK = 1.0 / (ell * ell); P->d2psi0 = -P->cK; break;
+  }
+  P->psi0 = 1.0;
+
+  // L0^-1 by forward substitution on the unit columns, packed column-major (Npad rows)
+  const int Npad = P->Npad;
+  std::vector<double> Li((size_t)N * N, 0.0);  // col-major N×N
+  for (int j = 0; j < N; ++j) {
+    double* col = &Li[(size_t)j * N];
+    for (int i = j; i < N; ++i) {
+      double sacc = (i == j) ? 1.0 : 0.0;
+      for (int k = j; k < i; ++k) sacc -= s->L[i + (size_t)ldL * k] * col[k];
+      col[i] = sacc / s->L[i + (size_t)ldL * i];
+    }
+  }
+  std::vector<double> packed((size_t)linv_size(Npad), 0.0);
+  for (int j = 0; j < N; ++j)
+    for (int i = j; i < N; ++i) packed[(size_t)linv_colstart(j, Npad) + (i - j)] = Li[i + (size_t)N * j];
+  std::vector<double> X0((size_t)d * P->NR, 0.0), c0(P->NR, 0.0);
+  for (int i = 0; i < N; ++i) {
+    for (int a = 0; a < d; ++a) X0[(size_t)a * P->NR + i] = s->X[a + (size_t)d * i];
+    c0[i] = s->c[i];
+  }
+
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) { delete P; return fail(MRBO_ERR_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e)); }
+  KernelSet ks;
+  get_kset(d, P->RPL, ks);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete P; return fail(MRBO_ERR_HIP, "device props"); }
+  const size_t linv_bytes = sizeof(double) * (size_t)((linv_size(Npad) + 1) & ~1LL);
+  if (!pick_grid(ks.rollout, linv_bytes, ks.wave_bytes, prop.multiProcessorCount, P->wpg, P->blocks, P->smem) ||
+      !pick_grid(ks.evalb, linv_bytes, ks.wave_bytes, prop.multiProcessorCount, P->ewpg, P->eblocks, P->esmem)) {
+    delete P;
+    return fail(MRBO_ERR_UNSUPPORTED, "no feasible launch configuration");
+  }
+  const int slots = std::max(P->blocks * P->wpg, P->eblocks * P->ewpg);
+  P->work_stride = (long long)(2 * FMAX + 1) * P->NR;
+  bool ok = hipMalloc(&P->dX0, sizeof(double) * X0.size()) == hipSuccess &&
+            hipMalloc(&P->dc0, sizeof(double) * c0.size()) == hipSuccess &&
+            hipMalloc(&P->dLinv, sizeof(double) * packed.size()) == hipSuccess &&
+            hipMalloc(&P->dlbs, sizeof(double) * d) == hipSuccess &&
+            hipMalloc(&P->dubs, sizeof(double) * d) == hipSuccess &&
+            hipMalloc(&P->dwork, sizeof(double) * (size_t)slots * P->work_stride) == hipSuccess &&
+            hipMalloc(&P->dqueue, sizeof(int) * 4) == hipSuccess;
+  ok = ok && hipMemcpy(P->dX0, X0.data(), sizeof(double) * X0.size(), hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(P->dc0, c0.data(), sizeof(double) * c0.size(), hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(P->dLinv, packed.data(), sizeof(double) * packed.size(), hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(P->dlbs, P->lbs.data(), sizeof(double) * d, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(P->dubs, P->ubs.data(), sizeof(double) * d, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemset(P->dwork, 0, sizeof(double) * (size_t)slots * P->work_stride) == hipSuccess &&
+       hipEventCreate(&P->ev0) == hipSuccess && hipEventCreate(&P->ev1) == hipSuccess;
+  if (!ok) {
+    mrbo_plan_destroy(P);
+    return fail(MRBO_ERR_NOMEM, "device allocation failed");
+  }
+  *out = P;
+  return MRBO_OK;
+}
+
+int mrbo_plan_destroy(mrbo_plan_t* P) {
+  if (!P) return MRBO_OK;
+  for (void* b : {(void*)P->dX0, (void*)P->dc0, (void*)P->dLinv, (void*)P->dlbs, (void*)P->dubs, (void*)P->dwork,
+                  (void*)P->dqueue})
+    if (b) (void)hipFree(b);
+  if (P->ev0) (void)hipEventDestroy(P->ev0);
+  if (P->ev1) (void)hipEventDestroy(P->ev1);
+  delete P;
+  return MRBO_OK;
+}
+
+int mrbo_simulate_mc(mrbo_plan_t* P, const double* x0s, const double* rnstream, const double* xstarts,
+                     const double* dual_y_dx, const double* replay_x, double* values, double* grad_x,
+                     double* grad_theta, int32_t* status, double* policy_x, double* obs, int64_t* evals,
+                     uint32_t flags, void* stream) {
+  if (!P || !x0s || !rnstream || !xstarts || !values || !status) return fail(MRBO_ERR_ARG, "null argument");
+  const bool with_grad = !(flags & MRBO_FLAG_NO_GRADIENT);
+  if (with_grad && (!grad_x || !grad_theta)) return fail(MRBO_ERR_ARG, "gradient containers required");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipSetDevice(P->device) != hipSuccess) return fail(MRBO_ERR_HIP, "hipSetDevice");
+  const int d = P->d, h = P->p.h, M = P->p.M, R = P->p.R;
+  const size_t T = (size_t)M * R;
+  KParams kp;
+  fill_common(P, kp);
+  kp.with_gradient = with_grad ? 1 : 0;
+  kp.T = (long long)T;
+  Stage sg;
+  const bool host = flags & MRBO_FLAG_HOST_POINTERS;
+  double *dvalues = values, *dgx = grad_x, *dgt = grad_theta, *dpol = policy_x, *dobs = obs;
+  int32_t* dstatus = status;
+  int64_t* devals = evals;
+  if (host) {
+    if (sg.in(x0s, (size_t)d * R, &kp.x0s) || sg.in(rnstream, (size_t)M * (d + 1) * (h + 1), &kp.rn) ||
+        sg.in(xstarts, (size_t)d * P->p.nstarts, &kp.xstarts) ||
+        sg.in(dual_y_dx, (size_t)d * std::max(h, 1) * T, &kp.dual_y) ||
+        sg.in(replay_x, (size_t)d * std::max(h, 1) * T, &kp.replay) || sg.out(T, values, &dvalues) ||
+        sg.out((size_t)d * T, with_grad ? grad_x : nullptr, &dgx) || sg.out(T, with_grad ? grad_theta : nullptr, &dgt) ||
+        sg.out(T, status, &dstatus) || sg.out((size_t)d * (h + 1) * T, policy_x, &dpol) ||
+        sg.out((size_t)(h + 1) * T, obs, &dobs) || sg.out(T, evals, &devals))
+      return fail(MRBO_ERR_NOMEM, "staging allocation failed");
+  } else {
+    kp.x0s = x0s; kp.rn = rnstream; kp.xstarts = xstarts; kp.dual_y = dual_y_dx; kp.replay = replay_x;
+  }
+  kp.values = dvalues; kp.grad_x = with_grad ? dgx : nullptr; kp.grad_theta = with_grad ? dgt : nullptr;
+  kp.status = (int*)dstatus; kp.policy = dpol; kp.obs = dobs; kp.evals = (long long*)devals;
+  HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * 4, st));
+  HIP_TRY(hipEventRecord(P->ev0, st));
+  launch_rollout(d, P->RPL, dim3(P->blocks), dim3(P->wpg * WAVE), P->smem, st, kp);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(P->ev1, st));
+  P->timed = true;
+  if (host) {
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipMemcpy(values, dvalues, sizeof(double) * T, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(status, dstatus, sizeof(int32_t) * T, hipMemcpyDeviceToHost));
+    if (with_grad) {
+      HIP_TRY(hipMemcpy(grad_x, dgx, sizeof(double) * d * T, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(grad_theta, dgt, sizeof(double) * T, hipMemcpyDeviceToHost));
+    }
+    if (policy_x) HIP_TRY(hipMemcpy(policy_x, dpol, sizeof(double) * d * (h + 1) * T, hipMemcpyDeviceToHost));
+    if (obs) HIP_TRY(hipMemcpy(obs, dobs, sizeof(double) * (h + 1) * T, hipMemcpyDeviceToHost));
+    if (evals) HIP_TRY(hipMemcpy(evals, devals, sizeof(int64_t) * T, hipMemcpyDeviceToHost));
+  }
+  return MRBO_OK;
+}
+
+int mrbo_eto_reduce(mrbo_plan_t* P, const double* values, const double* grad_x, const double* grad_theta,
+                    double* eto, uint32_t flags, void* stream) {
+  return reduce_common(P, values, grad_x, grad_theta, P ? P->p.M : 0, eto, 0, flags, stream);
+}
+
+int mrbo_partial_sums(mrbo_plan_t* P, const double* values, const double* grad_x, const double* grad_theta,
+                      int32_t M_local, double* sums, uint32_t flags, void* stream) {
+  return reduce_common(P, values, grad_x, grad_theta, M_local, sums, 1, flags, stream);
+}
+
+int mrbo_eval_base(mrbo_plan_t* P, int32_t npts, const double* xs, double* out, uint32_t flags, void* stream) {
+  if (!P || !xs || !out || npts < 1) return fail(MRBO_ERR_ARG, "bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipSetDevice(P->device) != hipSuccess) return fail(MRBO_ERR_HIP, "hipSetDevice");
+  const int d = P->d;
+  const size_t stride = 3 + 4 * d + d * d;
+  KParams kp;
+  fill_common(P, kp);
+  kp.T = npts;
+  Stage sg;
+  const double* dxs = xs;
+  double* dout = out;
+  if (flags & MRBO_FLAG_HOST_POINTERS) {
+    if (sg.in(xs, (size_t)d * npts, &dxs) || sg.out(stride * npts, out, &dout))
+      return fail(MRBO_ERR_NOMEM, "staging allocation failed");
+  }
+  kp.pts = dxs;
+  kp.pts_out = dout;
+  HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * 4, st));
+  launch_evalb(d, P->RPL, dim3(P->eblocks), dim3(P->ewpg * WAVE), P->esmem, st, kp);
+  HIP_TRY(hipGetLastError());
+  if (flags & MRBO_FLAG_HOST_POINTERS) {
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipMemcpy(out, dout, sizeof(double) * stride * npts, hipMemcpyDeviceToHost));
+  }
+  return MRBO_OK;
+}
+
+double mrbo_last_kernel_ms(mrbo_plan_t* P) {
+  if (!P || !P->timed) return -1.0;
+  float ms = -1.f;
+  if (hipEventSynchronize(P->ev1) != hipSuccess) return -1.0;
+  if (hipEventElapsedTime(&ms, P->ev0, P->ev1) != hipSuccess) return -1.0;
+  return ms;
+}
+
+// utils.jl:4-74 -- Sobol uniforms → Box–Muller with log10 (Q1) → column-major reshape (Q2)
+int mrbo_rnstream(int32_t M, int32_t d, int32_t H, double* out) {
+  if (M < 1 || d < 1 || H < 1 || !out) return fail(MRBO_ERR_ARG, "bad arguments");
+  const int off = ((d + 1) % 2 == 1) ? 1 : 0, Dp = d + 1 + off;
+  if (Dp > MRBO_SOBOL_TABLE_MAXDIM) return fail(MRBO_ERR_UNSUPPORTED, "dimension");
+  Sobol sob(Dp);
+  const long long cols = (long long)M * H;
+  std::vector<double> u(Dp), y(Dp);
+  const double twopi = 2.0 * 3.141592653589793;
+  for (long long j = 0; j < cols; ++j) {
+    sob.next(u.data());
+    for (int i = 0; i < Dp; ++i)
+      y[i] = (i % 2 == 0) ? std::sqrt(-2.0 * std::log10(u[i])) * std::cos(twopi * u[i + 1])
+                          : std::sqrt(-2.0 * std::log10(u[i - 1])) * std::sin(twopi * u[i]);
+    for (int i = 0; i < Dp; ++i) {
+      const long long l = j * Dp + i;             // linear index in the Dp × (M·H) matrix
+      const long long m = l % M, rest = l / M;    // reshape to M × Dp × H
+      const long long k = rest % Dp, t = rest / Dp;
+      if (k < d + 1) out[m + (long long)M * k + (long long)M * (d + 1) * t] = y[i];
+    }
+  }
+  return MRBO_OK;
+}
+
+int mrbo_initial_guesses(int32_t n, int32_t d, const double* lbs, const double* ubs, double* out) {
+  if (n < 0 || d < 1 || d > MRBO_SOBOL_TABLE_MAXDIM || !lbs || !ubs || !out) return fail(MRBO_ERR_ARG, "bad arguments");
+  Sobol sob(d);
+  std::vector<double> u(d);
+  for (int j = 0; j < n; ++j) {
+    sob.next(u.data());
+    for (int a = 0; a < d; ++a) out[(size_t)j * d + a] = lbs[a] + (ubs[a] - lbs[a]) * u[a];
+  }
+  for (int a = 0; a < d; ++a) out[(size_t)n * d + a] = lbs[a] + 1e-6;
+  for (int a = 0; a < d; ++a) out[(size_t)(n + 1) * d + a] = ubs[a] - 1e-6;
+  return MRBO_OK;
+}
+
+double mrbo_dual_uniform(uint64_t seed, int64_t traj, int32_t j, int32_t k) { return dual_uniform(seed, traj, j, k); }
+
+}  // extern "C"

@@ -1,0 +1,1241 @@
+// mrbo_rollout.hip -- the MI355X rollout-trajectory kernel (forward rollout + adjoint).
+//
+// Restates, for one wavefront per trajectory:
+//   rollout!              rollout.jl:39-74        (draw at x0, h × [inner solve, draw, condition!])
+//   gp_draw / observable  radial_basis_surrogates.jl:588-611, observables.jl:106-121
+//   condition!            radial_basis_surrogates.jl:431-441 (rank-1 append; inverse-factor row)
+//   eval(fs, x, θ)        radial_basis_surrogates.jl:482-581 (μ, σ, ∇, H of EI; no μσ term, Q11)
+//   multistart solve      rbf_optim.jl:1-101 (deterministic projected Newton)
+//   resolve               rollout.jl:108-111 (fmini over the capacity buffer, Q3)
+//   gradient(T)           rollout.jl:126-277 (adjoint back-substitution, sparse δK)
+// Numerics follow the reference formulas; the triangular solves use the explicit inverse
+// factor L⁻¹ = [[L0⁻¹,0],[E,Dinv]] instead of substitution (same maths, fp64).
+#include "mrbo_device.h"
+
+namespace mrbo {
+
+template <int D, int RPL>
+struct Lay {
+  static constexpr int D1 = D + 1;
+  static constexpr int BS = (D1 + 1) & ~1;         // B row stride in doubles (16-B aligned rows)
+  static constexpr int NR = RPL * WAVE;            // base-row capacity of the wave
+  static constexpr int BROWS = NR + FMAX;          // base rows + fantasy rows
+  static constexpr int NG = D1 * (D1 + 1) / 2;     // Gram entries (a ≤ b)
+  static constexpr int NH = D * (D + 1) / 2;       // Hessian entries (a ≤ b)
+  // reduction-total layout
+  static constexpr int R_VAL = 0;                  // [vv, μ0, E_r·B0 (r<FMAX)]  (8)
+  static constexpr int R_G = 8;                    // Gram entries 1..NG-1
+  static constexpr int NGC = (NG - 1 + 15) / 16;   // G chunks
+  static constexpr int R_MF = R_G + 16 * NGC;      // [c·∇k (D), E_r·∇k (D each)]
+  static constexpr int NMF = D * (1 + FMAX);
+  static constexpr int NMFC = (NMF + 15) / 16;
+  static constexpr int NPAIR = D * D + 2 * D;      // adjoint pair products
+  static constexpr int NPC = (NPAIR + 15) / 16;
+  static constexpr int NHC = (NH + 1 + 15) / 16;
+  static constexpr int REDN_A = R_MF + 16 * NMFC;
+  static constexpr int REDN_B = 16 * (NPC > NHC ? NPC : NHC);
+  static constexpr int REDN = ((REDN_A > REDN_B ? REDN_A : REDN_B) + 1) & ~1;
+  // lane-uniform LDS area (doubles)
+  static constexpr int U_X = 0;                          // eval point            D
+  static constexpr int U_XB = U_X + 8;                   // best multistart point D
+  static constexpr int U_XF = U_XB + 8;                  // fantasy points        FMAX*D
+  static constexpr int U_YF = U_XF + FMAX * D;           // fantasy observations  FMAX
+  static constexpr int U_GF = U_YF + FMAX;               // sampled gradients     FMAX*D
+  static constexpr int U_DINV = U_GF + FMAX * D;         // Dinv row-major        FMAX*FMAX
+  static constexpr int U_CF = U_DINV + FMAX * FMAX;      // fantasy coeffs/surf.  (FMAX+1)*FMAX
+  static constexpr int U_FMIN = U_CF + (FMAX + 1) * FMAX;// fmin per surface      FMAX+1
+  static constexpr int U_SC = U_FMIN + FMAX + 1;         // scalars: μ,σ,α,G00,σ²,... 16
+  static constexpr int U_GMU = U_SC + 16;                // ∇μ   D
+  static constexpr int U_GSIG = U_GMU + D;               // ∇σ   D
+  static constexpr int U_GAL = U_GSIG + D;               // ∇α   D
+  static constexpr int U_MIX = U_GAL + D;                // d2α/dxdθ D
+  static constexpr int U_G = U_MIX + D;                  // Gram D1×D1
+  static constexpr int U_H = U_G + D1 * D1;              // Hα   D×D
+  static constexpr int U_YFV = U_H + D * D;              // Yf   FMAX×D1
+  static constexpr int U_WF = U_YFV + FMAX * D1;         // w_f  FMAX
+  static constexpr int U_PF = U_WF + FMAX;               // P_f  FMAX×D
+  static constexpr int U_GMU0 = U_PF + FMAX * D;         // ∇μ(x0) on the base surface  D
+  static constexpr int U_XBAR = U_GMU0 + D;              // x̄_j  FMAX×D
+  static constexpr int U_ACC = U_XBAR + FMAX * D;        // Σ dri' x̄  FMAX×D
+  static constexpr int U_YBAR = U_ACC + FMAX * D;        // ȳ_j  FMAX+1
+  static constexpr int U_DX = U_YBAR + FMAX + 1;         // δx    D
+  static constexpr int U_SIZE = ((U_DX + 8) + 1) & ~1;
+  static constexpr int WAVE_LDS = BROWS * BS + REDN + U_SIZE;
+};
+// scalar slots in U_SC
+enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, SC_GSIG = 6, SC_GMUMU = 7,
+       SC_GSIGSIG = 8, SC_GMUTH = 9, SC_GSIGTH = 10, SC_FMIN = 11, SC_ST = 12 };
+
+template <int D, int RPL>
+struct WaveCtx {
+  using Ly = Lay<D, RPL>;
+  int lane;
+  double* B;            // LDS: BROWS × BS
+  double* red;          // LDS: REDN
+  double* U;            // LDS: U_SIZE
+  const double* Linv;   // LDS: packed L0⁻¹
+  double* E;            // global: FMAX × NR   inverse-factor fantasy rows (base columns)
+  double* C;            // global: (FMAX+1) × NR  base part of c for surfaces -1..h
+  double X0[RPL][D];    // own base rows
+  bool valid[RPL];
+  int N, Npad;
+  Radial rad;
+};
+
+// Per-lane results of an evaluation that later phases (conditioning, adjoint) need.
+template <int D, int RPL>
+struct LaneRes {
+  double w[RPL];
+  double P[RPL][D];
+  double cb[RPL];
+};
+
+// Linv(k, i), k ≥ i, from the packed layout
+template <int D, int RPL>
+__device__ __forceinline__ double linv_at(const WaveCtx<D, RPL>& W, int k, int i) {
+  return W.Linv[linv_colstart(i, W.Npad) + (k - i)];
+}
+
+// ================================================================================
+// eval(fs, x, θ; fantasy_index = S)  -- radial_basis_surrogates.jl:482-581
+//   x is read from U[U_X].  Results land in U (lane-uniform) and `lr` (per lane).
+// ================================================================================
+template <int D, int RPL>
+__device__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, int S, int mode, LaneRes<D, RPL>& lr) {
+  using Ly = Lay<D, RPL>;
+  constexpr int D1 = Ly::D1, BS = Ly::BS, NR = Ly::NR;
+  const int lane = W.lane;
+  const int nf = S + 1;
+  double* U = W.U;
+  double* B = W.B;
+  double* red = W.red;
+  const bool all_cols = (mode != EV_VALUE);
+
+  double x[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) x[a] = U[Ly::U_X + a];
+
+  // base coefficients of surface S and this lane's entries of the fantasy inverse-factor rows
+  double Ev[RPL][FMAX];
+#pragma unroll
+  for (int s = 0; s < RPL; ++s) {
+    lr.cb[s] = W.C[(long long)(S + 1) * NR + lane + WAVE * s];
+#pragma unroll
+    for (int r = 0; r < FMAX; ++r) Ev[s][r] = (r < nf) ? W.E[(long long)r * NR + lane + WAVE * s] : 0.0;
+  }
+
+  // ---- 1. kernel rows B[i] = [k(x,X_i), ∇k(x - X_i)]  (eval_KxX :180-191, eval_∇KxX :193-208)
+  double Bown[RPL][D1];
+#pragma unroll
+  for (int s = 0; s < RPL; ++s) {
+    double r[D], rho2 = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) { r[a] = x[a] - W.X0[s][a]; rho2 = fma(r[a], r[a], rho2); }
+    const double rho = sqrt(rho2);
+    double psi, dpsi;
+    rad_psi(W.rad, rho, psi, dpsi);
+    const bool v = W.valid[s];
+    Bown[s][0] = v ? psi : 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) Bown[s][1 + a] = (v && rho > 0.0) ? dpsi * (r[a] / rho) : 0.0;
+    double* row = B + (lane + WAVE * s) * BS;
+    if (all_cols) {
+#pragma unroll
+      for (int c = 0; c < D1; ++c) row[c] = Bown[s][c];
+    } else {
+      row[0] = Bown[s][0];
+    }
+  }
+  if (lane < nf) {  // fantasy rows B[N + r]
+    double r[D], rho2 = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) { r[a] = x[a] - U[Ly::U_XF + lane * D + a]; rho2 = fma(r[a], r[a], rho2); }
+    const double rho = sqrt(rho2);
+    double psi, dpsi;
+    rad_psi(W.rad, rho, psi, dpsi);
+    double* row = B + (NR + lane) * BS;
+    row[0] = psi;
+#pragma unroll
+    for (int a = 0; a < D; ++a) row[1 + a] = (rho > 0.0) ? dpsi * (r[a] / rho) : 0.0;
+  }
+  wave_sync();
+
+  // ---- 2. forward product  Y[i] = Σ_{j ≤ i} L0⁻¹[i,j] B[j]   (L\kxX' , r_b_s.jl:525-526)
+  double acc[RPL][D1];
+#pragma unroll
+  for (int s = 0; s < RPL; ++s)
+#pragma unroll
+    for (int c = 0; c < D1; ++c) acc[s][c] = 0.0;
+  const int N = W.N;
+  if (all_cols) {
+    for (int j = 0; j < N; ++j) {
+      const double* bj = B + j * BS;
+      double bv[D1];
+#pragma unroll
+      for (int c = 0; c < D1; ++c) bv[c] = bj[c];
+      const long long cs = linv_colstart(j, W.Npad) - j;
+#pragma unroll
+      for (int s = 0; s < RPL; ++s) {
+        const int i = lane + WAVE * s;
+        const double l = (i >= j && W.valid[s]) ? W.Linv[cs + i] : 0.0;
+#pragma unroll
+        for (int c = 0; c < D1; ++c) acc[s][c] = fma(l, bv[c], acc[s][c]);
+      }
+    }
+  } else {
+    for (int j = 0; j < N; ++j) {
+      const double b0 = B[j * BS];
+      const long long cs = linv_colstart(j, W.Npad) - j;
+#pragma unroll
+      for (int s = 0; s < RPL; ++s) {
+        const int i = lane + WAVE * s;
+        const double l = (i >= j && W.valid[s]) ? W.Linv[cs + i] : 0.0;
+        acc[s][0] = fma(l, b0, acc[s][0]);
+      }
+    }
+  }
+
+  // ---- 3. per-lane products and wave reductions
+  {
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = 0.0;
+#pragma unroll
+    for (int s = 0; s < RPL; ++s) {
+      v[0] = fma(acc[s][0], acc[s][0], v[0]);      // |v|² = kx'K⁻¹kx (base part)
+      v[1] = fma(lr.cb[s], Bown[s][0], v[1]);       // μ = kx·c (base part)
+#pragma unroll
+      for (int r = 0; r < FMAX; ++r)
+        if (r < nf) v[2 + r] = fma(Ev[s][r], Bown[s][0], v[2 + r]);
+    }
+    wave_reduce<8>(v, red + Ly::R_VAL, lane);
+  }
+  if (all_cols) {
+    // Gram entries (a ≤ b) except (0,0)
+#pragma unroll
+    for (int ch = 0; ch < Ly::NGC; ++ch) {
+      double v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int t = 1 + 16 * ch + q;  // linear pair index
+        double s_ = 0.0;
+        if (t < Ly::NG) {
+          // unrank t -> (a, b), a ≤ b, row-major upper triangle
+          int a = 0, rem = t;
+#pragma unroll
+          for (int aa = 0; aa < D1; ++aa) if (a == aa && rem >= D1 - aa) { rem -= D1 - aa; a = aa + 1; }
+          const int b = a + rem;
+#pragma unroll
+          for (int s = 0; s < RPL; ++s) s_ = fma(acc[s][a], acc[s][b], s_);
+        }
+        v[q] = s_;
+      }
+      wave_reduce<16>(v, red + Ly::R_G + 16 * ch, lane);
+    }
+    // ∇μ and fantasy cross products for the gradient columns
+#pragma unroll
+    for (int ch = 0; ch < Ly::NMFC; ++ch) {
+      double v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int t = 16 * ch + q;
+        double s_ = 0.0;
+        if (t < Ly::NMF) {
+          const int grp = t / D, a = t % D;  // grp 0: c ; grp r+1: E_r
+          if (grp == 0) {
+#pragma unroll
+            for (int s = 0; s < RPL; ++s) s_ = fma(lr.cb[s], Bown[s][1 + a], s_);
+          } else if (grp - 1 < nf) {
+#pragma unroll
+            for (int s = 0; s < RPL; ++s) s_ = fma(Ev[s][grp - 1], Bown[s][1 + a], s_);
+          }
+        }
+        v[q] = s_;
+      }
+      wave_reduce<16>(v, red + Ly::R_MF + 16 * ch, lane);
+    }
+  }
+  wave_sync();
+
+  // ---- 4. fantasy rows of the forward product: Yf = Fpart + Dinv · Bf   (lane = (r, c))
+  {
+    const int ncol = all_cols ? D1 : 1;
+    if (lane < nf * ncol) {
+      const int r = lane / ncol, c = lane % ncol;
+      double y = (c == 0) ? red[Ly::R_VAL + 2 + r] : red[Ly::R_MF + D + r * D + (c - 1)];
+      for (int q = 0; q <= r; ++q) y = fma(U[Ly::U_DINV + r * FMAX + q], B[(NR + q) * BS + c], y);
+      U[Ly::U_YFV + r * D1 + c] = y;
+    }
+  }
+  wave_sync();
+  // ---- Gram (incl. fantasy rows) and μ, ∇μ  (lanes own entries)
+  {
+    const int ng = all_cols ? Ly::NG : 1;
+    if (lane < ng) {
+      int a = 0, rem = lane;
+#pragma unroll
+      for (int aa = 0; aa < D1; ++aa) if (a == aa && rem >= D1 - aa) { rem -= D1 - aa; a = aa + 1; }
+      const int b = a + rem;
+      double g = (lane == 0) ? red[Ly::R_VAL] : red[Ly::R_G + lane - 1];
+      for (int r = 0; r < nf; ++r) g = fma(U[Ly::U_YFV + r * D1 + a], U[Ly::U_YFV + r * D1 + b], g);
+      U[Ly::U_G + a * D1 + b] = g;
+      U[Ly::U_G + b * D1 + a] = g;
+    }
+    const int nm = all_cols ? D1 : 1;
+    if (lane >= 48 && lane < 48 + nm) {
+      const int c = lane - 48;
+      double mu = (c == 0) ? red[Ly::R_VAL + 1] : red[Ly::R_MF + c - 1];
+      for (int r = 0; r < nf; ++r) mu = fma(U[Ly::U_CF + (S + 1) * FMAX + r], B[(NR + r) * BS + c], mu);
+      if (c == 0) U[Ly::U_SC + SC_MU] = mu; else U[Ly::U_GMU + c - 1] = mu;
+    }
+  }
+  wave_sync();
+
+  // ---- σ, EI partials (all lanes, wave-uniform values)
+  const double mu = U[Ly::U_SC + SC_MU];
+  const double g00 = U[Ly::U_G];
+  const double var = kp.psi0 - g00;
+  const double sig = sqrt(var);
+  const double fmin = U[Ly::U_FMIN + S + 1];
+  const EIp e = ei_partials(mu, sig, kp.theta, fmin, kp.sigma_tol);
+  if (lane == 0) {
+    U[Ly::U_SC + SC_SIG] = sig;
+    U[Ly::U_SC + SC_VAR] = var;
+    U[Ly::U_SC + SC_ALPHA] = e.g;
+    U[Ly::U_SC + SC_GMU] = e.gmu;
+    U[Ly::U_SC + SC_GSIG] = e.gsig;
+    U[Ly::U_SC + SC_GMUMU] = e.gmumu;
+    U[Ly::U_SC + SC_GSIGSIG] = e.gsigsig;
+    U[Ly::U_SC + SC_GMUTH] = e.gmuth;
+    U[Ly::U_SC + SC_GSIGTH] = e.gsigth;
+    U[Ly::U_SC + SC_FMIN] = fmin;
+  }
+  if (mode == EV_VALUE) { wave_sync(); return; }
+  if (lane < D) {
+    const double gs = -U[Ly::U_G + (1 + lane) * D1] / sig;       // ∇σ = -(∇kx·w)/σ
+    const double gm = U[Ly::U_GMU + lane];
+    U[Ly::U_GSIG + lane] = gs;
+    U[Ly::U_GAL + lane] = e.gmu * gm + e.gsig * gs;                // ∇αx :567
+    U[Ly::U_MIX + lane] = gm * e.gmuth + gs * e.gsigth;            // d2α_dxdθ :575-577
+  }
+
+  // ---- 5. backward product w = L⁻ᵀ v (and P = L⁻ᵀ V for the adjoint)
+  // stash Y rows (base) into B, then lane i walks column i of L0⁻¹
+  const bool rich = (mode == EV_RICH);
+#pragma unroll
+  for (int s = 0; s < RPL; ++s) {
+    double* row = B + (lane + WAVE * s) * BS;
+    row[0] = acc[s][0];
+    if (rich) {
+#pragma unroll
+      for (int a = 0; a < D; ++a) row[1 + a] = acc[s][1 + a];
+    }
+  }
+  wave_sync();
+  {
+    double wv[RPL], pv[RPL][D];
+#pragma unroll
+    for (int s = 0; s < RPL; ++s) {
+      wv[s] = 0.0;
+#pragma unroll
+      for (int a = 0; a < D; ++a) pv[s][a] = 0.0;
+    }
+    // lane i walks column i of L0⁻¹ in a wave-uniform k loop: Y[k] is an LDS broadcast and the
+    // packed-column addresses colstart(i)+k-i form a bank permutation (Npad ≡ 0 mod 32)
+    const double* colp[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; ++s) colp[s] = W.Linv + linv_colstart(lane + WAVE * s, W.Npad) - (lane + WAVE * s);
+    if (rich) {
+      for (int k = 0; k < N; ++k) {
+        const double* yk = B + k * BS;
+        double yv[D1];
+#pragma unroll
+        for (int c = 0; c < D1; ++c) yv[c] = yk[c];
+#pragma unroll
+        for (int s = 0; s < RPL; ++s) {
+          const int i = lane + WAVE * s;
+          const double l = (k >= i && W.valid[s]) ? colp[s][k] : 0.0;
+          wv[s] = fma(l, yv[0], wv[s]);
+#pragma unroll
+          for (int a = 0; a < D; ++a) pv[s][a] = fma(l, yv[1 + a], pv[s][a]);
+        }
+      }
+    } else {
+      for (int k = 0; k < N; ++k) {
+        const double y0 = B[k * BS];
+#pragma unroll
+        for (int s = 0; s < RPL; ++s) {
+          const int i = lane + WAVE * s;
+          const double l = (k >= i && W.valid[s]) ? colp[s][k] : 0.0;
+          wv[s] = fma(l, y0, wv[s]);
+        }
+      }
+    }
+    // fantasy part: + Σ_r E[r][i] Yf[r]
+#pragma unroll
+    for (int s = 0; s < RPL; ++s) {
+#pragma unroll
+      for (int r = 0; r < FMAX; ++r) {
+        if (r >= nf) break;
+        const double er = Ev[s][r];
+        wv[s] = fma(er, U[Ly::U_YFV + r * D1], wv[s]);
+        if (rich) {
+#pragma unroll
+          for (int a = 0; a < D; ++a) pv[s][a] = fma(er, U[Ly::U_YFV + r * D1 + 1 + a], pv[s][a]);
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < RPL; ++s) {
+      lr.w[s] = wv[s];
+#pragma unroll
+      for (int a = 0; a < D; ++a) lr.P[s][a] = pv[s][a];
+    }
+  }
+  // w_f[q] = Σ_{r ≥ q} Dinv[r][q] Yf[r][0]  (and P_f)
+  {
+    const int ncol = rich ? D1 : 1;
+    if (lane < nf * ncol) {
+      const int q = lane / ncol, c = lane % ncol;
+      double t = 0.0;
+      for (int r = q; r < nf; ++r) t = fma(U[Ly::U_DINV + r * FMAX + q], U[Ly::U_YFV + r * D1 + c], t);
+      if (c == 0) U[Ly::U_WF + q] = t; else U[Ly::U_PF + q * D + c - 1] = t;
+    }
+  }
+  if (mode == EV_DRAW) { wave_sync(); return; }
+
+  // ---- 6. Hessian  Hα = gμμ∇μ∇μ' + gσσ∇σ∇σ' − (gσ/σ)(∇σ∇σ' + ∇kx·Dw) + Σ_j coef_j Hk_j
+  const double gsig_over = (e.gsig == 0.0) ? 0.0 : e.gsig / sig;
+  {
+    double nv[RPL][D], ca[RPL], tb[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; ++s) {
+      double r[D], rho2 = 0.0;
+#pragma unroll
+      for (int a = 0; a < D; ++a) { r[a] = x[a] - W.X0[s][a]; rho2 = fma(r[a], r[a], rho2); }
+      const double rho = sqrt(rho2);
+      const double coef = W.valid[s] ? (e.gmu * lr.cb[s] - gsig_over * lr.w[s]) : 0.0;
+      if (rho > 0.0) {
+        double dpsi, d2psi;
+        rad_psi12(W.rad, rho, dpsi, d2psi);
+        const double Dpr = dpsi / rho;
+        ca[s] = coef * (d2psi - Dpr);
+        tb[s] = coef * Dpr;
+#pragma unroll
+        for (int a = 0; a < D; ++a) nv[s][a] = r[a] / rho;
+      } else {
+        ca[s] = 0.0;
+        tb[s] = coef * kp.d2psi0;
+#pragma unroll
+        for (int a = 0; a < D; ++a) nv[s][a] = 0.0;
+      }
+    }
+    wave_sync();  // previous users of red are done (all lanes passed phase 4)
+#pragma unroll
+    for (int ch = 0; ch < Ly::NHC; ++ch) {
+      double vv[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int t = 16 * ch + q;
+        double s_ = 0.0;
+        if (t < Ly::NH) {
+          int a = 0, rem = t;
+#pragma unroll
+          for (int aa = 0; aa < D; ++aa) if (a == aa && rem >= D - aa) { rem -= D - aa; a = aa + 1; }
+          const int b = a + rem;
+#pragma unroll
+          for (int s = 0; s < RPL; ++s) s_ = fma(ca[s], nv[s][a] * nv[s][b], s_);
+        } else if (t == Ly::NH) {
+#pragma unroll
+          for (int s = 0; s < RPL; ++s) s_ += tb[s];
+        }
+        vv[q] = s_;
+      }
+      wave_reduce<16>(vv, red + 16 * ch, lane);
+    }
+  }
+  wave_sync();
+  if (lane < Ly::NH) {
+    int a = 0, rem = lane;
+#pragma unroll
+    for (int aa = 0; aa < D; ++aa) if (a == aa && rem >= D - aa) { rem -= D - aa; a = aa + 1; }
+    const int b = a + rem;
+    const double gma = U[Ly::U_GMU + a], gmb = U[Ly::U_GMU + b];
+    const double gsa = U[Ly::U_GSIG + a], gsb = U[Ly::U_GSIG + b];
+    double hv = red[lane] + ((a == b) ? red[Ly::NH] : 0.0);
+    // fantasy data points
+    for (int r = 0; r < nf; ++r) {
+      double rr[D], rho2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) { rr[k] = x[k] - U[Ly::U_XF + r * D + k]; rho2 = fma(rr[k], rr[k], rho2); }
+      const double rho = sqrt(rho2);
+      const double coef = e.gmu * U[Ly::U_CF + (S + 1) * FMAX + r] - gsig_over * U[Ly::U_WF + r];
+      if (rho > 0.0) {
+        double dpsi, d2psi;
+        rad_psi12(W.rad, rho, dpsi, d2psi);
+        const double Dpr = dpsi / rho;
+        hv = fma(coef * (d2psi - Dpr), (rr[a] / rho) * (rr[b] / rho), hv);
+        if (a == b) hv = fma(coef, Dpr, hv);
+      } else if (a == b) {
+        hv = fma(coef, kp.d2psi0, hv);
+      }
+    }
+    hv += e.gmumu * gma * gmb + e.gsigsig * gsa * gsb - gsig_over * (gsa * gsb + U[Ly::U_G + (1 + a) * D1 + 1 + b]);
+    U[Ly::U_H + a * D + b] = hv;
+    U[Ly::U_H + b * D + a] = hv;
+  }
+  wave_sync();
+}
+
+// ================================================================================
+// condition!(fs, x, y) -- radial_basis_surrogates.jl:431-441, after an EV_DRAW eval at x
+// on surface S = nf-1.  Appends the inverse-factor row and the new coefficient vector.
+// ================================================================================
+template <int D, int RPL>
+__device__ int condition(WaveCtx<D, RPL>& W, const KParams& kp, int S, double yv, const double* gy,
+                         const LaneRes<D, RPL>& lr) {
+  using Ly = Lay<D, RPL>;
+  constexpr int NR = Ly::NR;
+  double* U = W.U;
+  const int lane = W.lane;
+  const int nf = S + 1;   // index of the new fantasy row
+  const double g00 = U[Ly::U_G];
+  const double mu = U[Ly::U_SC + SC_MU];
+  const double l22sq = kp.psi0 + kp.sn2 - g00;   // C - L21·L21 (update_cholesky! :405-418)
+  if (!(l22sq > 0.0)) return 4;                  // PosDefException
+  const double inv = 1.0 / sqrt(l22sq);
+  const double gam = (yv - mu) / l22sq;          // c_new = [c - γ w; γ]
+#pragma unroll
+  for (int s = 0; s < RPL; ++s) {
+    const int i = lane + WAVE * s;
+    W.E[(long long)nf * NR + i] = W.valid[s] ? -lr.w[s] * inv : 0.0;
+    W.C[(long long)(S + 2) * NR + i] = W.valid[s] ? (lr.cb[s] - gam * lr.w[s]) : 0.0;
+  }
+  wave_sync();
+  if (lane < nf) {
+    const double wq = U[Ly::U_WF + lane];
+    U[Ly::U_DINV + nf * FMAX + lane] = -wq * inv;
+    U[Ly::U_CF + (S + 2) * FMAX + lane] = U[Ly::U_CF + (S + 1) * FMAX + lane] - gam * wq;
+  }
+  if (lane == nf) {
+    U[Ly::U_DINV + nf * FMAX + nf] = inv;
+    U[Ly::U_CF + (S + 2) * FMAX + nf] = gam;
+    U[Ly::U_YF + nf] = yv;
+    const double fm = U[Ly::U_FMIN + S + 1];
+    U[Ly::U_FMIN + S + 2] = (yv < fm) ? yv : fm;
+  }
+  if (lane < D) {
+    U[Ly::U_XF + nf * D + lane] = U[Ly::U_X + lane];
+    U[Ly::U_GF + nf * D + lane] = gy[lane];
+  }
+  wave_sync();
+  return 0;
+}
+
+// gp_draw with gradient (r_b_s.jl:588-611): [y;∇y] = [μ;∇μ] + chol(Dk(0) − G)·z.
+// Every lane computes the (d+1)² Cholesky redundantly (wave-uniform registers).
+template <int D, int RPL>
+__device__ int draw(WaveCtx<D, RPL>& W, const KParams& kp, const double* z, double& yv, double* gy) {
+  using Ly = Lay<D, RPL>;
+  constexpr int D1 = Ly::D1;
+  const double* U = W.U;
+  double Lc[D1 * (D1 + 1) / 2];
+#define TRI(i, j) ((i) * ((i) + 1) / 2 + (j))
+#pragma unroll
+  for (int j = 0; j < D1; ++j) {
+    // Symmetric(σx) uses the upper triangle: σx[j][i] for i ≥ j
+    const double kjj = (j == 0) ? kp.psi0 : -kp.d2psi0;
+    double sdiag = kjj - U[Ly::U_G + j * D1 + j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) sdiag -= Lc[TRI(j, k)] * Lc[TRI(j, k)];
+    if (!(sdiag > 0.0)) return 2;
+    const double ljj = sqrt(sdiag);
+    Lc[TRI(j, j)] = ljj;
+#pragma unroll
+    for (int i = j + 1; i < D1; ++i) {
+      double t = -U[Ly::U_G + j * D1 + i];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t -= Lc[TRI(i, k)] * Lc[TRI(j, k)];
+      Lc[TRI(i, j)] = t / ljj;
+    }
+  }
+  double out[D1];
+  out[0] = U[Ly::U_SC + SC_MU];
+#pragma unroll
+  for (int a = 0; a < D; ++a) out[1 + a] = U[Ly::U_GMU + a];
+#pragma unroll
+  for (int a = 0; a < D1; ++a) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k <= a; ++k) s += Lc[TRI(a, k)] * z[k];
+    out[a] += s;
+  }
+#undef TRI
+  yv = out[0];
+#pragma unroll
+  for (int a = 0; a < D; ++a) gy[a] = out[1 + a];
+  return 0;
+}
+
+// ================================================================================
+// Inner solve: deterministic projected Newton on f = -α, surface S.
+// ================================================================================
+template <int D>
+__device__ __forceinline__ bool chol_packed(double (&A)[D * (D + 1) / 2]) {
+#define TRI(i, j) ((i) * ((i) + 1) / 2 + (j))
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    double s = A[TRI(j, j)];
+#pragma unroll
+    for (int k = 0; k < j; ++k) s -= A[TRI(j, k)] * A[TRI(j, k)];
+    ok = ok && (s > 0.0);
+    const double ljj = sqrt(s);
+    A[TRI(j, j)] = ljj;
+#pragma unroll
+    for (int i = j + 1; i < D; ++i) {
+      double t = A[TRI(i, j)];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t -= A[TRI(i, k)] * A[TRI(j, k)];
+      A[TRI(i, j)] = t / ljj;
+    }
+  }
+#undef TRI
+  return ok;
+}
+
+template <int D, int RPL>
+__device__ void newton(WaveCtx<D, RPL>& W, const KParams& kp, int S, const double* xs, double* xout, double& fout,
+                       long long& nevals, int& st) {
+  using Ly = Lay<D, RPL>;
+  double* U = W.U;
+  const int lane = W.lane;
+  LaneRes<D, RPL> lr;
+  double x[D], g[D];
+  double lb[D], ub[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) { lb[a] = kp.lbs[a]; ub[a] = kp.ubs[a]; x[a] = clampd(xs[a], lb[a], ub[a]); }
+  if (lane < D) U[Ly::U_X + lane] = x[lane];
+  wave_sync();
+  evaluate<D, RPL>(W, kp, S, EV_FULL, lr);
+  ++nevals;
+  if (U[Ly::U_SC + SC_VAR] < 0.0) st |= 1;
+  double f = -U[Ly::U_SC + SC_ALPHA];
+#pragma unroll
+  for (int a = 0; a < D; ++a) g[a] = -U[Ly::U_GAL + a];
+  double box = 0.0;
+#pragma unroll
+  for (int a = 0; a < D; ++a) box = fmax(box, ub[a] - lb[a]);
+  for (int it = 0; it < kp.max_iters; ++it) {
+    if (f != f) break;
+    bool fr[D];
+    double pg = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+      const bool act = (x[a] <= lb[a] && g[a] > 0.0) || (x[a] >= ub[a] && g[a] < 0.0);
+      fr[a] = !act;
+      if (!act) pg = fmax(pg, fabs(g[a]));
+    }
+    if (!(pg > kp.g_tol)) break;
+    // masked reduced Hessian (identity on the active set) -- packed lower
+    double A[D * (D + 1) / 2], H0[D * (D + 1) / 2];
+    {
+      int t = 0;
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) {
+          const double hij = -U[Ly::U_H + i * D + j];
+          H0[t] = (fr[i] && fr[j]) ? hij : ((i == j) ? 1.0 : 0.0);
+          A[t] = H0[t];
+          ++t;
+        }
+    }
+    bool ok = chol_packed<D>(A);
+    if (!ok) {
+      double tau = 0.0, hmax = 0.0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        if (!fr[i]) continue;
+        double off = 0.0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+          if (j == i || !fr[j]) continue;
+          const int ii = i > j ? i : j, jj = i > j ? j : i;
+          off += fabs(H0[ii * (ii + 1) / 2 + jj]);
+        }
+        const double hii = H0[i * (i + 1) / 2 + i];
+        tau = fmax(tau, off - hii);
+        hmax = fmax(hmax, fabs(hii));
+      }
+      tau += 1e-8 * (1.0 + hmax);
+#pragma unroll
+      for (int t = 0; t < D * (D + 1) / 2; ++t) A[t] = H0[t];
+#pragma unroll
+      for (int i = 0; i < D; ++i) if (fr[i]) A[i * (i + 1) / 2 + i] += tau;
+      ok = chol_packed<D>(A);
+    }
+    double p[D];
+    if (ok) {
+      double t1[D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        double s = fr[i] ? g[i] : 0.0;
+#pragma unroll
+        for (int k = 0; k < i; ++k) s -= A[i * (i + 1) / 2 + k] * t1[k];
+        t1[i] = s / A[i * (i + 1) / 2 + i];
+      }
+#pragma unroll
+      for (int i = D - 1; i >= 0; --i) {
+        double s = t1[i];
+#pragma unroll
+        for (int k = i + 1; k < D; ++k) s -= A[k * (k + 1) / 2 + i] * p[k];
+        p[i] = s / A[i * (i + 1) / 2 + i];
+      }
+#pragma unroll
+      for (int i = 0; i < D; ++i) p[i] = fr[i] ? -p[i] : 0.0;
+    } else {
+#pragma unroll
+      for (int i = 0; i < D; ++i) p[i] = fr[i] ? -g[i] : 0.0;
+    }
+    double pn = 0.0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) pn = fmax(pn, fabs(p[i]));
+    if (pn > box) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) p[i] *= box / pn;
+    }
+    // projected backtracking Armijo
+    double t = 1.0, ft = 0.0, xt[D];
+    bool accepted = false;
+    int ls = 0;
+    for (; ls < kp.max_ls; ++ls) {
+      double dec = 0.0;
+#pragma unroll
+      for (int a = 0; a < D; ++a) {
+        xt[a] = clampd(x[a] + t * p[a], lb[a], ub[a]);
+        dec += g[a] * (xt[a] - x[a]);
+      }
+      wave_sync();
+      if (lane < D) U[Ly::U_X + lane] = xt[lane];
+      wave_sync();
+      evaluate<D, RPL>(W, kp, S, ls == 0 ? EV_FULL : EV_VALUE, lr);
+      if (ls == 0) ++nevals;
+      if (U[Ly::U_SC + SC_VAR] < 0.0) st |= 1;
+      ft = -U[Ly::U_SC + SC_ALPHA];
+      if (ft == ft && ft <= f + 1e-4 * dec) { accepted = true; break; }
+      t *= 0.5;
+    }
+    if (!accepted) break;
+    if (ls != 0) {
+      evaluate<D, RPL>(W, kp, S, EV_FULL, lr);
+      ++nevals;
+    }
+    double dx = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) dx = fmax(dx, fabs(xt[a] - x[a]));
+    const double df = fabs(ft - f);
+#pragma unroll
+    for (int a = 0; a < D; ++a) { x[a] = xt[a]; g[a] = -U[Ly::U_GAL + a]; }
+    f = ft;
+    if (dx <= kp.x_tol || df <= kp.f_tol * fabs(f)) break;
+  }
+#pragma unroll
+  for (int a = 0; a < D; ++a) xout[a] = x[a];
+  fout = f;
+  wave_sync();
+}
+
+// multistart_base_solve!(fs, …) rbf_optim.jl:68-101 -> U[U_XB]
+template <int D, int RPL>
+__device__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp, int S, long long& nevals) {
+  using Ly = Lay<D, RPL>;
+  double* U = W.U;
+  int st = 0;
+  int best = -1;
+  bool best_nan = false;
+  double bestf = 0.0, xb[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) xb[a] = 0.0;
+  for (int k = 0; k < kp.nstarts; ++k) {
+    double xs[D], xo[D], fo;
+#pragma unroll
+    for (int a = 0; a < D; ++a) xs[a] = kp.xstarts[(long long)k * D + a];
+    newton<D, RPL>(W, kp, S, xs, xo, fo, nevals, st);
+    bool xnan = false;
+#pragma unroll
+    for (int a = 0; a < D; ++a) xnan = xnan || (xo[a] != xo[a]);
+    if (xnan) continue;
+    if (fo != fo) {
+      if (!best_nan) {
+        best_nan = true;
+#pragma unroll
+        for (int a = 0; a < D; ++a) xb[a] = xo[a];
+      }
+      continue;
+    }
+    if (!best_nan && (best < 0 || fo < bestf)) {
+      best = k;
+      bestf = fo;
+#pragma unroll
+      for (int a = 0; a < D; ++a) xb[a] = xo[a];
+    }
+  }
+  if (st) return st;
+  if (best < 0 && !best_nan) return 8;
+  if (W.lane < D) U[Ly::U_XB + W.lane] = xb[W.lane];
+  wave_sync();
+  return 0;
+}
+
+// ================================================================================
+// Adjoint pair (i, q): perturb fantasy point q (data index N+q) in the surface S=i-1
+// seen from x_i (RICH eval in U/lr).  Lane k < D handles spatial direction e_k and adds
+// dri[:,k]'·x̄_i to ACC[q][k]; lane D handles the data direction δx and adds to ȳ_q.
+// Reference: SpatialPerturbationSurrogate r_b_s.jl:652-694, DataPerturbation :711-757,
+// solve_dual_x rollout.jl:173-186, solve_dual_y :135-145, gather_g :199-215.
+// ================================================================================
+template <int D, int RPL>
+__device__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& kp, int S, int q, int i_pol,
+                             const LaneRes<D, RPL>& lr) {
+  using Ly = Lay<D, RPL>;
+  constexpr int NR = Ly::NR;
+  double* U = W.U;
+  double* red = W.red;
+  const int lane = W.lane;
+  const int nf = S + 1;
+  double Xq[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) Xq[a] = U[Ly::U_XF + q * D + a];
+  // per-lane U_a = ∇k(X_q - X_a) and products  [Uᵀc (D), Uᵀw (D), PᵀU (D×D, m-major)]
+  double u[RPL][D];
+#pragma unroll
+  for (int s = 0; s < RPL; ++s) {
+    double r[D], rho2 = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) { r[a] = Xq[a] - W.X0[s][a]; rho2 = fma(r[a], r[a], rho2); }
+    const double rho = sqrt(rho2);
+    double psi, dpsi;
+    rad_psi(W.rad, rho, psi, dpsi);
+#pragma unroll
+    for (int a = 0; a < D; ++a) u[s][a] = (W.valid[s] && rho > 0.0) ? dpsi * (r[a] / rho) : 0.0;
+  }
+  wave_sync();
+#pragma unroll
+  for (int ch = 0; ch < Ly::NPC; ++ch) {
+    double v[16];
+#pragma unroll
+    for (int qq = 0; qq < 16; ++qq) {
+      const int t = 16 * ch + qq;
+      double s_ = 0.0;
+      if (t < D) {
+#pragma unroll
+        for (int s = 0; s < RPL; ++s) s_ = fma(lr.cb[s], u[s][t], s_);
+      } else if (t < 2 * D) {
+#pragma unroll
+        for (int s = 0; s < RPL; ++s) s_ = fma(lr.w[s], u[s][t - D], s_);
+      } else if (t < Ly::NPAIR) {
+        const int m = (t - 2 * D) / D, k = (t - 2 * D) % D;
+#pragma unroll
+        for (int s = 0; s < RPL; ++s) s_ = fma(lr.P[s][m], u[s][k], s_);
+      }
+      v[qq] = s_;
+    }
+    wave_reduce<16>(v, red + 16 * ch, lane);
+  }
+  wave_sync();
+  if (lane > D) return;
+  // fantasy data points r ≤ S contribute lane-uniformly; recompute their ∇k(X_q − X_r)
+  double uc[D], uw[D], PU[D][D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    uc[k] = red[k];
+    uw[k] = red[D + k];
+#pragma unroll
+    for (int m = 0; m < D; ++m) PU[m][k] = red[2 * D + m * D + k];
+  }
+  for (int r = 0; r < nf; ++r) {
+    double rr[D], rho2 = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) { rr[a] = Xq[a] - U[Ly::U_XF + r * D + a]; rho2 = fma(rr[a], rr[a], rho2); }
+    const double rho = sqrt(rho2);
+    if (!(rho > 0.0)) continue;
+    double psi, dpsi;
+    rad_psi(W.rad, rho, psi, dpsi);
+    const double cr = U[Ly::U_CF + (S + 1) * FMAX + r], wr = U[Ly::U_WF + r];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const double uk = dpsi * (rr[k] / rho);
+      uc[k] = fma(cr, uk, uc[k]);
+      uw[k] = fma(wr, uk, uw[k]);
+#pragma unroll
+      for (int m = 0; m < D; ++m) PU[m][k] = fma(U[Ly::U_PF + r * D + m], uk, PU[m][k]);
+    }
+  }
+  // direction δ: e_lane (spatial) or δx (data, lane D)
+  double dl[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) dl[a] = (lane == D) ? U[Ly::U_DX + a] : ((a == lane) ? 1.0 : 0.0);
+  double udc = 0.0, udw = 0.0, Pu[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) { udc = fma(uc[k], dl[k], udc); udw = fma(uw[k], dl[k], udw); }
+#pragma unroll
+  for (int m = 0; m < D; ++m) {
+    double s_ = 0.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) s_ = fma(PU[m][k], dl[k], s_);
+    Pu[m] = s_;
+  }
+  // δkx_q, δ∇kx_q at x = x_i
+  double rq[D], rho2 = 0.0;
+#pragma unroll
+  for (int a = 0; a < D; ++a) { rq[a] = U[Ly::U_X + a] - Xq[a]; rho2 = fma(rq[a], rq[a], rho2); }
+  const double rho = sqrt(rho2);
+  double dkx = 0.0, dgkx[D];
+  if (rho > 0.0) {
+    double dpsi, d2psi;
+    rad_psi12(W.rad, rho, dpsi, d2psi);
+    const double Dpr = dpsi / rho;
+    double rd = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) { dkx -= dpsi * (rq[a] / rho) * dl[a]; rd += (rq[a] / rho) * dl[a]; }
+#pragma unroll
+    for (int a = 0; a < D; ++a) dgkx[a] = -((d2psi - Dpr) * (rq[a] / rho) * rd + Dpr * dl[a]);
+  } else {
+#pragma unroll
+    for (int a = 0; a < D; ++a) dgkx[a] = -kp.d2psi0 * dl[a];
+  }
+  const double cq = U[Ly::U_CF + (S + 1) * FMAX + q];
+  const double wq = U[Ly::U_WF + q];
+  const double sig = U[Ly::U_SC + SC_SIG];
+  const double gmu = U[Ly::U_SC + SC_GMU], gsig = U[Ly::U_SC + SC_GSIG];
+  const double kxdc = -(wq * udc + udw * cq);
+  const double dmu = dkx * cq + kxdc;
+  const double dsig = wq * (udw - dkx) / sig;
+  double dgm, dgs;
+  ei_first(dmu, dsig, kp.theta, U[Ly::U_SC + SC_FMIN], kp.sigma_tol, dgm, dgs);
+  double contrib = 0.0;
+#pragma unroll
+  for (int a = 0; a < D; ++a) {
+    const double Pqa = U[Ly::U_PF + q * D + a];
+    const double gkdc = -(Pqa * udc + Pu[a] * cq);
+    const double dgmu = dgkx[a] * cq + gkdc;
+    const double gsa = U[Ly::U_GSIG + a];
+    double da = gmu * dgmu + dgm * U[Ly::U_GMU + a] + dgs * gsa;
+    if (lane < D) {
+      const double dgsig = (Pqa * udw + Pu[a] * wq - dgkx[a] * wq - Pqa * dkx - dsig * gsa) / sig;
+      da += gsig * dgsig;
+    }
+    contrib = fma(da, U[Ly::U_XBAR + (i_pol - 1) * D + a], contrib);
+  }
+  if (lane < D) U[Ly::U_ACC + q * D + lane] += contrib;
+  else U[Ly::U_YBAR + q] += contrib;
+}
+
+// small LU with partial pivoting (Julia det / \ on a Matrix), all lanes redundantly.
+template <int D>
+__device__ __forceinline__ bool lu_det_solve(double (&A)[D][D], double* b, double& det, bool do_solve) {
+  int piv[D];
+  bool sing = false;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    int p = k;
+    double mx = fabs(A[k][k]);
+#pragma unroll
+    for (int i = k + 1; i < D; ++i) if (fabs(A[i][k]) > mx) { mx = fabs(A[i][k]); p = i; }
+    piv[k] = p;
+#pragma unroll
+    for (int i = k + 1; i < D; ++i) {
+      if (i == p) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) { const double t = A[k][j]; A[k][j] = A[i][j]; A[i][j] = t; }
+      }
+    }
+    if (A[k][k] == 0.0) { sing = true; continue; }
+#pragma unroll
+    for (int i = k + 1; i < D; ++i) A[i][k] /= A[k][k];
+#pragma unroll
+    for (int j = k + 1; j < D; ++j)
+#pragma unroll
+      for (int i = k + 1; i < D; ++i) A[i][j] -= A[i][k] * A[k][j];
+  }
+  det = 1.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) { det *= A[k][k]; if (piv[k] != k) det = -det; }
+  if (sing) det = 0.0;
+  if (!do_solve || sing) return !sing;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+#pragma unroll
+    for (int i = k + 1; i < D; ++i) {
+      if (i == piv[k]) { const double t = b[k]; b[k] = b[i]; b[i] = t; }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    double s = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) s -= A[i][k] * b[k];
+    b[i] = s;
+  }
+#pragma unroll
+  for (int i = D - 1; i >= 0; --i) {
+    double s = b[i];
+#pragma unroll
+    for (int k = i + 1; k < D; ++k) s -= A[i][k] * b[k];
+    b[i] = s / A[i][i];
+  }
+  return true;
+}
+
+// set U_X to fantasy point j and run a RICH eval on surface j-1
+template <int D, int RPL>
+__device__ __forceinline__ void rich_eval_at(WaveCtx<D, RPL>& W, const KParams& kp, int j, LaneRes<D, RPL>& lr) {
+  using Ly = Lay<D, RPL>;
+  wave_sync();
+  if (W.lane < D) W.U[Ly::U_X + W.lane] = W.U[Ly::U_XF + j * D + W.lane];
+  wave_sync();
+  evaluate<D, RPL>(W, kp, j - 1, EV_RICH, lr);
+}
+
+// ================================================================================
+// One trajectory.
+// ================================================================================
+template <int D, int RPL>
+__device__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp, long long tr) {
+  using Ly = Lay<D, RPL>;
+  constexpr int D1 = Ly::D1, NR = Ly::NR;
+  double* U = W.U;
+  const int lane = W.lane;
+  const int M = kp.M, h = kp.h;
+  const int r = (int)(tr / M), m = (int)(tr % M);
+  long long nevals = 0;
+  int st = 0;
+  LaneRes<D, RPL> lr;
+
+  // surface -1 = the base surrogate; C[0] = c0
+#pragma unroll
+  for (int s = 0; s < RPL; ++s) W.C[lane + WAVE * s] = kp.c0[lane + WAVE * s];
+  if (lane == 0) U[Ly::U_FMIN] = kp.fmin_base;
+  if (lane < D) U[Ly::U_X + lane] = kp.x0s[(long long)r * D + lane];
+  wave_sync();
+
+  for (int k = 0; k <= h; ++k) {
+    const int S = k - 1;
+    if (k > 0) {
+      if (kp.replay) {
+        if (lane < D) U[Ly::U_X + lane] = kp.replay[(long long)lane + D * ((k - 1) + (long long)h * (m + (long long)M * r))];
+        wave_sync();
+      } else {
+        st |= multistart<D, RPL>(W, kp, S, nevals);
+        if (st) break;
+        if (lane < D) U[Ly::U_X + lane] = U[Ly::U_XB + lane];
+        wave_sync();
+      }
+    }
+    if (kp.policy && lane < D) kp.policy[(long long)lane + D * (k + (long long)(h + 1) * (m + (long long)M * r))] = U[Ly::U_X + lane];
+    evaluate<D, RPL>(W, kp, S, EV_DRAW, lr);
+    if (U[Ly::U_SC + SC_VAR] < 0.0) { st |= 1; break; }
+    if (k == 0 && lane < D) U[Ly::U_GMU0 + lane] = U[Ly::U_GMU + lane];
+    double z[D1], yv, gy[D];
+#pragma unroll
+    for (int a = 0; a < D1; ++a) z[a] = kp.rn[(long long)m + (long long)M * a + (long long)M * D1 * k];
+    st |= draw<D, RPL>(W, kp, z, yv, gy);
+    if (st) break;
+    wave_sync();
+    st |= condition<D, RPL>(W, kp, S, yv, gy, lr);
+    if (st) break;
+  }
+  wave_sync();
+  const long long oidx = (long long)m + (long long)M * r;
+  if (kp.obs && lane <= h) kp.obs[oidx * (h + 1) + lane] = st ? NAN : U[Ly::U_YF + lane];
+  if (kp.evals && lane == 0) kp.evals[oidx] = nevals;
+  if (st) {
+    if (lane == 0) { kp.values[oidx] = NAN; kp.status[oidx] = st; if (kp.grad_theta) kp.grad_theta[oidx] = NAN; }
+    if (kp.grad_x && lane < D) kp.grad_x[oidx * D + lane] = NAN;
+    return;
+  }
+  // resolve (observables.jl:12-14, Q3)
+  double bo = U[Ly::U_YF];
+  int t = 0;
+  for (int k = 1; k <= h; ++k) { const double yk = U[Ly::U_YF + k]; if (yk < bo) { bo = yk; t = k; } }
+  const double value = fmax(kp.fmini - bo, 0.0);
+  double gth = 0.0;
+  bool grad_zero = true;
+  if (kp.with_gradient && kp.fmini > bo) {
+    if (t == 0) {
+      grad_zero = false;  // ∇x = -∇y₀ (Q10)
+      if (lane < D) U[Ly::U_ACC + lane] = U[Ly::U_GF + lane];  // reuse ACC[0] as output staging
+      if (lane == 0) U[Ly::U_YBAR] = 0.0;
+      if (lane < D) U[Ly::U_GMU0 + lane] = 0.0;
+      wave_sync();
+    } else {
+      grad_zero = false;
+      // zero adjoint state
+      for (int q = lane; q < FMAX * D; q += WAVE) { U[Ly::U_ACC + q] = 0.0; U[Ly::U_XBAR + q] = 0.0; }
+      if (lane <= FMAX) U[Ly::U_YBAR + lane] = 0.0;
+      wave_sync();
+      if (lane == 0) U[Ly::U_YBAR + t] = 1.0;
+      wave_sync();
+      for (int j = t; j >= 1; --j) {
+        // ---- solve_dual_x(j)
+        rich_eval_at<D, RPL>(W, kp, j, lr);
+        double Hm[D][D], xd[D], det;
+#pragma unroll
+        for (int a = 0; a < D; ++a)
+#pragma unroll
+          for (int b = 0; b < D; ++b) Hm[a][b] = U[Ly::U_H + b * D + a];  // Hα' (symmetric)
+        const double ybj = U[Ly::U_YBAR + j];
+#pragma unroll
+        for (int a = 0; a < D; ++a) xd[a] = -U[Ly::U_GF + (j - 1) * D + a] * ybj - U[Ly::U_ACC + j * D + a];
+        double Hd[D][D];
+#pragma unroll
+        for (int a = 0; a < D; ++a)
+#pragma unroll
+          for (int b = 0; b < D; ++b) Hd[a][b] = Hm[a][b];
+        lu_det_solve<D>(Hd, xd, det, false);
+        bool zero = !(det >= kp.htol);  // det(H) < htol → zeros (Q4); NaN det keeps going in Julia
+        if (det != det) zero = false;
+        if (zero) {
+#pragma unroll
+          for (int a = 0; a < D; ++a) xd[a] = 0.0;
+        } else {
+          double dd;
+          if (!lu_det_solve<D>(Hm, xd, dd, true)) st |= 16;
+        }
+        wave_sync();
+        if (lane < D) U[Ly::U_XBAR + (j - 1) * D + lane] = xd[lane];
+        // gather_q: ∇θ += mixed_jᵀ x̄_j
+        double gq = 0.0;
+#pragma unroll
+        for (int a = 0; a < D; ++a) gq = fma(U[Ly::U_MIX + a], xd[a], gq);
+        gth += gq;
+        // δx of solve_dual_y call j (rollout.jl:133)
+        if (lane < D) {
+          U[Ly::U_DX + lane] = kp.dual_y
+              ? kp.dual_y[(long long)lane + D * ((j - 1) + (long long)h * (m + (long long)M * r))]
+              : dual_uniform(kp.seed, (long long)m + (long long)M * r, j, lane);
+        }
+        wave_sync();
+        // ---- pairs (i, q = j-1), i = j..t  (data part → ȳ_{j-1}; spatial part → ACC[j-1])
+        for (int i = j; i <= t; ++i) {
+          bool xz = true;
+#pragma unroll
+          for (int a = 0; a < D; ++a) xz = xz && (U[Ly::U_XBAR + (i - 1) * D + a] == 0.0);
+          if (xz) continue;
+          if (i != j) rich_eval_at<D, RPL>(W, kp, i, lr);
+          adjoint_pair<D, RPL>(W, kp, i - 1, j - 1, i, lr);
+          wave_sync();
+        }
+      }
+    }
+  }
+  // outputs: ∇x = -(∇μ(x0)·ȳ0 + ACC[0]),  ∇θ = -Σ mixed·x̄
+  wave_sync();
+  const long long base = oidx;
+  if (lane == 0) {
+    kp.values[base] = value;
+    kp.status[base] = st;
+    if (kp.grad_theta) kp.grad_theta[base] = (grad_zero || st) ? (st ? NAN : 0.0) : -gth;
+  }
+  if (kp.grad_x && lane < D) {
+    double gx = 0.0;
+    if (!grad_zero) gx = -(U[Ly::U_GMU0 + lane] * U[Ly::U_YBAR] + U[Ly::U_ACC + lane]);
+    if (st) gx = NAN;
+    kp.grad_x[base * D + lane] = gx;
+  }
+  if (st && lane == 0) kp.values[base] = NAN;
+  wave_sync();
+}
+
+// ================================================================================
+// Kernels
+// ================================================================================
+template <int D, int RPL>
+__device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp, double* smem, int wave_in_block) {
+  using Ly = Lay<D, RPL>;
+  W.lane = threadIdx.x & (WAVE - 1);
+  const long long lin = linv_size(kp.Npad);
+  const long long lin_al = (lin + 1) & ~1LL;
+  double* wbase = smem + lin_al + (long long)wave_in_block * Ly::WAVE_LDS;
+  W.B = wbase;
+  W.red = wbase + Ly::BROWS * Ly::BS;
+  W.U = W.red + Ly::REDN;
+  W.Linv = smem;
+  const long long slot = (long long)blockIdx.x * (blockDim.x / WAVE) + wave_in_block;
+  W.E = kp.work + slot * kp.work_stride;
+  W.C = W.E + (long long)FMAX * Ly::NR;
+  W.N = kp.N;
+  W.Npad = kp.Npad;
+  W.rad.kind = kp.kernel;
+  W.rad.cK = kp.cK;
+#pragma unroll
+  for (int s = 0; s < RPL; ++s) {
+    const int i = W.lane + WAVE * s;
+    W.valid[s] = i < kp.N;
+#pragma unroll
+    for (int a = 0; a < D; ++a) W.X0[s][a] = kp.X0[(long long)a * Ly::NR + i];
+  }
+  // zero this wave's LDS so that padded rows read as zeros
+  for (int q = W.lane; q < Ly::WAVE_LDS; q += WAVE) wbase[q] = 0.0;
+}
+
+template <int D, int RPL>
+__global__ void __launch_bounds__(256) rollout_kernel(KParams kp) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  // stage the packed L0⁻¹ once per workgroup (the only block-wide barrier)
+  const long long lin = linv_size(kp.Npad);
+  for (long long q = threadIdx.x; q < lin; q += blockDim.x) smem[q] = kp.Linv[q];
+  __syncthreads();
+  WaveCtx<D, RPL> W;
+  wave_setup<D, RPL>(W, kp, smem, threadIdx.x / WAVE);
+  wave_sync();
+  for (;;) {
+    long long tr = 0;
+    if (W.lane == 0) tr = atomicAdd(kp.queue, 1);
+    tr = __shfl(tr, 0, WAVE);
+    if (tr >= kp.T) break;
+    trajectory<D, RPL>(W, kp, tr);
+  }
+}
+
+// eval(s, x, θ) on the base surrogate for P points (fixture / primitive parity path)
+template <int D, int RPL>
+__global__ void __launch_bounds__(256) eval_base_kernel(KParams kp) {
+  using Ly = Lay<D, RPL>;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const long long lin = linv_size(kp.Npad);
+  for (long long q = threadIdx.x; q < lin; q += blockDim.x) smem[q] = kp.Linv[q];
+  __syncthreads();
+  WaveCtx<D, RPL> W;
+  wave_setup<D, RPL>(W, kp, smem, threadIdx.x / WAVE);
+  const int lane = W.lane;
+#pragma unroll
+  for (int s = 0; s < RPL; ++s) W.C[lane + WAVE * s] = kp.c0[lane + WAVE * s];
+  if (lane == 0) W.U[Ly::U_FMIN] = kp.fmin_base;
+  wave_sync();
+  LaneRes<D, RPL> lr;
+  const int stride = 3 + 4 * D + D * D;
+  for (;;) {
+    long long p = 0;
+    if (lane == 0) p = atomicAdd(kp.queue, 1);
+    p = __shfl(p, 0, WAVE);
+    if (p >= kp.T) break;
+    if (lane < D) W.U[Ly::U_X + lane] = kp.pts[p * D + lane];
+    wave_sync();
+    evaluate<D, RPL>(W, kp, -1, EV_FULL, lr);
+    double* o = kp.pts_out + p * stride;
+    const double* U = W.U;
+    if (lane == 0) { o[0] = U[Ly::U_SC + SC_MU]; o[1] = U[Ly::U_SC + SC_SIG]; o[2] = U[Ly::U_SC + SC_ALPHA]; }
+    if (lane < D) {
+      o[3 + lane] = U[Ly::U_GMU + lane];
+      o[3 + D + lane] = U[Ly::U_GSIG + lane];
+      o[3 + 2 * D + lane] = U[Ly::U_GAL + lane];
+      o[3 + 3 * D + D * D + lane] = U[Ly::U_MIX + lane];
+    }
+    for (int q = lane; q < D * D; q += WAVE) o[3 + 3 * D + q] = U[Ly::U_H + (q % D) * D + q / D];
+    wave_sync();
+  }
+}
+
+}  // namespace mrbo

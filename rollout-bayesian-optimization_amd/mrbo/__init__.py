@@ -1,0 +1,21 @@
+"""mrbo -- MI355X-native rollout-acquisition evaluator (host mirror of the reference API).
+
+Reference API surface kept (DarianNwankwo/Rollout-Bayesian-Optimization):
+  kernels            Matern52/32/12, SquaredExponential        radial_basis_functions.jl
+  decision rules     EI (compiled), POI/LCB/Random (declared)  decision_rules.jl
+  surrogates         Surrogate, FantasySurrogate               radial_basis_surrogates.jl
+  trajectories       Trajectory, TrajectoryParameters, ExpectedTrajectoryOutput  trajectory.jl
+  rollout            simulate_trajectory_mc                    rollout.jl:279-340
+  outer ascent       StandardSGA, Adam, eswavs, stochastic_solve  optimizers.jl, utils.jl
+Compute runs in libmrbo.so (hand-written HIP for gfx950); see include/mrbo.h.
+"""
+from .decision_rules import EI, LCB, POI, DecisionRule, RandomAcquisition, get_name
+from .kernels import Matern12, Matern32, Matern52, SquaredExponential, eval_KxX, eval_KXX
+from .optimizers import Adam, StandardSGA, update
+from .rollout import simulate_trajectory_mc, simulate_trajectory_mc_batch
+from .surrogates import DEFAULT_CAPACITY, GROUND_TRUTH_OBSERVATIONS, FantasySurrogate, Surrogate
+from .trajectory import ExpectedTrajectoryOutput, Trajectory, TrajectoryParameters, gen_low_discrepancy_sequence
+from .utils import (ExperimentSetup, eswavs, generate_batch, generate_initial_guesses, kronecker_quasirand,
+                    stochastic_solve, stochastic_solve_batch)
+
+__version__ = "0.1.0"

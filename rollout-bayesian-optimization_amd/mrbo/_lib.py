@@ -1,0 +1,87 @@
+"""ctypes binding of libmrbo.so (include/mrbo.h) -- the product's only compute path.
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc --offload-arch=gfx950).
+There is no CPU fallback: importing a compute entry point without the library, or calling
+one without a GPU, raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmrbo.so")
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_vp = ctypes.c_void_p
+
+MRBO_FLAG_HOST_POINTERS = 1
+MRBO_FLAG_NO_GRADIENT = 2
+
+STATUS_BITS = {
+    1: "DomainError: sqrt of a negative posterior variance (radial_basis_surrogates.jl:528)",
+    2: "PosDefException: gp_draw covariance (radial_basis_surrogates.jl:537)",
+    4: "PosDefException: update_cholesky! (radial_basis_surrogates.jl:412)",
+    8: "ArgumentError: findmin over an empty candidate list (rbf_optim.jl:96-97)",
+    16: "SingularException: solve_dual_x Hessian (rollout.jl:188)",
+}
+
+# exported symbols of include/mrbo.h (the library must export all of them)
+EXPORTS = [
+    "mrbo_version", "mrbo_last_error", "mrbo_device_count", "mrbo_plan_create", "mrbo_plan_destroy",
+    "mrbo_simulate_mc", "mrbo_eto_reduce", "mrbo_partial_sums", "mrbo_eval_base", "mrbo_rnstream",
+    "mrbo_initial_guesses", "mrbo_dual_uniform", "mrbo_last_kernel_ms",
+]
+
+
+class SurrogateDesc(ctypes.Structure):
+    _fields_ = [("d", ctypes.c_int32), ("N", ctypes.c_int32), ("kernel", ctypes.c_int32),
+                ("lengthscale", ctypes.c_double), ("sigma_n2", ctypes.c_double), ("fmini", ctypes.c_double),
+                ("X", _dp), ("L", _dp), ("ldL", ctypes.c_int32), ("c", _dp), ("y", _dp)]
+
+
+class ParamsDesc(ctypes.Structure):
+    _fields_ = [("h", ctypes.c_int32), ("M", ctypes.c_int32), ("R", ctypes.c_int32), ("nstarts", ctypes.c_int32),
+                ("rule", ctypes.c_int32), ("theta", ctypes.c_double), ("lbs", _dp), ("ubs", _dp),
+                ("max_iters", ctypes.c_int32), ("max_ls", ctypes.c_int32), ("x_tol", ctypes.c_double),
+                ("f_tol", ctypes.c_double), ("g_tol", ctypes.c_double), ("htol", ctypes.c_double),
+                ("sigma_tol", ctypes.c_double), ("seed", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+class MrboError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libmrbo.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MrboError(f"libmrbo.so not built at {LIB_PATH}: run __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    L.mrbo_version.restype = ctypes.c_char_p
+    L.mrbo_last_error.restype = ctypes.c_char_p
+    L.mrbo_device_count.restype = ctypes.c_int
+    L.mrbo_plan_create.argtypes = [ctypes.POINTER(SurrogateDesc), ctypes.POINTER(ParamsDesc), ctypes.c_int32,
+                                   ctypes.POINTER(_vp)]
+    L.mrbo_plan_destroy.argtypes = [_vp]
+    L.mrbo_simulate_mc.argtypes = [_vp] + [_vp] * 12 + [ctypes.c_uint32, _vp]
+    L.mrbo_eto_reduce.argtypes = [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]
+    L.mrbo_partial_sums.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_int32, _vp, ctypes.c_uint32, _vp]
+    L.mrbo_eval_base.argtypes = [_vp, ctypes.c_int32, _vp, _vp, ctypes.c_uint32, _vp]
+    L.mrbo_rnstream.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _dp]
+    L.mrbo_initial_guesses.argtypes = [ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp]
+    L.mrbo_dual_uniform.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]
+    L.mrbo_dual_uniform.restype = ctypes.c_double
+    L.mrbo_last_kernel_ms.argtypes = [_vp]
+    L.mrbo_last_kernel_ms.restype = ctypes.c_double
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise MrboError(f"mrbo error {rc}: {load().mrbo_last_error().decode()}")
+    return rc

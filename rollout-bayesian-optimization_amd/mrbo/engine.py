@@ -1,0 +1,165 @@
+"""RolloutPlan -- owns one libmrbo plan (device copy of the base surrogate + workspace) and
+launches the rollout kernel on device-resident torch tensors.
+
+torch is plumbing here (device memory, streams, torch.distributed); every arithmetic step of
+the rollout path runs in libmrbo.so.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+DEFAULTS = dict(max_iters=50, max_ls=20, x_tol=1e-3, f_tol=1e-3, g_tol=1e-8, htol=1e-4, sigma_tol=1e-8, seed=1906)
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise _lib.MrboError("libmrbo requires a ROCm GPU (torch.cuda.is_available() is False); there is no CPU path")
+    return torch
+
+
+def _f64(a):
+    return np.asfortranarray(np.asarray(a, dtype=np.float64))
+
+
+def to_device(a, device):
+    """numpy (any order) -> flat column-major float64 device tensor"""
+    torch = _torch()
+    flat = np.asarray(a, dtype=np.float64).ravel(order="F").copy()
+    return torch.from_numpy(flat).to(device)
+
+
+def from_device(t, shape):
+    return t.detach().cpu().numpy().reshape(shape, order="F")
+
+
+class RolloutPlan:
+    """Device state for (surrogate, trajectory parameters)."""
+
+    def __init__(self, X, L, c, y, kernel, lengthscale, sigma_n2, fmini, h, M, R, nstarts, lbs, ubs, theta,
+                 device=0, **opts):
+        self.lib = _lib.load()
+        o = dict(DEFAULTS)
+        o.update(opts)
+        self.opts = o
+        self._X, self._L, self._c, self._y = _f64(X), _f64(L), _f64(c), _f64(y)
+        self.d, self.N = self._X.shape
+        self.h, self.M, self.R, self.nstarts = int(h), int(M), int(R), int(nstarts)
+        self._lbs, self._ubs = _f64(lbs).ravel(), _f64(ubs).ravel()
+        self.theta = float(theta)
+        self.device = device
+        dp = ctypes.POINTER(ctypes.c_double)
+        sd = _lib.SurrogateDesc(self.d, self.N, int(kernel), float(lengthscale), float(sigma_n2), float(fmini),
+                                self._X.ctypes.data_as(dp), self._L.ctypes.data_as(dp), self.N,
+                                self._c.ctypes.data_as(dp), self._y.ctypes.data_as(dp))
+        pd = _lib.ParamsDesc(self.h, self.M, self.R, self.nstarts, 0, self.theta, self._lbs.ctypes.data_as(dp),
+                             self._ubs.ctypes.data_as(dp), int(o["max_iters"]), int(o["max_ls"]), float(o["x_tol"]),
+                             float(o["f_tol"]), float(o["g_tol"]), float(o["htol"]), float(o["sigma_tol"]),
+                             int(o["seed"]))
+        h_ = ctypes.c_void_p()
+        _lib.check(self.lib.mrbo_plan_create(ctypes.byref(sd), ctypes.byref(pd), int(device), ctypes.byref(h_)))
+        self.handle = h_
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.mrbo_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------------------------
+    def alloc_outputs(self, with_gradient=True, want_policy=False, want_obs=False, want_evals=True):
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        T = self.M * self.R
+        out = dict(values=torch.empty(T, dtype=torch.float64, device=dev),
+                   status=torch.empty(T, dtype=torch.int32, device=dev))
+        if with_gradient:
+            out["grad_x"] = torch.empty(self.d * T, dtype=torch.float64, device=dev)
+            out["grad_theta"] = torch.empty(T, dtype=torch.float64, device=dev)
+        if want_policy:
+            out["policy_x"] = torch.empty(self.d * (self.h + 1) * T, dtype=torch.float64, device=dev)
+        if want_obs:
+            out["obs"] = torch.empty((self.h + 1) * T, dtype=torch.float64, device=dev)
+        if want_evals:
+            out["evals"] = torch.empty(T, dtype=torch.int64, device=dev)
+        return out
+
+    def simulate(self, x0s, rnstream, xstarts, out, dual_y_dx=None, replay_x=None, stream=None):
+        """Launch mrbo_simulate_mc on device tensors (flat, column-major)."""
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        flags = 0 if "grad_x" in out else _lib.MRBO_FLAG_NO_GRADIENT
+        _lib.check(self.lib.mrbo_simulate_mc(
+            self.handle, p(x0s), p(rnstream), p(xstarts), p(dual_y_dx), p(replay_x), p(out["values"]),
+            p(out.get("grad_x")), p(out.get("grad_theta")), p(out["status"]), p(out.get("policy_x")),
+            p(out.get("obs")), p(out.get("evals")), flags, ctypes.c_void_p(st.cuda_stream)))
+        return out
+
+    def eto(self, out, stream=None):
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        W = 2 + 2 * self.d + 2
+        e = torch.empty(W * self.R, dtype=torch.float64, device=f"cuda:{self.device}")
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        _lib.check(self.lib.mrbo_eto_reduce(self.handle, p(out["values"]), p(out.get("grad_x")),
+                                            p(out.get("grad_theta")), p(e), 0, ctypes.c_void_p(st.cuda_stream)))
+        return e
+
+    def partial_sums(self, out, M_local, stream=None):
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        W = 2 + 2 * self.d + 2
+        e = torch.empty(W * self.R, dtype=torch.float64, device=f"cuda:{self.device}")
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        _lib.check(self.lib.mrbo_partial_sums(self.handle, p(out["values"]), p(out.get("grad_x")),
+                                              p(out.get("grad_theta")), int(M_local), p(e), 0,
+                                              ctypes.c_void_p(st.cuda_stream)))
+        return e
+
+    def eval_base(self, xs):
+        """eval(s, x, θ) at the columns of xs (d×P); returns (3+4d+d²)×P numpy."""
+        torch = _torch()
+        xs = _f64(xs)
+        d, P = xs.shape
+        stride = 3 + 4 * d + d * d
+        dx = to_device(xs, f"cuda:{self.device}")
+        do = torch.empty(stride * P, dtype=torch.float64, device=f"cuda:{self.device}")
+        st = torch.cuda.current_stream(self.device)
+        _lib.check(self.lib.mrbo_eval_base(self.handle, P, ctypes.c_void_p(dx.data_ptr()),
+                                           ctypes.c_void_p(do.data_ptr()), 0, ctypes.c_void_p(st.cuda_stream)))
+        torch.cuda.synchronize(self.device)
+        return from_device(do, (stride, P))
+
+    def last_kernel_ms(self):
+        return self.lib.mrbo_last_kernel_ms(self.handle)
+
+
+def rnstream(M, d, H):
+    """gen_low_discrepancy_sequence (utils.jl:65-74) via the library's host Sobol."""
+    lib = _lib.load()
+    out = np.zeros((M, d + 1, H), order="F")
+    _lib.check(lib.mrbo_rnstream(int(M), int(d), int(H), out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+    return out
+
+
+def initial_guesses(n, lbs, ubs):
+    lib = _lib.load()
+    lbs, ubs = _f64(lbs).ravel(), _f64(ubs).ravel()
+    d = lbs.size
+    out = np.zeros((d, n + 2), order="F")
+    dp = ctypes.POINTER(ctypes.c_double)
+    _lib.check(lib.mrbo_initial_guesses(int(n), d, lbs.ctypes.data_as(dp), ubs.ctypes.data_as(dp),
+                                        out.ctypes.data_as(dp)))
+    return out
+
+
+def dual_uniform(seed, traj, j, k):
+    return _lib.load().mrbo_dual_uniform(int(seed), int(traj), int(j), int(k))

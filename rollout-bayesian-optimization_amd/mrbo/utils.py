@@ -1,0 +1,109 @@
+"""Outer stochastic-gradient ascent and helpers -- mirror of utils.jl / low_discrepancy.jl."""
+import numpy as np
+
+from .engine import initial_guesses as _initial_guesses
+from .trajectory import gen_low_discrepancy_sequence  # noqa: F401  (re-export, utils.jl:65-74)
+
+
+def kronecker_quasirand(d, N, start=0):
+    """low_discrepancy.jl:7-28"""
+    ϕ = 1.0 + 1.0 / d
+    for _ in range(10):
+        g = ϕ ** (d + 1) - ϕ - 1
+        dg = (d + 1) * ϕ ** d - 1
+        ϕ -= g / dg
+    αs = np.array([np.mod(1.0 / ϕ ** j, 1.0) for j in range(1, d + 1)])
+    Z = np.zeros((d, N))
+    for j in range(1, N + 1):
+        Z[:, j - 1] = np.mod(0.5 + (start + j) * αs, 1.0)
+    return Z
+
+
+def generate_initial_guesses(N, lbs, ubs):
+    """utils.jl:145-153: N Sobol points in [lbs, ubs] plus lbs+1e-6 and ubs-1e-6."""
+    return _initial_guesses(N, lbs, ubs)
+
+
+def generate_batch(N, lbs, ubs, ϵinterior=1e-2):
+    """utils.jl:97-106"""
+    B = _initial_guesses(N, lbs, ubs)
+    B[:, N] = np.asarray(lbs, dtype=np.float64) + ϵinterior
+    B[:, N + 1] = np.asarray(ubs, dtype=np.float64) - ϵinterior
+    return B
+
+
+def early_stopping_without_a_validation_set(grad_f, var_grad_f, sample_size):
+    """utils.jl:114-123 (Mahsereci et al.); NaN ratios keep iterating, as in Julia."""
+    grad_f = np.asarray(grad_f, dtype=np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ratio = np.sum((grad_f ** 2) / np.asarray(var_grad_f, dtype=np.float64))
+    return bool((1.0 - (sample_size / grad_f.size) * ratio) > 0.0)
+
+
+eswavs = early_stopping_without_a_validation_set
+
+
+class ExperimentSetup:
+    """utils.jl:174-208"""
+
+    def __init__(self, tp, number_of_starts):
+        lbs, ubs = tp.get_spatial_bounds()
+        self.tp = tp
+        self.inner_solve_xstarts = generate_initial_guesses(number_of_starts, lbs, ubs)
+        self.resolutions = np.zeros(tp.mc_iters)
+        self.spatial_gradients_container = np.zeros((tp.x0.size, tp.mc_iters))
+        self.hyperparameter_gradients_container = np.zeros((tp.θ.size, tp.mc_iters))
+
+    def get_container(self, symbol):
+        return {"f": self.resolutions, "grad_f": self.spatial_gradients_container,
+                "grad_hypers": self.hyperparameter_gradients_container}[symbol]
+
+    def get_starts(self):
+        return self.inner_solve_xstarts
+
+
+def gap(initial_best, observed_best, actual_best):
+    """utils.jl:126-128"""
+    return (initial_best - observed_best) / (initial_best - actual_best)
+
+
+def simple_regret(actual_minimum, observation):
+    """utils.jl:143"""
+    return observation - actual_minimum
+
+
+def stochastic_solve(optimizer, surrogate, tp, es, start, T=None, iterations=50, device=0, **opts):
+    """utils.jl:235-265 for one start (the intended callee simulate_trajectory_mc)."""
+    x, _ = stochastic_solve_batch([optimizer], surrogate, tp, es, np.asarray(start, dtype=np.float64).reshape(-1, 1),
+                                  T=T, iterations=iterations, device=device, **opts)
+    return x[:, 0]
+
+
+def stochastic_solve_batch(optimizers, surrogate, tp, es, starts, T=None, iterations=50, device=0, **opts):
+    """R restarts of the outer ascent at once: one batched rollout launch per SGA iteration;
+    each restart keeps its own optimizer state and eswavs stop flag."""
+    from .rollout import simulate_trajectory_mc_batch
+    from .surrogates import FantasySurrogate
+    from .trajectory import Trajectory
+    x = np.array(starts, dtype=np.float64)
+    d, R = x.shape
+    if T is None:
+        T = Trajectory(surrogate, FantasySurrogate(surrogate, tp.horizon), start=x[:, 0], hypers=tp.θ,
+                       horizon=tp.horizon)
+    active = np.ones(R, dtype=bool)
+    history = []
+    for _ in range(iterations):
+        if not active.any():
+            break
+        br = simulate_trajectory_mc_batch(T, tp, x, es.get_starts(), device=device, **opts)
+        etos = br.etos()
+        history.append(etos)
+        for r in range(R):
+            if not active[r]:
+                continue
+            e = etos[r]
+            if eswavs(e.gradient(), e.std_gradient() ** 2, tp.mc_iters):
+                active[r] = False
+                continue
+            optimizers[r].update(x[:, r], e.gradient())
+    return x, history
