@@ -99,6 +99,8 @@ typedef struct {
   double htol;          /* solve_dual_x det threshold (rollout.jl:156) = 1e-4    */
   double sigma_tol;     /* EI σtol (decision_rules.jl:84) = 1e-8                 */
   uint64_t seed;        /* δx for solve_dual_y (rollout.jl:133) when dual_y_dx == NULL */
+  int32_t sample_offset;/* global index of this plan's first MC sample (multi-GPU shard), 0 */
+  int32_t samples_total;/* global MC samples per restart (0 → M); keys the δx counter RNG  */
 } mrbo_params_t;
 
 typedef struct mrbo_plan mrbo_plan_t;
@@ -124,7 +126,8 @@ int mrbo_plan_destroy(mrbo_plan_t* plan);
  *   status     M×R          MRBO_ST_* bits
  *   policy_x   d×(h+1)×M×R or NULL: x_0..x_h of every trajectory (fs.X[:, N+1:N+h+1])
  *   obs        (h+1)×M×R or NULL:   sampled observations y_0..y_h
- *   evals      M×R or NULL:         full surrogate evaluations spent in the inner solves
+ *   evals      4×M×R or NULL: per trajectory [full evals, value-only evals, adjoint rich evals,
+ *              adjoint perturbation pairs] -- the work counters of the FLOP roofline model
  * Launches on `stream` (hipStream_t, may be NULL) and returns without synchronising.       */
 int mrbo_simulate_mc(mrbo_plan_t* plan, const double* x0s, const double* rnstream, const double* xstarts,
                      const double* dual_y_dx, const double* replay_x, double* values, double* grad_x,

@@ -34,6 +34,7 @@ class Params(ctypes.Structure):
                 ("max_iters", ctypes.c_int32), ("max_ls", ctypes.c_int32),
                 ("x_tol", ctypes.c_double), ("f_tol", ctypes.c_double), ("g_tol", ctypes.c_double),
                 ("htol", ctypes.c_double), ("sigma_tol", ctypes.c_double), ("seed", ctypes.c_uint64),
+                ("sample_offset", ctypes.c_int32), ("samples_total", ctypes.c_int32),
                 ("with_gradient", ctypes.c_int32), ("nthreads", ctypes.c_int32)]
 
 
@@ -126,7 +127,8 @@ def eval_base(osur, xs, theta=0.0, sigma_tol=1e-8):
 
 def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=None, replay_x=None,
                 max_iters=50, max_ls=20, x_tol=1e-3, f_tol=1e-3, g_tol=1e-8, htol=1e-4, sigma_tol=1e-8,
-                seed=1906, with_gradient=True, nthreads=0, want_policy=True):
+                seed=1906, with_gradient=True, nthreads=0, want_policy=True, sample_offset=0,
+                samples_total=0):
     """Run the oracle's simulate_trajectory_mc for every restart column of x0s (d×R)."""
     x0s, rnstream, xstarts = _f64(x0s), _f64(rnstream), _f64(xstarts)
     lbs, ubs = _f64(lbs), _f64(ubs)
@@ -134,7 +136,7 @@ def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=
     M = rnstream.shape[0]
     assert rnstream.shape == (M, d + 1, h + 1), rnstream.shape
     prm = Params(h, M, R, xstarts.shape[1], theta, _p(lbs), _p(ubs), max_iters, max_ls, x_tol, f_tol, g_tol,
-                 htol, sigma_tol, seed, 1 if with_gradient else 0, nthreads)
+                 htol, sigma_tol, seed, sample_offset, samples_total, 1 if with_gradient else 0, nthreads)
     values = np.zeros((M, R), order="F")
     grad_x = np.zeros((d, M, R), order="F")
     grad_t = np.zeros((1, M, R), order="F")

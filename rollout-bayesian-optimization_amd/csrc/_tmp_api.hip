@@ -12,7 +12,7 @@
 #include <vector>
 
 #include "../../include/mrbo.h"
-#include "mrbo_rollout.hip"
+#include "_w.hip"
 #include "sobol_table.h"
 
 using namespace mrbo;
@@ -89,11 +89,7 @@ bool get_kset(int d, int rpl, KernelSet& ks) {
     ks = (rpl == 1) ? kset<DD, 1>() : kset<DD, 2>();    \
     return true;
   switch (d) {
-#ifdef MRBO_ONLY_D
-    CASE(MRBO_ONLY_D)
-#else
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
-#endif
     default: return false;
   }
 #undef CASE
@@ -105,11 +101,7 @@ void launch_rollout(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, c
     if (rpl == 1) hipLaunchKernelGGL((rollout_kernel<DD, 1>), g, b, sm, st, kp);           \
     else hipLaunchKernelGGL((rollout_kernel<DD, 2>), g, b, sm, st, kp);                    \
     break;
-#ifdef MRBO_ONLY_D
-  switch (d) { CASE(MRBO_ONLY_D) }
-#else
   switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) }
-#endif
 #undef CASE
 }
 void launch_evalb(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
@@ -118,11 +110,7 @@ void launch_evalb(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, con
     if (rpl == 1) hipLaunchKernelGGL((eval_base_kernel<DD, 1>), g, b, sm, st, kp);         \
     else hipLaunchKernelGGL((eval_base_kernel<DD, 2>), g, b, sm, st, kp);                  \
     break;
-#ifdef MRBO_ONLY_D
-  switch (d) { CASE(MRBO_ONLY_D) }
-#else
   switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) }
-#endif
 #undef CASE
 }
 

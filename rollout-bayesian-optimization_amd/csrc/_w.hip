@@ -12,10 +12,6 @@
 // factor L⁻¹ = [[L0⁻¹,0],[E,Dinv]] instead of substitution (same maths, fp64).
 #include "mrbo_device.h"
 
-#ifndef MRBO_WAVES_PER_SIMD
-#define MRBO_WAVES_PER_SIMD 2
-#endif
-
 namespace mrbo {
 
 template <int D, int RPL>
@@ -89,12 +85,6 @@ struct WaveCtx {
   bool valid[RPL];
   int N, Npad;
   Radial rad;
-  // opaque lane index (see evaluate): per-lane addresses are rematerialised where used
-  __device__ __forceinline__ int ln() const {
-    int l = lane;
-    asm volatile("" : "+v"(l));
-    return l;
-  }
 };
 
 // work counters per trajectory (for the algorithmic-FLOP roofline)
@@ -124,11 +114,7 @@ template <int D, int RPL>
 __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, int S, int mode, LaneRes<D, RPL>& lr) {
   using Ly = Lay<D, RPL>;
   constexpr int D1 = Ly::D1, BS = Ly::BS, NR = Ly::NR;
-  // Opaque copy of the lane index: keeps the per-lane LDS/global addresses derived from it
-  // inside this evaluation instead of being hoisted (and held live in VGPRs) across the
-  // caller's Newton / horizon loops -- the difference between 1 and 3-4 waves per SIMD.
-  int lane = W.lane;
-  asm volatile("" : "+v"(lane));
+  const int lane = W.lane;
   const int nf = S + 1;
   double* U = W.U;
   double* B = W.B;
@@ -525,7 +511,7 @@ __device__ __forceinline__ int condition(WaveCtx<D, RPL>& W, const KParams& kp, 
   using Ly = Lay<D, RPL>;
   constexpr int NR = Ly::NR;
   double* U = W.U;
-  const int lane = W.ln();
+  const int lane = W.lane;
   const int nf = S + 1;   // index of the new fantasy row
   const double g00 = U[Ly::U_G];
   const double mu = U[Ly::U_SC + SC_MU];
@@ -715,8 +701,7 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
   for (int i = 0; i < D; ++i) { pn = fmax(pn, fabs(p[i])); box = fmax(box, U[Ly::U_UB + i] - U[Ly::U_LB + i]); }
   const double sc = (pn > box) ? box / pn : 1.0;
   wave_sync();
-  const int lane = W.ln();
-  if (lane < D) U[Ly::U_NP + lane] = (pn > box) ? p[lane] * sc : p[lane];
+  if (W.lane < D) U[Ly::U_NP + W.lane] = (pn > box) ? p[W.lane] * sc : p[W.lane];
   wave_sync();
   return true;
 }
@@ -726,17 +711,16 @@ template <int D, int RPL>
 __device__ __forceinline__ double newton_trial_point(WaveCtx<D, RPL>& W, double t) {
   using Ly = Lay<D, RPL>;
   double* U = W.U;
-  const int lane = W.ln();
   double dec = 0.0, mine = 0.0;
 #pragma unroll
   for (int a = 0; a < D; ++a) {
     const double xa = U[Ly::U_NX + a];
     const double xt = clampd(xa + t * U[Ly::U_NP + a], U[Ly::U_LB + a], U[Ly::U_UB + a]);
     dec += U[Ly::U_NG + a] * (xt - xa);
-    if (a == lane) mine = xt;
+    if (a == W.lane) mine = xt;
   }
   wave_sync();
-  if (lane < D) U[Ly::U_X + lane] = mine;
+  if (W.lane < D) U[Ly::U_X + W.lane] = mine;
   wave_sync();
   return dec;
 }
@@ -748,7 +732,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
                                          int& st, LaneRes<D, RPL>& lr) {
   using Ly = Lay<D, RPL>;
   double* U = W.U;
-  const int lane = W.ln();
+  const int lane = W.lane;
   enum { P_INIT = 0, P_TRIAL = 1, P_REFULL = 2 };
   if (lane < D) {
     const double xa = clampd(kp.xstarts[(long long)k * D + lane], U[Ly::U_LB + lane], U[Ly::U_UB + lane]);
@@ -819,7 +803,7 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
                                           LaneRes<D, RPL>& lr) {
   using Ly = Lay<D, RPL>;
   double* U = W.U;
-  const int lane = W.ln();
+  const int lane = W.lane;
   int st = 0;
   int best = -1;
   bool best_nan = false;
@@ -863,7 +847,7 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
   constexpr int NR = Ly::NR;
   double* U = W.U;
   double* red = W.red;
-  const int lane = W.ln();
+  const int lane = W.lane;
   const int nf = S + 1;
   double Xq[D];
 #pragma unroll
@@ -1045,8 +1029,7 @@ template <int D, int RPL>
 __device__ __forceinline__ void rich_eval_at(WaveCtx<D, RPL>& W, const KParams& kp, int j, LaneRes<D, RPL>& lr) {
   using Ly = Lay<D, RPL>;
   wave_sync();
-  const int lane = W.ln();
-  if (lane < D) W.U[Ly::U_X + lane] = W.U[Ly::U_XF + j * D + lane];
+  if (W.lane < D) W.U[Ly::U_X + W.lane] = W.U[Ly::U_XF + j * D + W.lane];
   wave_sync();
   evaluate<D, RPL>(W, kp, j - 1, EV_RICH, lr);
 }
@@ -1059,7 +1042,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
   using Ly = Lay<D, RPL>;
   constexpr int D1 = Ly::D1, NR = Ly::NR;
   double* U = W.U;
-  const int lane = W.ln();
+  const int lane = W.lane;
   const int M = kp.M, h = kp.h;
   const int r = (int)(tr / M), m = (int)(tr % M);
   Counters nevals;
@@ -1084,9 +1067,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
         if (lane < D) U[Ly::U_X + lane] = kp.replay[(long long)lane + D * ((k - 1) + (long long)h * (m + (long long)M * r))];
         wave_sync();
       } else {
-#ifndef MRBO_EXP_NO_NEWTON
         st |= multistart<D, RPL>(W, kp, S, nevals, lr);
-#endif
         if (st) break;
         if (lane < D) U[Ly::U_X + lane] = U[Ly::U_XB + lane];
         wave_sync();
@@ -1124,7 +1105,6 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
   const double value = fmax(kp.fmini - bo, 0.0);
   double gth = 0.0;
   bool grad_zero = true;
-#ifndef MRBO_EXP_NO_ADJOINT
   if (kp.with_gradient && kp.fmini > bo) {
     if (t == 0) {
       grad_zero = false;  // ∇x = -∇y₀ (Q10)
@@ -1196,7 +1176,6 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
       }
     }
   }
-#endif
   // outputs: ∇x = -(∇μ(x0)·ȳ0 + ACC[0]),  ∇θ = -Σ mixed·x̄
   wave_sync();
   const long long base = oidx;
@@ -1252,7 +1231,7 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
 }
 
 template <int D, int RPL>
-__global__ void __launch_bounds__(256, MRBO_WAVES_PER_SIMD) rollout_kernel(KParams kp) {
+__global__ void __launch_bounds__(256, 3) rollout_kernel(KParams kp) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // stage the packed L0⁻¹ once per workgroup (the only block-wide barrier)
   const long long lin = linv_size(kp.Npad);
@@ -1272,7 +1251,7 @@ __global__ void __launch_bounds__(256, MRBO_WAVES_PER_SIMD) rollout_kernel(KPara
 
 // eval(s, x, θ) on the base surrogate for P points (fixture / primitive parity path)
 template <int D, int RPL>
-__global__ void __launch_bounds__(256, MRBO_WAVES_PER_SIMD) eval_base_kernel(KParams kp) {
+__global__ void __launch_bounds__(256) eval_base_kernel(KParams kp) {
   using Ly = Lay<D, RPL>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const long long lin = linv_size(kp.Npad);
@@ -1280,7 +1259,7 @@ __global__ void __launch_bounds__(256, MRBO_WAVES_PER_SIMD) eval_base_kernel(KPa
   __syncthreads();
   WaveCtx<D, RPL> W;
   wave_setup<D, RPL>(W, kp, smem, threadIdx.x / WAVE);
-  const int lane = W.ln();
+  const int lane = W.lane;
 #pragma unroll
   for (int s = 0; s < RPL; ++s) W.C[lane + WAVE * s] = kp.c0[lane + WAVE * s];
   if (lane == 0) W.U[Ly::U_FMIN] = kp.fmin_base;

@@ -30,6 +30,7 @@ struct KParams {
   int max_iters, max_ls;
   double x_tol, f_tol, g_tol, htol, sigma_tol;
   unsigned long long seed;
+  int sample_offset, samples_total;
   int with_gradient;
   const double* X0;     // [d][NR]   lane-major base covariates
   const double* c0;     // [NR]      base coefficients
@@ -99,6 +100,13 @@ __device__ __forceinline__ void wave_reduce(double (&v)[K], double* red, int lan
   if ((lane & ((64 >> S) - 1)) == 0) red[idx] = v[0];
 }
 
+// ---- transcendentals behind leaf calls ---------------------------------------------------
+// The fp64 exp/erfc expansions carry tens of 64-bit polynomial constants; inlined into the
+// Newton/horizon loops, LICM hoists their materialisation out of the loops and the kernel
+// spills them.  As leaf calls the constants stay local to the callee.
+__device__ __attribute__((noinline)) double xexp(double x) { return exp(x); }
+__device__ __attribute__((noinline)) double xerfc(double x) { return erfc(x); }
+
 // ---- radial kernels (radial_basis_functions.jl:60-96; derivatives in closed form) -------
 struct Radial {
   int kind;
@@ -107,38 +115,38 @@ struct Radial {
 
 __device__ __forceinline__ void rad_psi(const Radial& k, double rho, double& psi, double& dpsi) {
   if (k.kind == 0) {
-    const double s = k.cK * rho, e = exp(-s);
+    const double s = k.cK * rho, e = xexp(-s);
     psi = (1.0 + s * (1.0 + s / 3.0)) * e;
     dpsi = -k.cK * (s / 3.0) * (1.0 + s) * e;
   } else if (k.kind == 1) {
-    const double s = k.cK * rho, e = exp(-s);
+    const double s = k.cK * rho, e = xexp(-s);
     psi = (1.0 + s) * e;
     dpsi = -k.cK * s * e;
   } else if (k.kind == 2) {
-    const double e = exp(-k.cK * rho);
+    const double e = xexp(-k.cK * rho);
     psi = e;
     dpsi = -k.cK * e;
   } else {
-    const double e = exp(-0.5 * rho * rho * k.cK);
+    const double e = xexp(-0.5 * rho * rho * k.cK);
     psi = e;
     dpsi = -(rho * k.cK) * e;
   }
 }
 __device__ __forceinline__ void rad_psi12(const Radial& k, double rho, double& dpsi, double& d2psi) {
   if (k.kind == 0) {
-    const double s = k.cK * rho, e = exp(-s);
+    const double s = k.cK * rho, e = xexp(-s);
     dpsi = -k.cK * (s / 3.0) * (1.0 + s) * e;
     d2psi = k.cK * k.cK * (s * s - s - 1.0) * e / 3.0;
   } else if (k.kind == 1) {
-    const double s = k.cK * rho, e = exp(-s);
+    const double s = k.cK * rho, e = xexp(-s);
     dpsi = -k.cK * s * e;
     d2psi = k.cK * k.cK * (s - 1.0) * e;
   } else if (k.kind == 2) {
-    const double e = exp(-k.cK * rho);
+    const double e = xexp(-k.cK * rho);
     dpsi = -k.cK * e;
     d2psi = k.cK * k.cK * e;
   } else {
-    const double e = exp(-0.5 * rho * rho * k.cK);
+    const double e = xexp(-0.5 * rho * rho * k.cK);
     dpsi = -(rho * k.cK) * e;
     d2psi = (rho * rho * k.cK * k.cK - k.cK) * e;
   }
@@ -156,8 +164,8 @@ __device__ __forceinline__ EIp ei_partials(double mu, double sig, double theta, 
   }
   const double imp = fmin - mu - theta;
   const double z = imp / sig;
-  const double Phi = erfc(-z * 0.7071067811865476) / 2.0;
-  const double phi = exp(-(z * z) / 2.0) * 0.3989422804014327;
+  const double Phi = xerfc(-z * 0.7071067811865476) / 2.0;
+  const double phi = xexp(-(z * z) / 2.0) * 0.3989422804014327;
   e.g = imp * Phi + sig * phi;
   e.gmu = -Phi;
   e.gsig = phi;
@@ -172,8 +180,8 @@ __device__ __forceinline__ void ei_first(double mu, double sig, double theta, do
                                          double& gmu, double& gsig) {
   if (!(sig >= sigma_tol) && !(sig != sig)) { gmu = 0.0; gsig = 0.0; return; }
   const double z = (fmin - mu - theta) / sig;
-  gmu = -(erfc(-z * 0.7071067811865476) / 2.0);
-  gsig = exp(-(z * z) / 2.0) * 0.3989422804014327;
+  gmu = -(xerfc(-z * 0.7071067811865476) / 2.0);
+  gsig = xexp(-(z * z) / 2.0) * 0.3989422804014327;
 }
 
 // counter-based uniform (bit-identical to the host / oracle version)

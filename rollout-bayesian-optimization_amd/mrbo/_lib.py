@@ -43,7 +43,8 @@ class ParamsDesc(ctypes.Structure):
                 ("rule", ctypes.c_int32), ("theta", ctypes.c_double), ("lbs", _dp), ("ubs", _dp),
                 ("max_iters", ctypes.c_int32), ("max_ls", ctypes.c_int32), ("x_tol", ctypes.c_double),
                 ("f_tol", ctypes.c_double), ("g_tol", ctypes.c_double), ("htol", ctypes.c_double),
-                ("sigma_tol", ctypes.c_double), ("seed", ctypes.c_uint64)]
+                ("sigma_tol", ctypes.c_double), ("seed", ctypes.c_uint64),
+                ("sample_offset", ctypes.c_int32), ("samples_total", ctypes.c_int32)]
 
 
 _lib = None

@@ -10,7 +10,8 @@ import numpy as np
 
 from . import _lib
 
-DEFAULTS = dict(max_iters=50, max_ls=20, x_tol=1e-3, f_tol=1e-3, g_tol=1e-8, htol=1e-4, sigma_tol=1e-8, seed=1906)
+DEFAULTS = dict(max_iters=50, max_ls=20, x_tol=1e-3, f_tol=1e-3, g_tol=1e-8, htol=1e-4, sigma_tol=1e-8, seed=1906,
+                sample_offset=0, samples_total=0)
 
 
 def _torch():
@@ -57,7 +58,7 @@ class RolloutPlan:
         pd = _lib.ParamsDesc(self.h, self.M, self.R, self.nstarts, 0, self.theta, self._lbs.ctypes.data_as(dp),
                              self._ubs.ctypes.data_as(dp), int(o["max_iters"]), int(o["max_ls"]), float(o["x_tol"]),
                              float(o["f_tol"]), float(o["g_tol"]), float(o["htol"]), float(o["sigma_tol"]),
-                             int(o["seed"]))
+                             int(o["seed"]), int(o.get("sample_offset", 0)), int(o.get("samples_total", 0)))
         h_ = ctypes.c_void_p()
         _lib.check(self.lib.mrbo_plan_create(ctypes.byref(sd), ctypes.byref(pd), int(device), ctypes.byref(h_)))
         self.handle = h_
@@ -88,7 +89,7 @@ class RolloutPlan:
         if want_obs:
             out["obs"] = torch.empty((self.h + 1) * T, dtype=torch.float64, device=dev)
         if want_evals:
-            out["evals"] = torch.empty(T, dtype=torch.int64, device=dev)
+            out["evals"] = torch.empty(4 * T, dtype=torch.int64, device=dev)
         return out
 
     def simulate(self, x0s, rnstream, xstarts, out, dual_y_dx=None, replay_x=None, stream=None):

@@ -37,7 +37,7 @@ def run(name, M, R):
     dt = time.time() - t
     g = br.numpy()
     print(f"[{name}] gpu {M*R} traj in {dt:.3f}s kernel {br.plan.last_kernel_ms():.2f} ms; status", np.unique(g["status"]),
-          "evals mean", g["evals"].mean())
+          "evals mean", g["evals"][0].mean(), "value", g["evals"][1].mean(), "rich", g["evals"][2].mean(), "pairs", g["evals"][3].mean())
     t = time.time()
     o = O.simulate_mc(osur, pb.x0s, pb.tp.rnstream_sequence, pb.es.get_starts(), pb.lbs, pb.ubs, pb.cfg.h, nthreads=16)
     print(f"[{name}] oracle {time.time()-t:.2f}s status", np.unique(o["status"]), "evals mean", o["evals"].mean())
