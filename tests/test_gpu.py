@@ -1,0 +1,235 @@
+"""GPU parity tests: libmrbo.so (HIP, gfx950) against the CPU oracle and the golden fixtures.
+
+Tolerances (fp64 throughout):
+  primitives (μ, σ, ∇, Hα at base points)            rtol 1e-9
+  replay trajectories (policy points injected)         values rtol 1e-8, gradients rtol 1e-6
+  end-to-end (both sides run the inner Newton solve)  ≥ 97 % identical policy paths; on those,
+                                                      the replay tolerances
+The GPU computes triangular solves through the explicit inverse factor and sums in a
+different order than the oracle's substitution, hence tolerances rather than bit equality.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_CASES, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _plan(g, M=None, R=None, h=None, nstarts=None, kernel=0, **opts):
+    from mrbo.engine import RolloutPlan
+    M = M or g["rnstream"].shape[0]
+    R = R or g["x0s"].shape[1]
+    h = int(g["h"]) if h is None else h
+    return RolloutPlan(g["X"], g["L"], g["c"], g["y"], kernel, 1.0, 1e-6, float(g["fmini"]), h, M, R,
+                       nstarts or g["xstarts"].shape[1], g["lbs"], g["ubs"], 0.0, **opts)
+
+
+def _run(plan, g, dual=None, replay=None, want_policy=True, with_gradient=True, rn=None, x0s=None):
+    import torch
+    from mrbo.engine import from_device, to_device
+    dev = "cuda:0"
+    out = plan.alloc_outputs(with_gradient=with_gradient, want_policy=want_policy, want_obs=True)
+    plan.simulate(to_device(g["x0s"] if x0s is None else x0s, dev),
+                  to_device(g["rnstream"] if rn is None else rn, dev),
+                  to_device(g["xstarts"], dev), out,
+                  dual_y_dx=None if dual is None else to_device(dual, dev),
+                  replay_x=None if replay is None else to_device(replay, dev))
+    eto = plan.eto(out)
+    torch.cuda.synchronize()
+    d, M, R, h = plan.d, plan.M, plan.R, plan.h
+    res = dict(values=from_device(out["values"], (M, R)), status=from_device(out["status"], (M, R)),
+               obs=from_device(out["obs"], (h + 1, M, R)), eto=from_device(eto, (2 + 2 * d + 2, R)),
+               evals=from_device(out["evals"], (4, M, R)))
+    if with_gradient:
+        res["grad_x"] = from_device(out["grad_x"], (d, M, R))
+        res["grad_theta"] = from_device(out["grad_theta"], (1, M, R))
+    if want_policy:
+        res["policy_x"] = from_device(out["policy_x"], (d, h + 1, M, R))
+    return res
+
+
+def _osur(oracle, g, kernel="matern52"):
+    return oracle.OracleSurrogate(g["X"], g["L"], g["c"], g["y"], kernel=kernel, fmini=float(g["fmini"]))
+
+
+def _assert_grads_close(a, b, rtol=1e-6):
+    if b.size == 0:
+        return
+    scale = max(np.abs(b).max(), 1e-300)
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=1e-9 * scale)
+
+
+@pytest.mark.parametrize("case", GOLDEN_CASES)
+def test_eval_base_vs_golden(gpu, case):
+    g = load_golden(case)
+    p = _plan(g)
+    np.testing.assert_allclose(p.eval_base(g["pts"]), g["prim"], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("case", GOLDEN_CASES)
+def test_replay_vs_golden(gpu, case):
+    g = load_golden(case)
+    r = _run(_plan(g), g, dual=g["dual_y_dx"], replay=g["replay_x"])
+    assert (r["status"] == 0).all()
+    np.testing.assert_allclose(r["obs"], g["obs"], rtol=1e-9, atol=1e-11)
+    np.testing.assert_allclose(r["values"], g["values"], rtol=1e-8, atol=1e-11)
+    _assert_grads_close(r["grad_x"], g["grad_x"])
+    _assert_grads_close(r["grad_theta"], g["grad_theta"])
+
+
+def _problem_arrays(name, M, R, kernel=None, testfn=None, d=None, N=None, h=None):
+    from mrbo import configs
+    from mrbo.kernels import Matern12, Matern32, SquaredExponential
+    if testfn is not None:
+        cfg = configs.Config(f"T{testfn}{d}", testfn, d, h, M, R, N, 1)
+        pb = configs.Problem(cfg)
+    else:
+        pb = configs.problem(name, M=M, R=R)
+    s = pb.surrogate
+    if kernel is not None:
+        s.set_kernel({"matern32": Matern32(), "matern12": Matern12(), "se": SquaredExponential()}[kernel])
+    n = s.observed
+    return dict(X=s.X[:, :n], L=s.L[:n, :n], c=s.c[:n], y=s.y[:n], fmini=s.fmini(), lbs=pb.lbs, ubs=pb.ubs,
+                x0s=pb.x0s, rnstream=pb.tp.rnstream_sequence, xstarts=pb.es.get_starts(), h=pb.cfg.h)
+
+
+@pytest.mark.parametrize("name,M,R", [("C1", 32, 4), ("C2", 32, 4), ("C3", 32, 4)])
+def test_end_to_end_vs_oracle(gpu, oracle, name, M, R):
+    """Both sides run the full rollout including the inner Newton solves."""
+    g = _problem_arrays(name, M, R)
+    r = _run(_plan(g), g)
+    o = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
+                           nthreads=8)
+    assert (r["status"] == 0).all() and (o["status"] == 0).all()
+    same = np.all(np.abs(r["policy_x"] - o["policy_x"]) <= 1e-6 * (1 + np.abs(o["policy_x"])), axis=(0, 1))
+    assert same.mean() >= 0.97, same.mean()
+    np.testing.assert_allclose(r["values"][same], o["values"][same], rtol=1e-8, atol=1e-11)
+    _assert_grads_close(r["grad_x"][:, same], o["grad_x"][:, same])
+    np.testing.assert_array_equal(r["evals"][0][same], o["evals"][same])  # identical Newton work
+    # replay the GPU's own policy points through the oracle: every trajectory agrees
+    rp = np.asfortranarray(r["policy_x"][:, 1:])
+    o2 = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
+                            replay_x=rp, nthreads=8)
+    np.testing.assert_allclose(r["values"], o2["values"], rtol=1e-8, atol=1e-11)
+    _assert_grads_close(r["grad_x"], o2["grad_x"])
+
+
+@pytest.mark.parametrize("kernel,kid", [("matern32", 1), ("matern12", 2), ("se", 3)])
+def test_other_kernels_replay_vs_oracle(gpu, oracle, kernel, kid):
+    g = _problem_arrays("C2", 16, 2, kernel=kernel)
+    r = _run(_plan(g, kernel=kid), g)
+    rp = np.asfortranarray(r["policy_x"][:, 1:])
+    o = oracle.simulate_mc(_osur(oracle, g, kernel), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"],
+                           int(g["h"]), replay_x=rp, nthreads=8)
+    assert (r["status"] == o["status"]).all()
+    if kernel == "matern12":  # ψ''(0) > 0: Dk(0) is indefinite, gp_draw's cholesky fails (PosDefException)
+        assert (r["status"] & 2).all()
+    ok = r["status"] == 0
+    np.testing.assert_allclose(r["values"][ok], o["values"][ok], rtol=1e-8, atol=1e-11)
+    _assert_grads_close(r["grad_x"][:, ok], o["grad_x"][:, ok], rtol=1e-5)
+
+
+@pytest.mark.parametrize("d,N,h", [(1, 12, 2), (3, 24, 2), (4, 40, 3), (5, 30, 2), (7, 48, 2), (8, 64, 3), (3, 96, 2),
+                                   (6, 128, 4)])
+def test_dimensions_and_sizes_replay_vs_oracle(gpu, oracle, d, N, h):
+    """d = 1..8 and N up to 128 (two data rows per lane) on Ackley(d)."""
+    g = _problem_arrays(None, 8, 2, testfn="ackley", d=d, N=N, h=h)
+    r = _run(_plan(g), g)
+    assert (r["status"] == 0).all()
+    rp = np.asfortranarray(r["policy_x"][:, 1:])
+    o = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], h,
+                           replay_x=rp, nthreads=8)
+    np.testing.assert_allclose(r["values"], o["values"], rtol=1e-8, atol=1e-11)
+    _assert_grads_close(r["grad_x"], o["grad_x"], rtol=1e-5)
+
+
+def test_full_size_c3_properties(gpu):
+    """Headline size (65 536 trajectories): size-independent properties."""
+    g = _problem_arrays("C3", 1024, 64)
+    p = _plan(g)
+    a = _run(p, g, want_policy=False)
+    b = _run(p, g, want_policy=False)
+    assert (a["status"] == 0).all()
+    np.testing.assert_array_equal(a["values"], b["values"])          # deterministic
+    np.testing.assert_array_equal(a["grad_x"], b["grad_x"])
+    assert (a["values"] >= 0).all()
+    z = a["values"] == 0                                               # case 1: no improvement -> ∇ = 0
+    assert (a["grad_x"][:, z] == 0).all() and (a["grad_theta"][:, z] == 0).all()
+    # obs consistency: value = max(fmini - min(obs), 0)
+    np.testing.assert_allclose(a["values"], np.maximum(g["fmini"] - a["obs"].min(axis=0), 0.0), rtol=0, atol=0)
+    # ETO kernel == two-pass mean / std(n-1) (rollout.jl:328-339)
+    np.testing.assert_allclose(a["eto"][0], a["values"].mean(0), rtol=1e-12)
+    np.testing.assert_allclose(a["eto"][1], a["values"].std(0, ddof=1), rtol=1e-10)
+    np.testing.assert_allclose(a["eto"][2:8], a["grad_x"].mean(1), rtol=1e-10, atol=1e-18)
+
+
+def test_sharded_plans_equal_single_plan(gpu):
+    """Two MC shards (multi-GPU decomposition) reproduce the single launch bit for bit."""
+    g = _problem_arrays("C2", 64, 4)
+    full = _run(_plan(g), g)
+    parts = []
+    for lo, hi in [(0, 24), (24, 64)]:
+        gg = dict(g)
+        gg["rnstream"] = np.asfortranarray(g["rnstream"][lo:hi])
+        parts.append(_run(_plan(gg, M=hi - lo, sample_offset=lo, samples_total=64), gg))
+    np.testing.assert_array_equal(np.concatenate([q["values"] for q in parts], 0), full["values"])
+    np.testing.assert_array_equal(np.concatenate([q["grad_x"] for q in parts], 1), full["grad_x"])
+
+
+def test_horizon_zero_and_single_sample(gpu, oracle):
+    g = _problem_arrays("C2", 8, 2)
+    g["rnstream"] = np.asfortranarray(g["rnstream"][:, :, :1])
+    r = _run(_plan(g, h=0), g)
+    o = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], 0)
+    np.testing.assert_allclose(r["values"], o["values"], rtol=1e-9, atol=1e-12)
+    _assert_grads_close(r["grad_x"], o["grad_x"])
+    # M = 1: std with n-1 is NaN (Q14)
+    g1 = dict(g)
+    g1["rnstream"] = np.asfortranarray(g["rnstream"][:1])
+    r1 = _run(_plan(g1, M=1, h=0), g1)
+    assert np.isnan(r1["eto"][1]).all()
+
+
+def test_explicit_dual_draws_and_no_gradient(gpu):
+    g = load_golden("c2near")
+    p = _plan(g)
+    a = _run(p, g, dual=g["dual_y_dx"], replay=g["replay_x"])
+    b = _run(p, g, dual=g["dual_y_dx"], replay=g["replay_x"], with_gradient=False)
+    np.testing.assert_array_equal(a["values"], b["values"])
+    assert "grad_x" not in b
+
+
+def test_host_pointer_flag_matches_device_path(gpu):
+    """MRBO_FLAG_HOST_POINTERS: the Julia-shim path with host arrays (PCIe staging)."""
+    from mrbo import _lib
+    g = load_golden("c2")
+    p = _plan(g)
+    dev = _run(p, g, dual=g["dual_y_dx"], replay=g["replay_x"], want_policy=False)
+    d, M, R = p.d, p.M, p.R
+    vals = np.zeros((M, R), order="F")
+    gx = np.zeros((d, M, R), order="F")
+    gt = np.zeros((1, M, R), order="F")
+    st = np.zeros((M, R), dtype=np.int32, order="F")
+    keep = [np.asfortranarray(g[k], dtype=np.float64) for k in ("x0s", "rnstream", "xstarts", "dual_y_dx", "replay_x")]
+    ptr = [ctypes.c_void_p(a.ctypes.data) for a in keep]
+    outp = [ctypes.c_void_p(a.ctypes.data) for a in (vals, gx, gt, st)]
+    _lib.check(p.lib.mrbo_simulate_mc(p.handle, *ptr, *outp, None, None, None, _lib.MRBO_FLAG_HOST_POINTERS, None))
+    np.testing.assert_array_equal(vals, dev["values"])
+    np.testing.assert_array_equal(gx, dev["grad_x"])
+
+
+def test_reference_signature_and_outer_ascent(gpu):
+    """simulate_trajectory_mc(T, tp; …) fills the caller's containers (rollout.jl:318-322) and
+    stochastic_solve runs the outer SGA (utils.jl:235-265)."""
+    from mrbo import StandardSGA, configs, simulate_trajectory_mc, stochastic_solve
+    pb = configs.problem("C2", M=64, R=1)
+    es = pb.es
+    eto = simulate_trajectory_mc(pb.T, pb.tp, es.get_starts(), es.get_container("f"),
+                                 es.get_container("grad_f"), es.get_container("grad_hypers"))
+    assert eto.mean() == pytest.approx(es.resolutions.mean(), rel=1e-12)
+    np.testing.assert_allclose(eto.gradient(), es.spatial_gradients_container.mean(axis=1), rtol=1e-10)
+    x = stochastic_solve(StandardSGA(η=0.5), pb.surrogate, pb.tp, es, pb.x0s[:, 0], T=pb.T, iterations=3)
+    assert x.shape == (2,) and np.all(np.isfinite(x))

@@ -1,0 +1,132 @@
+"""CPU tests of the host side: the reference-API mirror (mrbo package), the C-ABI library's
+exports and host helpers, and the multi-GPU reduction logic (no GPU compute here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_CASES, ROOT, load_golden
+
+
+def test_library_exports_every_header_symbol():
+    """libmrbo.so loads without a GPU and exports every entry point include/mrbo.h declares."""
+    from mrbo import _lib
+    hdr = open(os.path.join(ROOT, "include", "mrbo.h")).read()
+    declared = sorted(set(re.findall(r"\b(mrbo_[a-z_]+)\s*\(", hdr)))
+    assert set(declared) == set(_lib.EXPORTS), (declared, _lib.EXPORTS)
+    L = _lib.load()
+    for sym in declared:
+        assert hasattr(L, sym), sym
+    assert b"gfx950" in L.mrbo_version()
+
+
+@pytest.mark.parametrize("case", GOLDEN_CASES)
+def test_library_rnstream_matches_golden_and_oracle(oracle, case):
+    from mrbo.engine import initial_guesses, rnstream
+    g = load_golden(case)
+    M, D1, H = g["rnstream"].shape
+    rn = rnstream(M, D1 - 1, H)
+    np.testing.assert_allclose(rn, g["rnstream"], rtol=1e-15, atol=1e-15)
+    np.testing.assert_array_equal(rn, oracle.gen_low_discrepancy_sequence(M, D1 - 1, H))
+    np.testing.assert_array_equal(initial_guesses(16, g["lbs"], g["ubs"]),
+                                  oracle.generate_initial_guesses(16, g["lbs"], g["ubs"]))
+
+
+def test_library_dual_uniform_bit_identical_to_oracle(oracle):
+    from mrbo.engine import dual_uniform
+    for t, j, k in [(0, 1, 0), (12345, 3, 5), (2 ** 31 + 7, 5, 7)]:
+        assert dual_uniform(1906, t, j, k) == oracle.dual_uniform(1906, t, j, k)
+
+
+def test_plan_create_rejects_unsupported_shapes():
+    """Argument errors come back as negative codes with a message (no exception inside C)."""
+    from mrbo import _lib
+    L = _lib.load()
+    dp = ctypes.POINTER(ctypes.c_double)
+    X = np.zeros((9, 4), order="F")
+    Lm = np.eye(4, order="F")
+    c = np.zeros(4)
+    sd = _lib.SurrogateDesc(9, 4, 0, 1.0, 1e-6, 0.0, X.ctypes.data_as(dp), Lm.ctypes.data_as(dp), 4,
+                            c.ctypes.data_as(dp), c.ctypes.data_as(dp))
+    lb = np.zeros(9)
+    pd = _lib.ParamsDesc(3, 8, 2, 18, 0, 0.0, lb.ctypes.data_as(dp), lb.ctypes.data_as(dp), 50, 20, 1e-3, 1e-3,
+                         1e-8, 1e-4, 1e-8, 1906, 0, 0)
+    h = ctypes.c_void_p()
+    rc = L.mrbo_plan_create(ctypes.byref(sd), ctypes.byref(pd), 0, ctypes.byref(h))
+    assert rc == -2 and b"d=9" in L.mrbo_last_error()
+
+
+def test_kronecker_matches_oracle(oracle):
+    from mrbo.utils import kronecker_quasirand
+    for d, N, s in [(1, 8, 0), (2, 32, 0), (6, 64, 64), (8, 16, 3)]:
+        np.testing.assert_allclose(kronecker_quasirand(d, N, s), oracle.kronecker_quasirand(d, N, s), rtol=0,
+                                   atol=1e-15)
+
+
+def test_surrogate_fit_and_condition_match_dense_refit():
+    """Surrogate ctor (r_b_s.jl:77-118) and condition! (:214-222) vs a dense re-fit."""
+    from mrbo import EI, Matern52, Surrogate
+    from mrbo.kernels import eval_KXX
+    rng = np.random.default_rng(0)
+    X = rng.uniform(size=(3, 10))
+    y = rng.normal(size=10)
+    s = Surrogate(Matern52(), X, y, capacity=16, decision_rule=EI(), σn2=1e-6)
+    x, yn = rng.uniform(size=3), 0.3
+    s.condition(x, yn)
+    X2, y2 = np.column_stack([X, x]), np.append(y, yn)
+    K = eval_KXX(Matern52(), X2, σn2=1e-6)
+    np.testing.assert_allclose(s.get_active_cholesky() @ s.get_active_cholesky().T, K, atol=1e-12)
+    np.testing.assert_allclose(s.get_active_coefficients(), np.linalg.solve(K, y2), rtol=1e-8, atol=1e-10)
+    assert s.fmini() == min(0.0, y2.min())  # Q3: zero padding of the capacity buffer
+
+
+def test_trajectory_parameters_contract():
+    from mrbo import TrajectoryParameters
+    tp = TrajectoryParameters(start=[0.1, 0.2], hypers=[0.0], horizon=2, mc_iterations=8,
+                              use_low_discrepancy_sequence=True, spatial_lowerbounds=[0, 0], spatial_upperbounds=[1, 1])
+    assert tp.rnstream_sequence.shape == (8, 3, 3)
+    with pytest.raises(AssertionError):
+        TrajectoryParameters(start=[0.1], hypers=[0.0], horizon=2, mc_iterations=8, use_low_discrepancy_sequence=True,
+                             spatial_lowerbounds=[0, 0], spatial_upperbounds=[1, 1])
+
+
+def test_eto_from_sums_matches_two_pass():
+    from mrbo.parallel import eto_from_sums
+    rng = np.random.default_rng(3)
+    M, R, d = 37, 3, 2
+    v = rng.normal(0.2, 0.1, size=(M, R))
+    gx = rng.normal(size=(d, M, R)) * 1e-3
+    gt = rng.normal(size=(M, R))
+    W = 2 + 2 * d + 2
+    sums = np.zeros((W, R))
+    sums[0], sums[1] = v.sum(0), (v ** 2).sum(0)
+    sums[2:2 + d], sums[2 + d:2 + 2 * d] = gx.sum(1), (gx ** 2).sum(1)
+    sums[2 + 2 * d], sums[3 + 2 * d] = gt.sum(0), (gt ** 2).sum(0)
+    e = eto_from_sums(sums, M, d)
+    np.testing.assert_allclose(e[0], v.mean(0), rtol=1e-13)
+    np.testing.assert_allclose(e[1], v.std(0, ddof=1), rtol=1e-10)
+    np.testing.assert_allclose(e[2:2 + d], gx.mean(1), rtol=1e-12)
+    np.testing.assert_allclose(e[2 + d:2 + 2 * d], gx.std(1, ddof=1), rtol=1e-9)
+
+
+def test_shard_partition():
+    from mrbo.parallel import shard
+    for M, W in [(1024, 1), (1024, 8), (1000, 3), (5, 8)]:
+        parts = [shard(M, W, r) for r in range(W)]
+        assert parts[0][0] == 0 and parts[-1][1] == M
+        assert all(parts[i][1] == parts[i + 1][0] for i in range(W - 1))
+
+
+def test_eswavs_and_optimizers():
+    from mrbo import Adam, StandardSGA, eswavs
+    assert eswavs(np.array([1e-6, 1e-6]), np.array([1.0, 1.0]), 16)        # noise dominates: stop
+    assert not eswavs(np.array([1.0, 1.0]), np.array([1e-3, 1e-3]), 16)    # clear signal: keep going
+    assert not eswavs(np.zeros(2), np.zeros(2), 16)                         # 0/0 -> NaN -> continue
+    x = np.zeros(2)
+    StandardSGA(η=0.5).update(x, np.array([1.0, -2.0]))
+    np.testing.assert_allclose(x, [0.5, -1.0])
+    a, x = Adam(η=0.1), np.zeros(2)
+    a.update(x, np.array([1.0, -1.0]))
+    np.testing.assert_allclose(x, [0.1, -0.1], rtol=1e-6)

@@ -1,0 +1,155 @@
+"""CPU tests of the oracle (oracle/rbo_oracle.c): pinned against scipy's Sobol, the golden
+fixtures of the independent NumPy restatement (tests/golden), closed forms, and the
+finite-difference methodology of the reference's own test harness (runtests.jl:11-157)."""
+import numpy as np
+import pytest
+from scipy.stats import qmc
+
+from conftest import GOLDEN_CASES, load_golden
+
+
+@pytest.mark.parametrize("dim", [1, 2, 3, 4, 7, 8, 10, 16])
+def test_sobol_matches_scipy(oracle, dim):
+    # Sobol.jl skips the zero point: point k of next! == scipy point k (utils.jl:4-13)
+    a = oracle.gen_uniform(257, dim).T
+    b = qmc.Sobol(dim, scramble=False).random(258)[1:]
+    np.testing.assert_array_equal(a, b)
+
+
+def test_rnstream_known_answers(oracle):
+    # first Sobol point is all 0.5 -> y1 = sqrt(-2 log10 .5) cos(pi), y2 = ... sin(pi)
+    rn = oracle.gen_low_discrepancy_sequence(4, 1, 2)
+    assert rn.shape == (4, 2, 2)
+    assert rn[0, 0, 0] == pytest.approx(-np.sqrt(2 * np.log10(2.0)), rel=1e-15)
+    assert abs(rn[1, 0, 0] - np.sqrt(2 * np.log10(2.0)) * np.sin(np.pi)) < 1e-30
+    # variance of the log10 Box-Muller normals is 1/ln(10) (Q1)
+    big = oracle.gen_low_discrepancy_sequence(4096, 1, 1)
+    assert np.var(big) == pytest.approx(1 / np.log(10), rel=2e-2)
+
+
+@pytest.mark.parametrize("case", GOLDEN_CASES)
+def test_rnstream_matches_golden(oracle, case):
+    g = load_golden(case)
+    M, D1, H = g["rnstream"].shape
+    rn = oracle.gen_low_discrepancy_sequence(M, D1 - 1, H)
+    np.testing.assert_allclose(rn, g["rnstream"], rtol=1e-15, atol=1e-15)
+
+
+@pytest.mark.parametrize("case", GOLDEN_CASES)
+def test_initial_guesses_match_golden(oracle, case):
+    g = load_golden(case)
+    xs = oracle.generate_initial_guesses(16, g["lbs"], g["ubs"])
+    np.testing.assert_allclose(xs, g["xstarts"], rtol=0, atol=1e-15)
+
+
+def _osur(oracle, g):
+    return oracle.OracleSurrogate(g["X"], g["L"], g["c"], g["y"], fmini=float(g["fmini"]))
+
+
+@pytest.mark.parametrize("case", GOLDEN_CASES)
+def test_eval_base_matches_golden(oracle, case):
+    g = load_golden(case)
+    out = oracle.eval_base(_osur(oracle, g), g["pts"])
+    np.testing.assert_allclose(out, g["prim"], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("case", GOLDEN_CASES)
+def test_replay_trajectories_match_golden(oracle, case):
+    """Forward rollout + adjoint gradient with injected policy points (replay)."""
+    g = load_golden(case)
+    h = int(g["h"])
+    o = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], h,
+                           dual_y_dx=g["dual_y_dx"], replay_x=g["replay_x"], nthreads=2)
+    assert (o["status"] == 0).all()
+    np.testing.assert_allclose(o["obs"], g["obs"], rtol=1e-9, atol=1e-11)
+    np.testing.assert_allclose(o["values"], g["values"], rtol=1e-9, atol=1e-11)
+    scale = np.abs(g["grad_x"]).max() + 1e-300
+    np.testing.assert_allclose(o["grad_x"], g["grad_x"], rtol=1e-7, atol=1e-9 * scale)
+    np.testing.assert_allclose(o["grad_theta"], g["grad_theta"], rtol=1e-7, atol=1e-9 * max(1.0, np.abs(g["grad_theta"]).max()))
+
+
+def test_fmini_capacity_quirk(oracle):
+    """Q3: fmini over the zero-padded capacity buffer; Branin y > 0 so fmini = 0 and no
+    trajectory can improve -> every value and gradient is exactly zero."""
+    g = load_golden("c2cap")
+    assert float(g["fmini"]) == 0.0
+    o = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
+                           dual_y_dx=g["dual_y_dx"], replay_x=g["replay_x"])
+    assert np.all(o["values"] == 0.0) and np.all(o["grad_x"] == 0.0)
+
+
+# --------------- finite-difference consistency (runtests.jl:11-118 methodology) -------------
+def _fd(f, x, h=1e-6):
+    g = np.zeros_like(x)
+    for i in range(x.size):
+        e = np.zeros_like(x)
+        e[i] = h
+        g[i] = (f(x + e) - f(x - e)) / (2 * h)
+    return g
+
+
+def test_eval_base_derivatives_fd(oracle):
+    g = load_golden("c2near")
+    s = _osur(oracle, g)
+    d = g["X"].shape[0]
+    x = g["x0s"][:, 0] + 0.3
+    col = lambda xx: oracle.eval_base(s, xx.reshape(-1, 1))[:, 0]
+    o = col(x)
+    mu, sig, alpha = o[0], o[1], o[2]
+    gmu, gsig, galpha = o[3:3 + d], o[3 + d:3 + 2 * d], o[3 + 2 * d:3 + 3 * d]
+    H = o[3 + 3 * d:3 + 3 * d + d * d].reshape(d, d, order="F")
+    np.testing.assert_allclose(gmu, _fd(lambda xx: col(xx)[0], x), rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(gsig, _fd(lambda xx: col(xx)[1], x), rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(galpha, _fd(lambda xx: col(xx)[2], x), rtol=1e-6, atol=1e-10)
+    # Q11: the reference Hessian omits g_μσ(∇μ∇σ' + ∇σ∇μ'); the FD of ∇α contains it
+    from scipy.special import erfc
+    z = (np.min(g["y"]) - mu) / sig
+    gmusig = z * np.exp(-z * z / 2) / np.sqrt(2 * np.pi) / sig
+    Hfd = np.column_stack([_fd(lambda xx: col(xx)[3 + 2 * d + a], x) for a in range(d)])
+    Htrue = H + gmusig * (np.outer(gmu, gsig) + np.outer(gsig, gmu))
+    np.testing.assert_allclose(Htrue, Hfd, rtol=1e-5, atol=1e-8)
+    _ = erfc
+
+
+def test_replay_mode_reproduces_own_policy(oracle):
+    """Replaying the oracle's own policy points reproduces the normal run exactly."""
+    g = load_golden("c2")
+    s = _osur(oracle, g)
+    h = int(g["h"])
+    a = oracle.simulate_mc(s, g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], h)
+    rp = np.asfortranarray(a["policy_x"][:, 1:])
+    b = oracle.simulate_mc(s, g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], h, replay_x=rp)
+    np.testing.assert_array_equal(a["values"], b["values"])
+    np.testing.assert_array_equal(a["grad_x"], b["grad_x"])
+
+
+def test_sharded_oracle_equals_full(oracle):
+    """Two MC shards with sample_offset/samples_total reproduce the full run (multi-GPU semantics)."""
+    g = load_golden("c2near")
+    s = _osur(oracle, g)
+    h, M = int(g["h"]), g["rnstream"].shape[0]
+    full = oracle.simulate_mc(s, g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], h)
+    parts = []
+    for lo, hi in [(0, M // 2), (M // 2, M)]:
+        parts.append(oracle.simulate_mc(s, g["x0s"], np.asfortranarray(g["rnstream"][lo:hi]), g["xstarts"], g["lbs"],
+                                        g["ubs"], h, sample_offset=lo, samples_total=M))
+    np.testing.assert_array_equal(np.concatenate([p["values"] for p in parts], axis=0), full["values"])
+    np.testing.assert_array_equal(np.concatenate([p["grad_x"] for p in parts], axis=1), full["grad_x"])
+
+
+def test_dual_uniform_range_and_determinism(oracle):
+    u = np.array([oracle.dual_uniform(1906, t, j, k) for t in range(50) for j in range(3) for k in range(4)])
+    assert np.all((u >= 0) & (u < 1))
+    assert abs(u.mean() - 0.5) < 0.06
+    assert oracle.dual_uniform(1906, 7, 2, 1) == oracle.dual_uniform(1906, 7, 2, 1)
+
+
+def test_eto_corrected_std(oracle):
+    g = load_golden("c2near")
+    o = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]))
+    d = g["X"].shape[0]
+    for r in range(g["x0s"].shape[1]):
+        v = o["values"][:, r]
+        assert o["eto"][0, r] == pytest.approx(v.mean(), rel=1e-14)
+        assert o["eto"][1, r] == pytest.approx(v.std(ddof=1), rel=1e-12)  # Q14: n-1
+        np.testing.assert_allclose(o["eto"][2:2 + d, r], o["grad_x"][:, :, r].mean(axis=1), rtol=1e-13, atol=1e-300)
