@@ -82,9 +82,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; MRBO_DIST_BACKEND=gloo + device wrap-around only for rehearsing the
+    # multi-rank path on a box with fewer GPUs than ranks
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)
     torch.cuda.set_device(local)
+    backend = os.environ.get("MRBO_DIST_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     cfg = configs.CONFIGS[args.config]
     M_local, R, d, h = cfg.M, cfg.R, cfg.d, cfg.h
     M_total = M_local * world
@@ -140,7 +148,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())

@@ -40,5 +40,10 @@ def allreduce_sums(sums_tensor, group=None):
     """one sum all-reduce of the (W·R) partial sums (fp64)."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(sums_tensor, op=dist.ReduceOp.SUM, group=group)
+        if sums_tensor.is_cuda and dist.get_backend(group) == "gloo":
+            host = sums_tensor.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+            sums_tensor.copy_(host)
+        else:
+            dist.all_reduce(sums_tensor, op=dist.ReduceOp.SUM, group=group)
     return sums_tensor
