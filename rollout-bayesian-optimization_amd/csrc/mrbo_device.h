@@ -104,8 +104,13 @@ __device__ __forceinline__ void wave_reduce(double (&v)[K], double* red, int lan
 // The fp64 exp/erfc expansions carry tens of 64-bit polynomial constants; inlined into the
 // Newton/horizon loops, LICM hoists their materialisation out of the loops and the kernel
 // spills them.  As leaf calls the constants stay local to the callee.
+#ifdef MRBO_INLINE_TRANSCENDENTALS
+__device__ __forceinline__ double xexp(double x) { return exp(x); }
+__device__ __forceinline__ double xerfc(double x) { return erfc(x); }
+#else
 __device__ __attribute__((noinline)) double xexp(double x) { return exp(x); }
 __device__ __attribute__((noinline)) double xerfc(double x) { return erfc(x); }
+#endif
 
 // ---- radial kernels (radial_basis_functions.jl:60-96; derivatives in closed form) -------
 struct Radial {

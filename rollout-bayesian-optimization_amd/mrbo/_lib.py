@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmrbo.so")
+LIB_PATH = os.environ.get("MRBO_LIB") or os.path.join(_HERE, "libmrbo.so")  # MRBO_LIB: A/B variant builds
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _vp = ctypes.c_void_p
