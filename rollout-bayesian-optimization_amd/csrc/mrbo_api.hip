@@ -50,7 +50,7 @@ struct mrbo_plan {
   // device state
   double* dX0 = nullptr;    // [d][NR]
   double* dc0 = nullptr;    // [NR]
-  double* dLinv = nullptr;  // packed
+  double* dLinv = nullptr;  // L0⁻¹ in the kernel's LDS layout (Lay::SQ)
   double* dlbs = nullptr;
   double* dubs = nullptr;
   double* dwork = nullptr;
@@ -76,11 +76,16 @@ struct KernelSet {
   const void* rollout;
   const void* evalb;
   size_t wave_bytes;
+  bool square;              // L0⁻¹ layout: dense square (ld) or packed triangle
+  int ld;
+  long long linv_doubles;
 };
 
 template <int D, int RPL>
 KernelSet kset() {
-  return KernelSet{(const void*)&rollout_kernel<D, RPL>, (const void*)&eval_base_kernel<D, RPL>, wave_lds_bytes<D, RPL>()};
+  using Ly = Lay<D, RPL>;
+  return KernelSet{(const void*)&rollout_kernel<D, RPL>, (const void*)&eval_base_kernel<D, RPL>, wave_lds_bytes<D, RPL>(),
+                   Ly::SQ, Ly::LD, Ly::LINV_DOUBLES};
 }
 
 bool get_kset(int d, int rpl, KernelSet& ks) {
@@ -354,9 +359,6 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
       col[i] = sacc / s->L[i + (size_t)ldL * i];
     }
   }
-  std::vector<double> packed((size_t)linv_size(Npad), 0.0);
-  for (int j = 0; j < N; ++j)
-    for (int i = j; i < N; ++i) packed[(size_t)linv_colstart(j, Npad) + (i - j)] = Li[i + (size_t)N * j];
   std::vector<double> X0((size_t)d * P->NR, 0.0), c0(P->NR, 0.0);
   for (int i = 0; i < N; ++i) {
     for (int a = 0; a < d; ++a) X0[(size_t)a * P->NR + i] = s->X[a + (size_t)d * i];
@@ -367,9 +369,14 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   if (e != hipSuccess) { delete P; return fail(MRBO_ERR_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e)); }
   KernelSet ks;
   get_kset(d, P->RPL, ks);
+  // the kernel's LDS image of L0⁻¹ (zero above the diagonal and on padded rows)
+  std::vector<double> packed((size_t)ks.linv_doubles, 0.0);
+  for (int j = 0; j < N; ++j)
+    for (int i = j; i < N; ++i)
+      packed[ks.square ? (size_t)j * ks.ld + i : (size_t)linv_colstart(j, Npad) + (i - j)] = Li[i + (size_t)N * j];
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete P; return fail(MRBO_ERR_HIP, "device props"); }
-  const size_t linv_bytes = sizeof(double) * (size_t)((linv_size(Npad) + 1) & ~1LL);
+  const size_t linv_bytes = sizeof(double) * (size_t)ks.linv_doubles;
   if (!pick_grid(ks.rollout, linv_bytes, ks.wave_bytes, prop.multiProcessorCount, P->wpg, P->blocks, P->smem) ||
       !pick_grid(ks.evalb, linv_bytes, ks.wave_bytes, prop.multiProcessorCount, P->ewpg, P->eblocks, P->esmem)) {
     delete P;

@@ -58,10 +58,10 @@ struct KParams {
 };
 
 // ---- packed L0⁻¹ layout: column j holds rows j..Npad-1 contiguously ----------------------
-__host__ __device__ __forceinline__ long long linv_colstart(int j, int Npad) {
+__host__ __device__ __forceinline__ constexpr long long linv_colstart(int j, int Npad) {
   return (long long)j * Npad - (long long)j * (j - 1) / 2;
 }
-__host__ __device__ __forceinline__ long long linv_size(int Npad) { return (long long)Npad * (Npad + 1) / 2; }
+__host__ __device__ __forceinline__ constexpr long long linv_size(int Npad) { return (long long)Npad * (Npad + 1) / 2; }
 
 // ---- wave-scope synchronisation for LDS hand-offs between lanes of ONE wave ------------
 __device__ __forceinline__ void wave_sync() {
@@ -70,33 +70,92 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ double shfl_xor_d(double v, int m) { return __shfl_xor(v, m, WAVE); }
+// ---- 64-bit cross-lane exchange ----------------------------------------------------------
+__device__ __forceinline__ void dsplit(double v, int& lo, int& hi) {
+  const long long b = __builtin_bit_cast(long long, v);
+  lo = (int)b;
+  hi = (int)(b >> 32);
+}
+__device__ __forceinline__ double djoin(int lo, int hi) {
+  return __builtin_bit_cast(double, (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
 
-// Transpose-reduce K per-lane values across the 64 lanes: after log2(K) butterfly steps
-// each lane holds one partial, then plain xor steps finish; one lane per group writes
-// red[idx].  Cost ≈ K+log2(64/K) shuffles instead of 6K.  Deterministic order.
+// M = 32 / 16: lanes with bit M clear get a(l) + a(l^M), lanes with it set get b(l^M) + b(l).
+// gfx950's v_permlane32_swap / v_permlane16_swap exchange exactly these cross halves of the
+// register pair in place: two swaps per double and one add -- no select, no LDS round trip.
+template <int M>
+__device__ __forceinline__ double swap_fold(double a, double b) {
+  int alo, ahi, blo, bhi;
+  dsplit(a, alo, ahi);
+  dsplit(b, blo, bhi);
+  if constexpr (M == 32) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+    return djoin(lo[0], hi[0]) + djoin(lo[1], hi[1]);
+  } else {
+    static_assert(M == 16, "swap_fold: M is 32 or 16");
+    const auto lo = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+    return djoin(lo[0], hi[0]) + djoin(lo[1], hi[1]);
+  }
+}
+
+// M = 8, 4, 2, 1: v from a partner lane that differs in bit M and agrees on all higher bits
+// (DPP row_mirror, row_half_mirror, quad_perm xor2 / xor1 -- one VALU move per dword).
+template <int M>
+__device__ __forceinline__ double dpp_partner(double v) {
+  constexpr int ctrl = (M == 8) ? 0x140 : (M == 4) ? 0x141 : (M == 2) ? 0x4E : 0xB1;
+  static_assert(M == 8 || M == 4 || M == 2 || M == 1, "dpp_partner: M in {8,4,2,1}");
+  int lo, hi;
+  dsplit(v, lo, hi);
+  lo = __builtin_amdgcn_update_dpp(0, lo, ctrl, 0xF, 0xF, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, ctrl, 0xF, 0xF, false);
+  return djoin(lo, hi);
+}
+
+// One transpose step: H pairs (v[q], v[q+H]) become H partial sums over twice as many lanes;
+// lanes with bit M set continue with the upper half of the values.
+template <int M, int H>
+__device__ __forceinline__ void fold_step(double* v, int lane, int& idx) {
+  const bool up = (lane & M) != 0;
+#pragma unroll
+  for (int q = 0; q < H; ++q) {
+    if constexpr (M >= 16) {
+      v[q] = swap_fold<M>(v[q], v[q + H]);
+    } else {
+      const double send = up ? v[q] : v[q + H];
+      const double keep = up ? v[q + H] : v[q];
+      v[q] = keep + dpp_partner<M>(send);
+    }
+  }
+  idx += up ? H : 0;
+}
+template <int M>
+__device__ __forceinline__ double fold_all(double v) {
+  if constexpr (M >= 16) return swap_fold<M>(v, v);
+  else return v + dpp_partner<M>(v);
+}
+
+// Transpose-reduce K per-lane values across the 64 lanes: log2(K) transpose steps (pairs
+// across lane bits 5, 4, …) leave one partial per lane, then plain all-reduce steps finish;
+// one lane per group writes red[idx].  Cost ≈ K + log2(64/K) exchanges instead of 6K.
+// The pairing and summation order are fixed: the result is deterministic.
 template <int K>
 __device__ __forceinline__ void wave_reduce(double (&v)[K], double* red, int lane) {
   constexpr int S = (K == 1) ? 0 : (K == 2) ? 1 : (K == 4) ? 2 : (K == 8) ? 3 : (K == 16) ? 4 : 5;
   static_assert((1 << S) == K, "K must be a power of two <= 32");
   int idx = 0;
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
-    const int m = 32 >> s;
-    constexpr int dummy = 0;
-    (void)dummy;
-    const int half = K >> (s + 1);
-    const bool up = (lane & m) != 0;
-#pragma unroll
-    for (int q = 0; q < (K >> (s + 1)); ++q) {
-      const double send = up ? v[q] : v[q + half];
-      const double keep = up ? v[q + half] : v[q];
-      v[q] = keep + shfl_xor_d(send, m);
-    }
-    idx += up ? half : 0;
-  }
-#pragma unroll
-  for (int m = (32 >> S); m >= 1; m >>= 1) v[0] += shfl_xor_d(v[0], m);
+  if constexpr (S >= 1) fold_step<32, K / 2>(v, lane, idx);
+  if constexpr (S >= 2) fold_step<16, K / 4>(v, lane, idx);
+  if constexpr (S >= 3) fold_step<8, K / 8>(v, lane, idx);
+  if constexpr (S >= 4) fold_step<4, K / 16>(v, lane, idx);
+  if constexpr (S >= 5) fold_step<2, K / 32>(v, lane, idx);
+  if constexpr (S < 1) v[0] = fold_all<32>(v[0]);
+  if constexpr (S < 2) v[0] = fold_all<16>(v[0]);
+  if constexpr (S < 3) v[0] = fold_all<8>(v[0]);
+  if constexpr (S < 4) v[0] = fold_all<4>(v[0]);
+  if constexpr (S < 5) v[0] = fold_all<2>(v[0]);
+  v[0] = fold_all<1>(v[0]);
   if ((lane & ((64 >> S) - 1)) == 0) red[idx] = v[0];
 }
 
@@ -118,42 +177,41 @@ struct Radial {
   double cK;   // √5/ℓ, √3/ℓ, 1/ℓ  (Matérn) ; 1/ℓ² (SE)
 };
 
-__device__ __forceinline__ void rad_psi(const Radial& k, double rho, double& psi, double& dpsi) {
-  if (k.kind == 0) {
-    const double s = k.cK * rho, e = xexp(-s);
-    psi = (1.0 + s * (1.0 + s / 3.0)) * e;
-    dpsi = -k.cK * (s / 3.0) * (1.0 + s) * e;
-  } else if (k.kind == 1) {
-    const double s = k.cK * rho, e = xexp(-s);
-    psi = (1.0 + s) * e;
-    dpsi = -k.cK * s * e;
-  } else if (k.kind == 2) {
-    const double e = xexp(-k.cK * rho);
+// ψ(ρ), g1 = ψ'(ρ)/ρ and g2 = (ψ''(ρ) − ψ'(ρ)/ρ)/ρ² from ρ², so that
+//   k(r) = ψ,   ∇k(r) = g1·r,   ∇²k(r) = g2·r rᵀ + g1·I.
+// The closed forms cancel the 1/ρ factors for Matérn-5/2 and SE (no division, no ρ = 0
+// branch); Matérn-3/2 and -1/2 keep one reciprocal.  At ρ = 0, g1 = ψ''(0) and g2 = 0 — the
+// reference's ρ = 0 branches (∇k = 0, ∇²k = ψ''(0)·I).
+__device__ __forceinline__ void rad_eval(const Radial& k, double rho2, double& psi, double& g1, double& g2) {
+  const double c = k.cK;
+  if (k.kind == 3) {
+    const double e = xexp(-0.5 * c * rho2);
     psi = e;
-    dpsi = -k.cK * e;
-  } else {
-    const double e = xexp(-0.5 * rho * rho * k.cK);
-    psi = e;
-    dpsi = -(rho * k.cK) * e;
+    g1 = -c * e;
+    g2 = c * c * e;
+    return;
   }
-}
-__device__ __forceinline__ void rad_psi12(const Radial& k, double rho, double& dpsi, double& d2psi) {
+  const double rho = sqrt(rho2);
+  const double s = c * rho, e = xexp(-s);
   if (k.kind == 0) {
-    const double s = k.cK * rho, e = xexp(-s);
-    dpsi = -k.cK * (s / 3.0) * (1.0 + s) * e;
-    d2psi = k.cK * k.cK * (s * s - s - 1.0) * e / 3.0;
+    const double c23 = c * c * (1.0 / 3.0);
+    psi = fma(s, fma(s, 1.0 / 3.0, 1.0), 1.0) * e;
+    g1 = -c23 * (1.0 + s) * e;
+    g2 = c23 * (c * c) * e;
   } else if (k.kind == 1) {
-    const double s = k.cK * rho, e = xexp(-s);
-    dpsi = -k.cK * s * e;
-    d2psi = k.cK * k.cK * (s - 1.0) * e;
-  } else if (k.kind == 2) {
-    const double e = xexp(-k.cK * rho);
-    dpsi = -k.cK * e;
-    d2psi = k.cK * k.cK * e;
+    psi = (1.0 + s) * e;
+    g1 = -(c * c) * e;
+    g2 = (rho > 0.0) ? (c * c * c) * e / rho : 0.0;
   } else {
-    const double e = xexp(-0.5 * rho * rho * k.cK);
-    dpsi = -(rho * k.cK) * e;
-    d2psi = (rho * rho * k.cK * k.cK - k.cK) * e;
+    psi = e;
+    if (rho > 0.0) {
+      const double ir = 1.0 / rho;
+      g1 = -c * e * ir;
+      g2 = ((c * c) * e - g1) * (ir * ir);
+    } else {
+      g1 = c * c;
+      g2 = 0.0;
+    }
   }
 }
 
@@ -168,16 +226,18 @@ __device__ __forceinline__ EIp ei_partials(double mu, double sig, double theta, 
     return e;
   }
   const double imp = fmin - mu - theta;
-  const double z = imp / sig;
-  const double Phi = xerfc(-z * 0.7071067811865476) / 2.0;
-  const double phi = xexp(-(z * z) / 2.0) * 0.3989422804014327;
+  const double isig = 1.0 / sig;
+  const double z = imp * isig;
+  const double Phi = 0.5 * xerfc(-z * 0.7071067811865476);
+  const double phi = xexp(-0.5 * (z * z)) * 0.3989422804014327;
+  const double pis = phi * isig;
   e.g = imp * Phi + sig * phi;
   e.gmu = -Phi;
   e.gsig = phi;
-  e.gmumu = phi / sig;
-  e.gsigsig = z * z * phi / sig;
-  e.gmuth = phi / sig;
-  e.gsigth = z * phi / sig;
+  e.gmumu = pis;
+  e.gsigsig = z * z * pis;
+  e.gmuth = pis;
+  e.gsigth = z * pis;
   return e;
 }
 // first partials only, at (μ', σ') -- the perturbation "second-order" coefficients (Q7, Q8)

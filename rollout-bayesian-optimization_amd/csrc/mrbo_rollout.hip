@@ -68,8 +68,18 @@ struct Lay {
   static constexpr int U_NP = U_NG + D;                  // Newton direction p    D
   static constexpr int U_LB = U_NP + D;                  // box lower bounds      D
   static constexpr int U_UB = U_LB + D;                  // box upper bounds      D
-  static constexpr int U_SIZE = ((U_UB + D) + 1) & ~1;
-  static constexpr int WAVE_LDS = BROWS * BS + REDN + U_SIZE;
+  static constexpr int U_HF = U_UB + D;                  // fantasy rows: [x - X_r (D), g1, g2]  FMAX×(D+2)
+  static constexpr int U_SIZE = ((U_HF + FMAX * (D + 2)) + 1) & ~1;
+  static constexpr int G12 = 2 * NR;                     // per-lane [g1, g2] of the base rows
+  static constexpr int WAVE_LDS = BROWS * BS + REDN + U_SIZE + G12;
+  // L0⁻¹ in LDS, shared by the waves of a workgroup.  RPL == 1: dense zero-padded square,
+  // column-major with odd leading dimension LD = NR + 1, so the column walk (forward product,
+  // lane i reads [i][j]) and the row walk (backward product, lane i reads [k][i]) are both
+  // bank-conflict free and neither needs a triangle mask.  RPL > 1: packed triangle (the
+  // square would not fit next to the per-wave areas).
+  static constexpr bool SQ = (RPL == 1);
+  static constexpr int LD = NR + 1;
+  static constexpr long long LINV_DOUBLES = ((SQ ? (long long)NR * LD : linv_size(NR)) + 1) & ~1LL;
 };
 // scalar slots in U_SC
 enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, SC_GSIG = 6, SC_GMUMU = 7,
@@ -82,7 +92,8 @@ struct WaveCtx {
   double* B;            // LDS: BROWS × BS
   double* red;          // LDS: REDN
   double* U;            // LDS: U_SIZE
-  const double* Linv;   // LDS: packed L0⁻¹
+  const double* Linv;   // LDS: L0⁻¹ (Lay::SQ layout)
+  double* G12;          // LDS: per-lane [g1, g2] of the base rows (FULL / RICH evaluations)
   double* E;            // global: FMAX × NR   inverse-factor fantasy rows (base columns)
   double* C;            // global: (FMAX+1) × NR  base part of c for surfaces -1..h
   double X0[RPL][D];    // own base rows
@@ -109,12 +120,6 @@ struct LaneRes {
   double P[RPL][D];
   double cb[RPL];
 };
-
-// Linv(k, i), k ≥ i, from the packed layout
-template <int D, int RPL>
-__device__ __forceinline__ double linv_at(const WaveCtx<D, RPL>& W, int k, int i) {
-  return W.Linv[linv_colstart(i, W.Npad) + (k - i)];
-}
 
 // ================================================================================
 // eval(fs, x, θ; fantasy_index = S)  -- radial_basis_surrogates.jl:482-581
@@ -155,13 +160,16 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     double r[D], rho2 = 0.0;
 #pragma unroll
     for (int a = 0; a < D; ++a) { r[a] = x[a] - W.X0[s][a]; rho2 = fma(r[a], r[a], rho2); }
-    const double rho = sqrt(rho2);
-    double psi, dpsi;
-    rad_psi(W.rad, rho, psi, dpsi);
+    double psi, g1, g2;
+    rad_eval(W.rad, rho2, psi, g1, g2);
     const bool v = W.valid[s];
     Bown[s][0] = v ? psi : 0.0;
 #pragma unroll
-    for (int a = 0; a < D; ++a) Bown[s][1 + a] = (v && rho > 0.0) ? dpsi * (r[a] / rho) : 0.0;
+    for (int a = 0; a < D; ++a) Bown[s][1 + a] = v ? g1 * r[a] : 0.0;
+    if (mode >= EV_FULL) {  // kept for the Hessian (phase 6)
+      W.G12[2 * (lane + WAVE * s)] = g1;
+      W.G12[2 * (lane + WAVE * s) + 1] = g2;
+    }
     double* row = B + (lane + WAVE * s) * BS;
     if (all_cols) {
 #pragma unroll
@@ -170,17 +178,23 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       row[0] = Bown[s][0];
     }
   }
-  if (lane < nf) {  // fantasy rows B[N + r]
+  if (lane < nf) {  // fantasy rows B[N + r]; [x − X_r, g1, g2] kept for the Hessian
     double r[D], rho2 = 0.0;
 #pragma unroll
     for (int a = 0; a < D; ++a) { r[a] = x[a] - U[Ly::U_XF + lane * D + a]; rho2 = fma(r[a], r[a], rho2); }
-    const double rho = sqrt(rho2);
-    double psi, dpsi;
-    rad_psi(W.rad, rho, psi, dpsi);
+    double psi, g1, g2;
+    rad_eval(W.rad, rho2, psi, g1, g2);
     double* row = B + (NR + lane) * BS;
     row[0] = psi;
 #pragma unroll
-    for (int a = 0; a < D; ++a) row[1 + a] = (rho > 0.0) ? dpsi * (r[a] / rho) : 0.0;
+    for (int a = 0; a < D; ++a) row[1 + a] = g1 * r[a];
+    if (mode >= EV_FULL) {
+      double* hf = U + Ly::U_HF + lane * (D + 2);
+#pragma unroll
+      for (int a = 0; a < D; ++a) hf[a] = r[a];
+      hf[D] = g1;
+      hf[D + 1] = g2;
+    }
   }
   wave_sync();
 
@@ -191,6 +205,16 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
 #pragma unroll
     for (int c = 0; c < D1; ++c) acc[s][c] = 0.0;
   const int N = W.N;
+  // L0⁻¹[i][j] for this lane's rows; zero above the diagonal and on padded rows
+  auto lfwd = [&](int s, int j) -> double {
+    if constexpr (Ly::SQ) {
+      return W.Linv[j * Ly::LD + lane];
+    } else {
+      const int i = lane + WAVE * s;
+      const double l = W.Linv[linv_colstart(j, W.Npad) - j + (i > j ? i : j)];
+      return (i >= j) ? l : 0.0;
+    }
+  };
   if (all_cols) {
 #pragma unroll 4
     for (int j = 0; j < N; ++j) {
@@ -198,26 +222,19 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       double bv[D1];
 #pragma unroll
       for (int c = 0; c < D1; ++c) bv[c] = bj[c];
-      const long long cs = linv_colstart(j, W.Npad) - j;
 #pragma unroll
       for (int s = 0; s < RPL; ++s) {
-        const int i = lane + WAVE * s;
-        const double l = (i >= j && W.valid[s]) ? W.Linv[cs + i] : 0.0;
+        const double l = lfwd(s, j);
 #pragma unroll
         for (int c = 0; c < D1; ++c) acc[s][c] = fma(l, bv[c], acc[s][c]);
       }
     }
   } else {
-#pragma unroll 4
+#pragma unroll 8
     for (int j = 0; j < N; ++j) {
       const double b0 = B[j * BS];
-      const long long cs = linv_colstart(j, W.Npad) - j;
 #pragma unroll
-      for (int s = 0; s < RPL; ++s) {
-        const int i = lane + WAVE * s;
-        const double l = (i >= j && W.valid[s]) ? W.Linv[cs + i] : 0.0;
-        acc[s][0] = fma(l, b0, acc[s][0]);
-      }
+      for (int s = 0; s < RPL; ++s) acc[s][0] = fma(lfwd(s, j), b0, acc[s][0]);
     }
   }
 
@@ -338,7 +355,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   }
   if (mode == EV_VALUE) { wave_sync(); return; }
   if (lane < D) {
-    const double gs = -U[Ly::U_G + (1 + lane) * D1] / sig;       // ∇σ = -(∇kx·w)/σ
+    const double gs = -U[Ly::U_G + (1 + lane) * D1] * (1.0 / sig);  // ∇σ = -(∇kx·w)/σ
     const double gm = U[Ly::U_GMU + lane];
     U[Ly::U_GSIG + lane] = gs;
     U[Ly::U_GAL + lane] = e.gmu * gm + e.gsig * gs;                // ∇αx :567
@@ -366,11 +383,17 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
 #pragma unroll
       for (int a = 0; a < D; ++a) pv[s][a] = 0.0;
     }
-    // lane i walks column i of L0⁻¹ in a wave-uniform k loop: Y[k] is an LDS broadcast and the
-    // packed-column addresses colstart(i)+k-i form a bank permutation (Npad ≡ 0 mod 32)
-    const double* colp[RPL];
-#pragma unroll
-    for (int s = 0; s < RPL; ++s) colp[s] = W.Linv + linv_colstart(lane + WAVE * s, W.Npad) - (lane + WAVE * s);
+    // lane i walks column i of L0⁻¹ (= row i of L0⁻ᵀ) in a wave-uniform k loop; Y[k] is an
+    // LDS broadcast.  L0⁻¹[k][i] is zero for k < i and on padded rows.
+    auto lbwd = [&](int s, int k) -> double {
+      if constexpr (Ly::SQ) {
+        return W.Linv[lane * Ly::LD + k];
+      } else {
+        const int i = lane + WAVE * s;
+        const double l = W.Linv[linv_colstart(i, W.Npad) - i + (k > i ? k : i)];
+        return (k >= i) ? l : 0.0;
+      }
+    };
     if (rich) {
 #pragma unroll 2
       for (int k = 0; k < N; ++k) {
@@ -380,23 +403,18 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
         for (int c = 0; c < D1; ++c) yv[c] = yk[c];
 #pragma unroll
         for (int s = 0; s < RPL; ++s) {
-          const int i = lane + WAVE * s;
-          const double l = (k >= i && W.valid[s]) ? colp[s][k] : 0.0;
+          const double l = lbwd(s, k);
           wv[s] = fma(l, yv[0], wv[s]);
 #pragma unroll
           for (int a = 0; a < D; ++a) pv[s][a] = fma(l, yv[1 + a], pv[s][a]);
         }
       }
     } else {
-#pragma unroll 4
+#pragma unroll 8
       for (int k = 0; k < N; ++k) {
         const double y0 = B[k * BS];
 #pragma unroll
-        for (int s = 0; s < RPL; ++s) {
-          const int i = lane + WAVE * s;
-          const double l = (k >= i && W.valid[s]) ? colp[s][k] : 0.0;
-          wv[s] = fma(l, y0, wv[s]);
-        }
+        for (int s = 0; s < RPL; ++s) wv[s] = fma(lbwd(s, k), y0, wv[s]);
       }
     }
     // fantasy part: + Σ_r E[r][i] Yf[r]
@@ -433,30 +451,17 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   if (mode == EV_DRAW) { wave_sync(); return; }
 
   // ---- 6. Hessian  Hα = gμμ∇μ∇μ' + gσσ∇σ∇σ' − (gσ/σ)(∇σ∇σ' + ∇kx·Dw) + Σ_j coef_j Hk_j
-  const double gsig_over = (e.gsig == 0.0) ? 0.0 : e.gsig / sig;
+  // Σ_i coef_i ∇²k(x − X_i) with ∇²k = g2·r rᵀ + g1·I (g1, g2 kept from phase 1)
+  const double gsig_over = (e.gsig == 0.0) ? 0.0 : e.gsig * (1.0 / sig);
   {
     double nv[RPL][D], ca[RPL], tb[RPL];
 #pragma unroll
     for (int s = 0; s < RPL; ++s) {
-      double r[D], rho2 = 0.0;
 #pragma unroll
-      for (int a = 0; a < D; ++a) { r[a] = x[a] - W.X0[s][a]; rho2 = fma(r[a], r[a], rho2); }
-      const double rho = sqrt(rho2);
+      for (int a = 0; a < D; ++a) nv[s][a] = x[a] - W.X0[s][a];
       const double coef = W.valid[s] ? (e.gmu * lr.cb[s] - gsig_over * lr.w[s]) : 0.0;
-      if (rho > 0.0) {
-        double dpsi, d2psi;
-        rad_psi12(W.rad, rho, dpsi, d2psi);
-        const double Dpr = dpsi / rho;
-        ca[s] = coef * (d2psi - Dpr);
-        tb[s] = coef * Dpr;
-#pragma unroll
-        for (int a = 0; a < D; ++a) nv[s][a] = r[a] / rho;
-      } else {
-        ca[s] = 0.0;
-        tb[s] = coef * kp.d2psi0;
-#pragma unroll
-        for (int a = 0; a < D; ++a) nv[s][a] = 0.0;
-      }
+      ca[s] = coef * W.G12[2 * (lane + WAVE * s) + 1];
+      tb[s] = coef * W.G12[2 * (lane + WAVE * s)];
     }
     wave_sync();  // previous users of red are done (all lanes passed phase 4)
 #pragma unroll
@@ -491,22 +496,12 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     const double gma = U[Ly::U_GMU + a], gmb = U[Ly::U_GMU + b];
     const double gsa = U[Ly::U_GSIG + a], gsb = U[Ly::U_GSIG + b];
     double hv = red[lane] + ((a == b) ? red[Ly::NH] : 0.0);
-    // fantasy data points
+    // fantasy data points ([x − X_r, g1, g2] from phase 1)
     for (int r = 0; r < nf; ++r) {
-      double rr[D], rho2 = 0.0;
-#pragma unroll
-      for (int k = 0; k < D; ++k) { rr[k] = x[k] - U[Ly::U_XF + r * D + k]; rho2 = fma(rr[k], rr[k], rho2); }
-      const double rho = sqrt(rho2);
+      const double* hf = U + Ly::U_HF + r * (D + 2);
       const double coef = e.gmu * U[Ly::U_CF + (S + 1) * FMAX + r] - gsig_over * U[Ly::U_WF + r];
-      if (rho > 0.0) {
-        double dpsi, d2psi;
-        rad_psi12(W.rad, rho, dpsi, d2psi);
-        const double Dpr = dpsi / rho;
-        hv = fma(coef * (d2psi - Dpr), (rr[a] / rho) * (rr[b] / rho), hv);
-        if (a == b) hv = fma(coef, Dpr, hv);
-      } else if (a == b) {
-        hv = fma(coef, kp.d2psi0, hv);
-      }
+      hv = fma(coef * hf[D + 1], hf[a] * hf[b], hv);
+      if (a == b) hv = fma(coef, hf[D], hv);
     }
     hv += e.gmumu * gma * gmb + e.gsigsig * gsa * gsb - gsig_over * (gsa * gsb + U[Ly::U_G + (1 + a) * D1 + 1 + b]);
     U[Ly::U_H + a * D + b] = hv;
@@ -578,13 +573,14 @@ __device__ __forceinline__ int draw(WaveCtx<D, RPL>& W, const KParams& kp, const
     for (int k = 0; k < j; ++k) sdiag -= Lc[TRI(j, k)] * Lc[TRI(j, k)];
     if (!(sdiag > 0.0)) return 2;
     const double ljj = sqrt(sdiag);
+    const double ij = 1.0 / ljj;
     Lc[TRI(j, j)] = ljj;
 #pragma unroll
     for (int i = j + 1; i < D1; ++i) {
       double t = -U[Ly::U_G + j * D1 + i];
 #pragma unroll
       for (int k = 0; k < j; ++k) t -= Lc[TRI(i, k)] * Lc[TRI(j, k)];
-      Lc[TRI(i, j)] = t / ljj;
+      Lc[TRI(i, j)] = t * ij;
     }
   }
   double out[D1];
@@ -608,8 +604,9 @@ __device__ __forceinline__ int draw(WaveCtx<D, RPL>& W, const KParams& kp, const
 // ================================================================================
 // Inner solve: deterministic projected Newton on f = -α, surface S.
 // ================================================================================
+// packed lower Cholesky in place; idg receives the reciprocals of the diagonal
 template <int D>
-__device__ __forceinline__ bool chol_packed(double (&A)[D * (D + 1) / 2]) {
+__device__ __forceinline__ bool chol_packed(double (&A)[D * (D + 1) / 2], double (&idg)[D]) {
 #define TRI(i, j) ((i) * ((i) + 1) / 2 + (j))
   bool ok = true;
 #pragma unroll
@@ -620,12 +617,13 @@ __device__ __forceinline__ bool chol_packed(double (&A)[D * (D + 1) / 2]) {
     ok = ok && (s > 0.0);
     const double ljj = sqrt(s);
     A[TRI(j, j)] = ljj;
+    idg[j] = 1.0 / ljj;
 #pragma unroll
     for (int i = j + 1; i < D; ++i) {
       double t = A[TRI(i, j)];
 #pragma unroll
       for (int k = 0; k < j; ++k) t -= A[TRI(i, k)] * A[TRI(j, k)];
-      A[TRI(i, j)] = t / ljj;
+      A[TRI(i, j)] = t * idg[j];
     }
   }
 #undef TRI
@@ -660,7 +658,8 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
         ++t;
       }
   }
-  bool ok = chol_packed<D>(A);
+  double idg[D];
+  bool ok = chol_packed<D>(A, idg);
   if (!ok) {  // Gershgorin shift over the free block, one retry
     double tau = 0.0, hmax = 0.0;
 #pragma unroll
@@ -685,7 +684,7 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
         A[t] = (fr[i] && fr[j]) ? -U[Ly::U_H + i * D + j] + ((i == j) ? tau : 0.0) : ((i == j) ? 1.0 : 0.0);
         ++t;
       }
-    ok = chol_packed<D>(A);
+    ok = chol_packed<D>(A, idg);
   }
   double p[D];
   if (ok) {
@@ -695,14 +694,14 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
       double s = fr[i] ? U[Ly::U_NG + i] : 0.0;
 #pragma unroll
       for (int k = 0; k < i; ++k) s -= A[i * (i + 1) / 2 + k] * t1[k];
-      t1[i] = s / A[i * (i + 1) / 2 + i];
+      t1[i] = s * idg[i];
     }
 #pragma unroll
     for (int i = D - 1; i >= 0; --i) {
       double s = t1[i];
 #pragma unroll
       for (int k = i + 1; k < D; ++k) s -= A[k * (k + 1) / 2 + i] * p[k];
-      p[i] = s / A[i * (i + 1) / 2 + i];
+      p[i] = s * idg[i];
     }
 #pragma unroll
     for (int i = 0; i < D; ++i) p[i] = fr[i] ? -p[i] : 0.0;
@@ -875,11 +874,10 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
     double r[D], rho2 = 0.0;
 #pragma unroll
     for (int a = 0; a < D; ++a) { r[a] = Xq[a] - W.X0[s][a]; rho2 = fma(r[a], r[a], rho2); }
-    const double rho = sqrt(rho2);
-    double psi, dpsi;
-    rad_psi(W.rad, rho, psi, dpsi);
+    double psi, g1, g2;
+    rad_eval(W.rad, rho2, psi, g1, g2);
 #pragma unroll
-    for (int a = 0; a < D; ++a) u[s][a] = (W.valid[s] && rho > 0.0) ? dpsi * (r[a] / rho) : 0.0;
+    for (int a = 0; a < D; ++a) u[s][a] = W.valid[s] ? g1 * r[a] : 0.0;
   }
   wave_sync();
 #pragma unroll
@@ -926,13 +924,13 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
     double rr[D], rho2 = 0.0;
 #pragma unroll
     for (int a = 0; a < D; ++a) { rr[a] = Xq[a] - U[Ly::U_XF + rr_ * D + a]; rho2 = fma(rr[a], rr[a], rho2); }
-    const double rho = sqrt(rho2);
-    if (!(rho > 0.0)) continue;
-    double psi, dpsi;
-    rad_psi(W.rad, rho, psi, dpsi);
+    if (!(rho2 > 0.0)) continue;   // ∇k(0) = 0 (r = q)
+    double psi, g1, g2;
+    rad_eval(W.rad, rho2, psi, g1, g2);
     double ud = 0.0;
 #pragma unroll
-    for (int k = 0; k < D; ++k) ud = fma(dpsi * (rr[k] / rho), dl[k], ud);
+    for (int k = 0; k < D; ++k) ud = fma(rr[k], dl[k], ud);
+    ud *= g1;
     udc = fma(U[Ly::U_CF + (S + 1) * FMAX + rr_], ud, udc);
     udw = fma(U[Ly::U_WF + rr_], ud, udw);
 #pragma unroll
@@ -942,20 +940,16 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
   double rq[D], rho2 = 0.0;
 #pragma unroll
   for (int a = 0; a < D; ++a) { rq[a] = U[Ly::U_X + a] - Xq[a]; rho2 = fma(rq[a], rq[a], rho2); }
-  const double rho = sqrt(rho2);
-  double dkx = 0.0, dgkx[D];
-  if (rho > 0.0) {
-    double dpsi, d2psi;
-    rad_psi12(W.rad, rho, dpsi, d2psi);
-    const double Dpr = dpsi / rho;
-    double rd = 0.0;
+  double dkx, dgkx[D];
+  {
+    double psi, g1, g2;
+    rad_eval(W.rad, rho2, psi, g1, g2);   // ρ = 0: g1 = ψ''(0), g2 = 0
+    double dot = 0.0;
 #pragma unroll
-    for (int a = 0; a < D; ++a) { dkx -= dpsi * (rq[a] / rho) * dl[a]; rd += (rq[a] / rho) * dl[a]; }
+    for (int a = 0; a < D; ++a) dot = fma(rq[a], dl[a], dot);
+    dkx = -g1 * dot;
 #pragma unroll
-    for (int a = 0; a < D; ++a) dgkx[a] = -((d2psi - Dpr) * (rq[a] / rho) * rd + Dpr * dl[a]);
-  } else {
-#pragma unroll
-    for (int a = 0; a < D; ++a) dgkx[a] = -kp.d2psi0 * dl[a];
+    for (int a = 0; a < D; ++a) dgkx[a] = -fma(g2 * rq[a], dot, g1 * dl[a]);
   }
   const double cq = U[Ly::U_CF + (S + 1) * FMAX + q];
   const double wq = U[Ly::U_WF + q];
@@ -963,7 +957,8 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
   const double gmu = U[Ly::U_SC + SC_GMU], gsig = U[Ly::U_SC + SC_GSIG];
   const double kxdc = -(wq * udc + udw * cq);
   const double dmu = dkx * cq + kxdc;
-  const double dsig = wq * (udw - dkx) / sig;
+  const double isig = 1.0 / sig;
+  const double dsig = wq * (udw - dkx) * isig;
   double dgm, dgs;
   ei_first(dmu, dsig, kp.theta, U[Ly::U_SC + SC_FMIN], kp.sigma_tol, dgm, dgs);
   double contrib = 0.0;
@@ -975,7 +970,7 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
     const double gsa = U[Ly::U_GSIG + a];
     double da = gmu * dgmu + dgm * U[Ly::U_GMU + a] + dgs * gsa;
     if (lane < D) {
-      const double dgsig = (Pqa * udw + Pu[a] * wq - dgkx[a] * wq - Pqa * dkx - dsig * gsa) / sig;
+      const double dgsig = (Pqa * udw + Pu[a] * wq - dgkx[a] * wq - Pqa * dkx - dsig * gsa) * isig;
       da += gsig * dgsig;
     }
     contrib = fma(da, U[Ly::U_XBAR + (i_pol - 1) * D + a], contrib);
@@ -1226,12 +1221,11 @@ template <int D, int RPL>
 __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp, double* smem, int wave_in_block) {
   using Ly = Lay<D, RPL>;
   W.lane = threadIdx.x & (WAVE - 1);
-  const long long lin = linv_size(kp.Npad);
-  const long long lin_al = (lin + 1) & ~1LL;
-  double* wbase = smem + lin_al + (long long)wave_in_block * Ly::WAVE_LDS;
+  double* wbase = smem + Ly::LINV_DOUBLES + (long long)wave_in_block * Ly::WAVE_LDS;
   W.B = wbase;
   W.red = wbase + Ly::BROWS * Ly::BS;
   W.U = W.red + Ly::REDN;
+  W.G12 = W.U + Ly::U_SIZE;
   W.Linv = smem;
   const long long slot = (long long)blockIdx.x * (blockDim.x / WAVE) + wave_in_block;
   W.E = kp.work + slot * kp.work_stride;
@@ -1254,9 +1248,9 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
 template <int D, int RPL>
 __global__ void __launch_bounds__(256, MRBO_WAVES_PER_SIMD) rollout_kernel(KParams kp) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  // stage the packed L0⁻¹ once per workgroup (the only block-wide barrier)
-  const long long lin = linv_size(kp.Npad);
-  for (long long q = threadIdx.x; q < lin; q += blockDim.x) smem[q] = kp.Linv[q];
+  // stage L0⁻¹ once per workgroup (the only block-wide barrier)
+  using Ly = Lay<D, RPL>;
+  for (int q = threadIdx.x; q < (int)Ly::LINV_DOUBLES; q += blockDim.x) smem[q] = kp.Linv[q];
   __syncthreads();
   WaveCtx<D, RPL> W;
   wave_setup<D, RPL>(W, kp, smem, threadIdx.x / WAVE);
@@ -1275,8 +1269,7 @@ template <int D, int RPL>
 __global__ void __launch_bounds__(256, MRBO_WAVES_PER_SIMD) eval_base_kernel(KParams kp) {
   using Ly = Lay<D, RPL>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const long long lin = linv_size(kp.Npad);
-  for (long long q = threadIdx.x; q < lin; q += blockDim.x) smem[q] = kp.Linv[q];
+  for (int q = threadIdx.x; q < (int)Ly::LINV_DOUBLES; q += blockDim.x) smem[q] = kp.Linv[q];
   __syncthreads();
   WaveCtx<D, RPL> W;
   wave_setup<D, RPL>(W, kp, smem, threadIdx.x / WAVE);
