@@ -452,11 +452,34 @@ int mrbo_simulate_mc(mrbo_plan_t* P, const double* x0s, const double* rnstream, 
   kp.values = dvalues; kp.grad_x = with_grad ? dgx : nullptr; kp.grad_theta = with_grad ? dgt : nullptr;
   kp.status = (int*)dstatus; kp.policy = dpol; kp.obs = dobs; kp.evals = (long long*)devals;
   HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * 4, st));
+#ifdef MRBO_STAMPS
+  static unsigned long long* dstamps = nullptr;
+  if (!dstamps) HIP_TRY(hipMalloc(&dstamps, sizeof(unsigned long long) * 16));
+  HIP_TRY(hipMemsetAsync(dstamps, 0, sizeof(unsigned long long) * 16, st));
+  kp.stamps = dstamps;
+#endif
   HIP_TRY(hipEventRecord(P->ev0, st));
   launch_rollout(d, P->RPL, dim3(P->blocks), dim3(P->wpg * WAVE), P->smem, st, kp);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(P->ev1, st));
   P->timed = true;
+#ifdef MRBO_STAMPS
+  {
+    // region names follow the STAMP(W, k) sites in mrbo_rollout.hip
+    static const char* stamp_names[NSTAMP] = {"kernel rows", "forward L0^-1 B", "wave reductions", "fantasy rows+Gram+mu",
+                                              "sigma+EI partials", "backward w/P", "Hessian reductions",
+                                              "Hessian assembly", "Newton/draw bookkeeping (outside eval)",
+                                              "adjoint pair", "draw+condition", "resolve+adjoint setup"};
+    unsigned long long hs[16];
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipMemcpy(hs, dstamps, sizeof(hs), hipMemcpyDeviceToHost));
+    double tot = 0;
+    for (int k = 0; k < NSTAMP; ++k) tot += (double)hs[k];
+    for (int k = 0; k < NSTAMP; ++k)
+      fprintf(stderr, "[mrbo stamps] %-40s %6.2f%%  %.3e ticks/traj\n", stamp_names[k], 100.0 * hs[k] / tot,
+              (double)hs[k] / (double)T);
+  }
+#endif
   if (host) {
     HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipMemcpy(values, dvalues, sizeof(double) * T, hipMemcpyDeviceToHost));

@@ -55,6 +55,7 @@ struct KParams {
   long long T;          // trajectories (or points for eval_base)
   const double* pts;    // eval_base: d×P
   double* pts_out;      // eval_base output
+  unsigned long long* stamps;  // MRBO_STAMPS builds: per-region cycle totals (else null)
 };
 
 // ---- packed L0⁻¹ layout: column j holds rows j..Npad-1 contiguously ----------------------

@@ -10,7 +10,10 @@
 //   gradient(T)           rollout.jl:126-277 (adjoint back-substitution, sparse δK)
 // Numerics follow the reference formulas; the triangular solves use the explicit inverse
 // factor L⁻¹ = [[L0⁻¹,0],[E,Dinv]] instead of substitution (same maths, fp64).
+#include <utility>
+
 #include "mrbo_device.h"
+#include "bcast_asm.h"
 
 #ifndef MRBO_WAVES_PER_SIMD
 #define MRBO_WAVES_PER_SIMD 2
@@ -69,7 +72,8 @@ struct Lay {
   static constexpr int U_LB = U_NP + D;                  // box lower bounds      D
   static constexpr int U_UB = U_LB + D;                  // box upper bounds      D
   static constexpr int U_HF = U_UB + D;                  // fantasy rows: [x - X_r (D), g1, g2]  FMAX×(D+2)
-  static constexpr int U_SIZE = ((U_HF + FMAX * (D + 2)) + 1) & ~1;
+  static constexpr int U_STAMP = U_HF + FMAX * (D + 2);   // cycle accumulators (MRBO_STAMPS) 16
+  static constexpr int U_SIZE = ((U_STAMP + 16) + 1) & ~1;
   static constexpr int G12 = 2 * NR;                     // per-lane [g1, g2] of the base rows
   static constexpr int WAVE_LDS = BROWS * BS + REDN + U_SIZE + G12;
   // L0⁻¹ in LDS, shared by the waves of a workgroup.  RPL == 1: dense zero-padded square,
@@ -100,6 +104,7 @@ struct WaveCtx {
   bool valid[RPL];
   int N, Npad;
   Radial rad;
+  unsigned long long tlast;
   // opaque lane index (see evaluate): per-lane addresses are rematerialised where used
   __device__ __forceinline__ int ln() const {
     int l = lane;
@@ -113,6 +118,16 @@ struct Counters {
   long long full = 0, value = 0, rich = 0, pairs = 0;
 };
 
+// Optional per-phase cycle accounting (build with -DMRBO_STAMPS): STAMP(W, k) charges the
+// s_memtime ticks since the previous stamp to region k (accumulated by lane 0 in LDS, summed
+// into kp.stamps at kernel exit).  Regions: see mrbo_api.hip stamp_names.
+#ifdef MRBO_STAMPS
+#define STAMP(W, k) stamp_region(W, k)
+#else
+#define STAMP(W, k) ((void)0)
+#endif
+constexpr int NSTAMP = 12;
+
 // Per-lane results of an evaluation that later phases (conditioning, adjoint) need.
 template <int D, int RPL>
 struct LaneRes {
@@ -120,6 +135,61 @@ struct LaneRes {
   double P[RPL][D];
   double cb[RPL];
 };
+
+#ifdef MRBO_STAMPS
+template <int D, int RPL>
+__device__ __forceinline__ void stamp_region(WaveCtx<D, RPL>& W, int k) {
+  const unsigned long long now = __builtin_amdgcn_s_memtime();
+  if (W.lane == 0) reinterpret_cast<unsigned long long*>(W.U + Lay<D, RPL>::U_STAMP)[k] += now - W.tlast;
+  W.tlast = now;
+}
+#endif
+
+// ---- register-broadcast triangular products (RPL == 1) -----------------------------------
+// acc[c] += Σ_j L(j) · V[j][c], where row j of V lives in lane j's registers (the kernel rows
+// B for the forward product, Y for the backward one) and L(j) is this lane's L0⁻¹ entry.
+// Two permlane swaps replicate 16-row block b of V into every 16-lane row (lane t holds row
+// 16b + t); v_fmac_f64 with DPP row_newbcast:n then broadcasts row 16b + n inside each row,
+// fused into the FMA (bcast_asm.h: one software-pipelined asm statement per block).  V never goes through LDS: the only LDS traffic is one ds_read_b64 of
+// L0⁻¹ per step (the row broadcast through LDS cost 8× that and bounded the whole loop).
+
+// blocks p and p+2 of v, each replicated into all four 16-lane rows
+template <int P>
+__device__ __forceinline__ void row_blocks(double v, double& blk_p, double& blk_p2) {
+  int lo, hi;
+  dsplit(v, lo, hi);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // [r0 r0 r2 r2], [r1 r1 r3 r3]
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const int tlo = P ? a[1] : a[0], thi = P ? b[1] : b[0];
+  const auto c = __builtin_amdgcn_permlane32_swap(tlo, tlo, false, false); // [rP ×4], [rP+2 ×4]
+  const auto d = __builtin_amdgcn_permlane32_swap(thi, thi, false, false);
+  blk_p = djoin(c[0], d[0]);
+  blk_p2 = djoin(c[1], d[1]);
+}
+
+// LDS byte address of a pointer into the dynamic shared array
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// acc[c] += Σ_{j < nrows} L(j) v[c](j) with L(j) = lbase[j · JSTRIDE] (zero-padded past N).
+// Blocks run in the order 0, 2, 1, 3 (two swaps yield blocks p and p+2 together).
+template <int K, int JSTRIDE>
+__device__ __forceinline__ void bcast_product(double (&acc)[K], const double (&v)[K], const double* lbase, int nrows) {
+  const unsigned a0 = lds_addr(lbase);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    if (16 * p >= nrows) break;
+    double bp[K], bp2[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      if (p == 0) row_blocks<0>(v[c], bp[c], bp2[c]);
+      else row_blocks<1>(v[c], bp[c], bp2[c]);
+    }
+    BcastAsm<K, 8 * JSTRIDE>::run(acc, bp, a0 + 8u * 16u * p * JSTRIDE);
+    if (16 * (p + 2) < nrows) BcastAsm<K, 8 * JSTRIDE>::run(acc, bp2, a0 + 8u * 16u * (p + 2) * JSTRIDE);
+  }
+}
 
 // ================================================================================
 // eval(fs, x, θ; fantasy_index = S)  -- radial_basis_surrogates.jl:482-581
@@ -139,6 +209,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   double* B = W.B;
   double* red = W.red;
   const bool all_cols = (mode != EV_VALUE);
+  STAMP(W, 8);
 
   double x[D];
 #pragma unroll
@@ -170,12 +241,14 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       W.G12[2 * (lane + WAVE * s)] = g1;
       W.G12[2 * (lane + WAVE * s) + 1] = g2;
     }
-    double* row = B + (lane + WAVE * s) * BS;
-    if (all_cols) {
+    if constexpr (!Ly::SQ) {   // the LDS row-broadcast path reads the base rows from B
+      double* row = B + (lane + WAVE * s) * BS;
+      if (all_cols) {
 #pragma unroll
-      for (int c = 0; c < D1; ++c) row[c] = Bown[s][c];
-    } else {
-      row[0] = Bown[s][0];
+        for (int c = 0; c < D1; ++c) row[c] = Bown[s][c];
+      } else {
+        row[0] = Bown[s][0];
+      }
     }
   }
   if (lane < nf) {  // fantasy rows B[N + r]; [x − X_r, g1, g2] kept for the Hessian
@@ -197,6 +270,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     }
   }
   wave_sync();
+  STAMP(W, 0);
 
   // ---- 2. forward product  Y[i] = Σ_{j ≤ i} L0⁻¹[i,j] B[j]   (L\kxX' , r_b_s.jl:525-526)
   double acc[RPL][D1];
@@ -205,6 +279,15 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
 #pragma unroll
     for (int c = 0; c < D1; ++c) acc[s][c] = 0.0;
   const int N = W.N;
+  if constexpr (Ly::SQ) {
+    // lane i reads L0⁻¹[i][j] at j·LD + i
+    if (all_cols) bcast_product<D1, Ly::LD>(acc[0], Bown[0], W.Linv + lane, N);
+    else {
+      double a1[1] = {0.0}, v1[1] = {Bown[0][0]};
+      bcast_product<1, Ly::LD>(a1, v1, W.Linv + lane, N);
+      acc[0][0] = a1[0];
+    }
+  } else {
   // L0⁻¹[i][j] for this lane's rows; zero above the diagonal and on padded rows
   auto lfwd = [&](int s, int j) -> double {
     if constexpr (Ly::SQ) {
@@ -237,7 +320,9 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       for (int s = 0; s < RPL; ++s) acc[s][0] = fma(lfwd(s, j), b0, acc[s][0]);
     }
   }
+  }
 
+  STAMP(W, 1);
   // ---- 3. per-lane products and wave reductions
   {
     double v[8];
@@ -299,6 +384,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     }
   }
   wave_sync();
+  STAMP(W, 2);
 
   // ---- 4. fantasy rows of the forward product: Yf = Fpart + Dinv · Bf   (lane = (r, c))
   {
@@ -333,6 +419,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     }
   }
   wave_sync();
+  STAMP(W, 3);
 
   // ---- σ, EI partials (all lanes, wave-uniform values)
   const double mu = U[Ly::U_SC + SC_MU];
@@ -353,7 +440,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     U[Ly::U_SC + SC_GSIGTH] = e.gsigth;
     U[Ly::U_SC + SC_FMIN] = fmin;
   }
-  if (mode == EV_VALUE) { wave_sync(); return; }
+  if (mode == EV_VALUE) { wave_sync(); STAMP(W, 4); return; }
   if (lane < D) {
     const double gs = -U[Ly::U_G + (1 + lane) * D1] * (1.0 / sig);  // ∇σ = -(∇kx·w)/σ
     const double gm = U[Ly::U_GMU + lane];
@@ -362,19 +449,22 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     U[Ly::U_MIX + lane] = gm * e.gmuth + gs * e.gsigth;            // d2α_dxdθ :575-577
   }
 
+  STAMP(W, 4);
   // ---- 5. backward product w = L⁻ᵀ v (and P = L⁻ᵀ V for the adjoint)
   // stash Y rows (base) into B, then lane i walks column i of L0⁻¹
   const bool rich = (mode == EV_RICH);
+  if constexpr (!Ly::SQ) {
 #pragma unroll
-  for (int s = 0; s < RPL; ++s) {
-    double* row = B + (lane + WAVE * s) * BS;
-    row[0] = acc[s][0];
-    if (rich) {
+    for (int s = 0; s < RPL; ++s) {
+      double* row = B + (lane + WAVE * s) * BS;
+      row[0] = acc[s][0];
+      if (rich) {
 #pragma unroll
-      for (int a = 0; a < D; ++a) row[1 + a] = acc[s][1 + a];
+        for (int a = 0; a < D; ++a) row[1 + a] = acc[s][1 + a];
+      }
     }
+    wave_sync();
   }
-  wave_sync();
   {
     double wv[RPL], pv[RPL][D];
 #pragma unroll
@@ -383,6 +473,22 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
 #pragma unroll
       for (int a = 0; a < D; ++a) pv[s][a] = 0.0;
     }
+    if constexpr (Ly::SQ) {
+      // lane i reads L0⁻¹[k][i] at i·LD + k; Y rows broadcast from registers
+      if (rich) {
+        double a7[D1];
+#pragma unroll
+        for (int c = 0; c < D1; ++c) a7[c] = 0.0;
+        bcast_product<D1, 1>(a7, acc[0], W.Linv + lane * Ly::LD, N);
+        wv[0] = a7[0];
+#pragma unroll
+        for (int a = 0; a < D; ++a) pv[0][a] = a7[1 + a];
+      } else {
+        double a1[1] = {0.0}, v1[1] = {acc[0][0]};
+        bcast_product<1, 1>(a1, v1, W.Linv + lane * Ly::LD, N);
+        wv[0] = a1[0];
+      }
+    } else {
     // lane i walks column i of L0⁻¹ (= row i of L0⁻ᵀ) in a wave-uniform k loop; Y[k] is an
     // LDS broadcast.  L0⁻¹[k][i] is zero for k < i and on padded rows.
     auto lbwd = [&](int s, int k) -> double {
@@ -417,6 +523,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
         for (int s = 0; s < RPL; ++s) wv[s] = fma(lbwd(s, k), y0, wv[s]);
       }
     }
+    }
     // fantasy part: + Σ_r E[r][i] Yf[r]
 #pragma unroll
     for (int s = 0; s < RPL; ++s) {
@@ -448,7 +555,8 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       if (c == 0) U[Ly::U_WF + q] = t; else U[Ly::U_PF + q * D + c - 1] = t;
     }
   }
-  if (mode == EV_DRAW) { wave_sync(); return; }
+  if (mode == EV_DRAW) { wave_sync(); STAMP(W, 5); return; }
+  STAMP(W, 5);
 
   // ---- 6. Hessian  Hα = gμμ∇μ∇μ' + gσσ∇σ∇σ' − (gσ/σ)(∇σ∇σ' + ∇kx·Dw) + Σ_j coef_j Hk_j
   // Σ_i coef_i ∇²k(x − X_i) with ∇²k = g2·r rᵀ + g1·I (g1, g2 kept from phase 1)
@@ -488,6 +596,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     }
   }
   wave_sync();
+  STAMP(W, 6);
   if (lane < Ly::NH) {
     int a = 0, rem = lane;
 #pragma unroll
@@ -508,6 +617,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     U[Ly::U_H + b * D + a] = hv;
   }
   wave_sync();
+  STAMP(W, 7);
 }
 
 // ================================================================================
@@ -864,6 +974,7 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
   double* red = W.red;
   const int lane = W.ln();
   const int nf = S + 1;
+  STAMP(W, 8);
   double Xq[D];
 #pragma unroll
   for (int a = 0; a < D; ++a) Xq[a] = U[Ly::U_XF + q * D + a];
@@ -903,7 +1014,7 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
     wave_reduce<16>(v, red + 16 * ch, lane);
   }
   wave_sync();
-  if (lane > D) return;
+  if (lane > D) { STAMP(W, 9); return; }
   // direction δ: e_lane (spatial) or δx (data, lane D).  Needed: u·c, u·w and Pᵀu for
   // u_a = ∇k(X_q − X_a)·δ over the surface's data; base rows come from the reduction, the
   // fantasy rows r ≤ S are added here (∇k(X_q − X_q) = 0 drops r = q).
@@ -977,6 +1088,7 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
   }
   if (lane < D) U[Ly::U_ACC + q * D + lane] += contrib;
   else U[Ly::U_YBAR + q] += contrib;
+  STAMP(W, 9);
 }
 
 // small LU with partial pivoting (Julia det / \ on a Matrix), all lanes redundantly.
@@ -1098,6 +1210,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
     if (st) break;
     wave_sync();
     st |= condition<D, RPL>(W, kp, S, yv, gy, lr);
+    STAMP(W, 10);
     if (st) break;
   }
   wave_sync();
@@ -1112,6 +1225,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
     if (kp.grad_x && lane < D) kp.grad_x[oidx * D + lane] = NAN;
     return;
   }
+  STAMP(W, 11);
   // resolve (observables.jl:12-14, Q3)
   double bo = U[Ly::U_YF];
   int t = 0;
@@ -1212,6 +1326,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
     kp.evals[4 * base + 3] = nevals.pairs;
   }
   wave_sync();
+  STAMP(W, 11);
 }
 
 // ================================================================================
@@ -1255,6 +1370,9 @@ __global__ void __launch_bounds__(256, MRBO_WAVES_PER_SIMD) rollout_kernel(KPara
   WaveCtx<D, RPL> W;
   wave_setup<D, RPL>(W, kp, smem, threadIdx.x / WAVE);
   wave_sync();
+#ifdef MRBO_STAMPS
+  W.tlast = __builtin_amdgcn_s_memtime();
+#endif
   for (;;) {
     long long tr = 0;
     if (W.lane == 0) tr = atomicAdd(kp.queue, 1);
@@ -1262,6 +1380,11 @@ __global__ void __launch_bounds__(256, MRBO_WAVES_PER_SIMD) rollout_kernel(KPara
     if (tr >= kp.T) break;
     trajectory<D, RPL>(W, kp, tr);
   }
+#ifdef MRBO_STAMPS
+  if (kp.stamps && W.lane == 0)
+    for (int k = 0; k < NSTAMP; ++k)
+      atomicAdd(kp.stamps + k, reinterpret_cast<unsigned long long*>(W.U + Lay<D, RPL>::U_STAMP)[k]);
+#endif
 }
 
 // eval(s, x, θ) on the base surrogate for P points (fixture / primitive parity path)
