@@ -117,8 +117,7 @@ def main():
         dx0.copy_(torch.from_numpy(x0.ravel(order="F")), non_blocking=False)
         plan.simulate(dx0, drn, dxs, out)
         sums = plan.partial_sums(out, hi - lo)
-        if timed:
-            evals_acc.add_(out["evals"])
+        evals_acc.add_(out["evals"])        # also in warmup: no first-use op inside the timed region
         parallel.allreduce_sums(sums)
         s = sums.cpu().numpy().reshape((W, R), order="F")
         eto = parallel.eto_from_sums(s, M_total, d)
@@ -136,6 +135,7 @@ def main():
 
     for _ in range(args.warmup):
         step(False)
+    evals_acc.zero_()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -154,7 +154,7 @@ def main():
     elapsed = float(el.item())
 
     st = out["status"].cpu().numpy()
-    ev = evals_acc.cpu().numpy().reshape((4, hi - lo, R), order="F") / max(args.steps, 1)
+    ev = evals_acc.cpu().numpy().reshape((flops.NCOUNTERS, hi - lo, R), order="F") / max(args.steps, 1)
     fl = flops.launch_flops(ev, cfg.N, d, h)
     kms = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
     achieved = fl / (kms * 1e-3) / 1e12
@@ -187,8 +187,9 @@ def main():
                      "note": "compute-bound fp64 FMA (VALU); algorithmic FLOP model in DESIGN.md §5; "
                              "HBM algorithmic bytes/traj ~0.3 KB so an HBM roofline does not bind"},
         "status_errors": int((st != 0).sum()),
-        "work_per_traj": {"full_evals": float(ev[0].mean()), "value_evals": float(ev[1].mean()),
-                          "rich_evals": float(ev[2].mean()), "pairs": float(ev[3].mean())},
+        "work_per_traj": {"grad_evals": float(ev[0].mean()), "value_evals": float(ev[1].mean()),
+                          "hessians": float(ev[2].mean()), "rich_evals": float(ev[3].mean()),
+                          "pairs": float(ev[4].mean())},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(pb, M_local, R, args.cpu_seconds)

@@ -126,13 +126,17 @@ int mrbo_plan_destroy(mrbo_plan_t* plan);
  *   status     M×R          MRBO_ST_* bits
  *   policy_x   d×(h+1)×M×R or NULL: x_0..x_h of every trajectory (fs.X[:, N+1:N+h+1])
  *   obs        (h+1)×M×R or NULL:   sampled observations y_0..y_h
- *   evals      4×M×R or NULL: per trajectory [full evals, value-only evals, adjoint rich evals,
- *              adjoint perturbation pairs] -- the work counters of the FLOP roofline model
+ *   evals      MRBO_NCOUNTERS×M×R or NULL: per trajectory [gradient evals, value-only evals,
+ *              Hessian completions, adjoint rich evals, adjoint perturbation pairs] -- the work
+ *              counters of the FLOP roofline model (inner-solve counts are identical to the
+ *              oracle's: same lazy Newton iteration)
  * Launches on `stream` (hipStream_t, may be NULL) and returns without synchronising.       */
 int mrbo_simulate_mc(mrbo_plan_t* plan, const double* x0s, const double* rnstream, const double* xstarts,
                      const double* dual_y_dx, const double* replay_x, double* values, double* grad_x,
                      double* grad_theta, int32_t* status, double* policy_x, double* obs, int64_t* evals,
                      uint32_t flags, void* stream);
+
+#define MRBO_NCOUNTERS 5
 
 /* ExpectedTrajectoryOutput per restart: eto R×W (row-major per restart, W = 2+2d+2):
  * [μxθ, σ_μxθ, ∇μx(d), σ_∇μx(d), ∇μθ, σ_∇μθ]; std uses n-1 (Q14).                     */

@@ -144,7 +144,7 @@ def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=
     policy = np.zeros((d, h + 1, M, R), order="F") if want_policy else None
     obs = np.zeros((h + 1, M, R), order="F")
     eto = np.zeros((2 + 2 * d + 2, R), order="F")
-    evals = np.zeros((M, R), dtype=np.int64, order="F")
+    evals = np.zeros((3, M, R), dtype=np.int64, order="F")   # [grad, value, hess] per trajectory
     dy = None if dual_y_dx is None else _f64(dual_y_dx)
     rp = None if replay_x is None else _f64(replay_x)
     rc = lib().rbo_simulate_mc(ctypes.byref(osur.s), ctypes.byref(prm), _p(x0s), _p(rnstream), _p(xstarts),

@@ -566,10 +566,55 @@ static int fsur_draw(const fsur_t* fs, const double* x, double theta, double sig
  * Optim IPNewton per start (:1-33), x_tol = f_tol = 1e-3.  IPNewton is absent here; the
  * build defines the deterministic projected Newton of DESIGN.md §4 (same on the GPU).
  * ---------------------------------------------------------------------------------- */
-typedef struct { const fsur_t* fs; const rbo_params* p; int fi; scratch_t* sc; int64_t evals; int st; } solve_ctx;
+/* n_grad / n_value / n_hess: evaluations the lazy iteration needs (below) -- the same counts
+ * the GPU kernel reports, so tests can assert identical Newton work. */
+typedef struct {
+  const fsur_t* fs;
+  const rbo_params* p;
+  int fi;
+  scratch_t* sc;
+  int64_t n_grad, n_value, n_hess;
+  int st;
+  double cabs; /* Σ|c| of the surface (grad_certified) */
+} solve_ctx;
+
+/* max_ρ |ψ'(ρ)| (+1%) and √(ψ(0)·(−ψ''(0))) (+1%; -1 when ψ''(0) > 0, Matérn-1/2) -- the
+ * constants of the gradient certificate, in closed form. */
+static void k_gcert(const kern_t* k, double* gmu, double* gsig) {
+  const double d2 = k_d2psi(k, 0.0);
+  switch (k->kind) {
+    case RBO_K_MATERN52: {
+      const double c = sqrt(5.0) / k->ell, s = 0.5 * (1.0 + sqrt(5.0));
+      *gmu = 1.01 * c * (s / 3.0) * (1.0 + s) * exp(-s);
+      break;
+    }
+    case RBO_K_MATERN32: *gmu = 1.01 * (sqrt(3.0) / k->ell) * exp(-1.0); break;
+    case RBO_K_MATERN12: *gmu = 1.01 / k->ell; break;
+    default: *gmu = 1.01 * (1.0 / k->ell) * exp(-0.5); break;
+  }
+  *gsig = (d2 < 0) ? 1.01 * sqrt(k_psi(k, 0.0) * -d2) : -1.0;
+}
+
+/* Gradient certificate from a value-only evaluation: ‖∇α‖∞ ≤ g_tol guaranteed:
+ * |∂μ| ≤ Σ|c| max|ψ'|, |∂σ| ≤ √(ψ(0)(−ψ''(0)))/σ, factor 4 for rounding; gμ = gσ = 0 makes
+ * ∇α zero or NaN, which stops the iteration as well. */
+static int grad_certified(const solve_ctx* cx, const sx_t* sx) {
+  const double gm = sx->e.gmu, gs = sx->e.gsig;
+  if (gm == 0.0 && gs == 0.0) return 1;
+  double cmu, csig;
+  k_gcert(&cx->fs->k, &cmu, &csig);
+  if (!(csig > 0.0)) return 0;
+  const double bound = fabs(gm) * cmu * cx->cabs + gs * csig / sx->sigma;
+  return bound <= 0.25 * cx->p->g_tol;
+}
 
 static double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+/* Projected Newton with projected-Armijo backtracking.  Evaluation is lazy:
+ * every point gets a value-only evaluation; the gradient only where the certificate cannot
+ * rule out a step, the Hessian only where a step is taken.  fsur_eval in full mode yields
+ * ∇α and Hα together (the counters record what the iteration needs: n_grad, n_hess).
+ * Values are identical in either mode, so the iterates do not depend on the laziness. */
 static void newton_solve(solve_ctx* cx, const double* xs, double* xout, double* fout) {
   const fsur_t* fs = cx->fs;
   const rbo_params* p = cx->p;
@@ -578,24 +623,30 @@ static void newton_solve(solve_ctx* cx, const double* xs, double* xout, double* 
   sx_t sx;
   int free_[16];
   for (int a = 0; a < d; ++a) x[a] = clampd(xs[a], p->lbs[a], p->ubs[a]);
-  fsur_eval(fs, x, p->theta, p->sigma_tol, cx->fi, 0, &sx, cx->sc);
-  cx->evals++;
+  fsur_eval(fs, x, p->theta, p->sigma_tol, cx->fi, 1, &sx, cx->sc);
+  cx->n_value++;
   cx->st |= sx.status;
   double f = -sx.alpha;
-  for (int a = 0; a < d; ++a) g[a] = -sx.galpha[a];
-  for (int q = 0; q < d * d; ++q) H[q] = -sx.Halpha[q];
   double box = 0;
   for (int a = 0; a < d; ++a) box = fmax(box, p->ubs[a] - p->lbs[a]);
-  for (int it = 0; it < p->max_iters; ++it) {
+  int it = 0;
+  for (;;) {
+    /* decision point at x; sx holds its value-only evaluation */
+    if (it >= p->max_iters) break;
     if (isnan(f)) break;
+    if (grad_certified(cx, &sx)) break;
+    fsur_eval(fs, x, p->theta, p->sigma_tol, cx->fi, 0, &sx, cx->sc);
+    cx->n_grad++;
+    for (int a = 0; a < d; ++a) g[a] = -sx.galpha[a];
+    for (int q = 0; q < d * d; ++q) H[q] = -sx.Halpha[q];
     double pg = 0;
-    int nf = 0;
     for (int a = 0; a < d; ++a) {
       const int act = (x[a] <= p->lbs[a] && g[a] > 0) || (x[a] >= p->ubs[a] && g[a] < 0);
       free_[a] = !act;
-      if (!act) { pg = fmax(pg, fabs(g[a])); nf++; }
+      if (!act) pg = fmax(pg, fabs(g[a]));
     }
     if (!(pg > p->g_tol)) break;
+    cx->n_hess++;
     /* reduced Hessian on the free set */
     int idx[16], m = 0;
     for (int a = 0; a < d; ++a) if (free_[a]) idx[m++] = a;
@@ -627,31 +678,29 @@ static void newton_solve(solve_ctx* cx, const double* xs, double* xout, double* 
     double pn = 0;
     for (int a = 0; a < d; ++a) pn = fmax(pn, fabs(pdir[a]));
     if (pn > box) for (int a = 0; a < d; ++a) pdir[a] *= box / pn;
-    /* projected backtracking Armijo line search */
+    /* projected backtracking Armijo line search, value-only trials */
     double t = 1.0, ft = NAN;
-    int accepted = 0, ls;
-    for (ls = 0; ls < p->max_ls; ++ls) {
+    int accepted = 0;
+    for (int ls = 0; ls < p->max_ls; ++ls) {
       double dec = 0;
       for (int a = 0; a < d; ++a) {
         xt[a] = clampd(x[a] + t * pdir[a], p->lbs[a], p->ubs[a]);
         dec += g[a] * (xt[a] - x[a]);
       }
-      fsur_eval(fs, xt, p->theta, p->sigma_tol, cx->fi, ls != 0, &sx, cx->sc);
-      if (ls == 0) cx->evals++;
+      fsur_eval(fs, xt, p->theta, p->sigma_tol, cx->fi, 1, &sx, cx->sc);
+      cx->n_value++;
       cx->st |= sx.status;
       ft = -sx.alpha;
       if (!isnan(ft) && ft <= f + 1e-4 * dec) { accepted = 1; break; }
       t *= 0.5;
     }
     if (!accepted) break;
-    if (ls != 0) { fsur_eval(fs, xt, p->theta, p->sigma_tol, cx->fi, 0, &sx, cx->sc); cx->evals++; }
     double dx = 0;
     for (int a = 0; a < d; ++a) dx = fmax(dx, fabs(xt[a] - x[a]));
     const double df = fabs(ft - f);
     for (int a = 0; a < d; ++a) x[a] = xt[a];
     f = ft;
-    for (int a = 0; a < d; ++a) g[a] = -sx.galpha[a];
-    for (int q = 0; q < d * d; ++q) H[q] = -sx.Halpha[q];
+    ++it;
     if (dx <= p->x_tol || df <= p->f_tol * fabs(f)) break;
   }
   for (int a = 0; a < d; ++a) xout[a] = x[a];
@@ -659,6 +708,13 @@ static void newton_solve(solve_ctx* cx, const double* xs, double* xout, double* 
 }
 
 static int multistart(solve_ctx* cx, const double* xstarts, double* xfinal) {
+  { /* Σ|c| of the solve surface (base + fantasy coefficients) for the gradient certificate */
+    const fsur_t* fs = cx->fs;
+    const double* c = fs->cs + (int64_t)(cx->fi + 1) * fs->cap;
+    double s = 0;
+    for (int j = 0; j < fs->N + cx->fi + 1; ++j) s += fabs(c[j]);
+    cx->cabs = s;
+  }
   const int d = cx->fs->d;
   int best = -1, best_nan = -1;
   double bestf = INFINITY, xc[16], fc, xb[16];
@@ -773,11 +829,11 @@ static int run_trajectory(const traj_in* in, int r, int m, const double* x0, fsu
                           double* value, double* gx, double* gth, double* pol, double* obs_out, int64_t* evals) {
   const rbo_params* p = in->p;
   const int d = fs->d, h = p->h, M = p->M, D1 = d + 1;
-  double obs[64], grads[64 * 16], z[17], xnext[16];
+  double obs[64] = {0}, grads[64 * 16], z[17], xnext[16];
   sx_t sx;
   int st = 0;
   fsur_reset(fs);
-  solve_ctx cx = {fs, p, -1, sc, 0, 0};
+  solve_ctx cx = {fs, p, -1, sc, 0, 0, 0, 0, 0.0};
   /* StochasticObservable (observables.jl:106-121): step k uses rns[m, :, k+1], fantasy_index k-1 */
   for (int k = 0; k <= h; ++k) {
     const double* xk;
@@ -801,7 +857,9 @@ static int run_trajectory(const traj_in* in, int r, int m, const double* x0, fsu
     st |= fsur_condition(fs, xk, obs[k], sc->tmp);
     if (st) break;
   }
-  *evals = cx.evals;
+  evals[0] = cx.n_grad;
+  evals[1] = cx.n_value;
+  evals[2] = cx.n_hess;
   if (obs_out) for (int k = 0; k <= h; ++k) obs_out[k] = st ? NAN : obs[k];
   if (st) {
     *value = NAN;
@@ -941,11 +999,11 @@ int rbo_simulate_mc(const rbo_surrogate* s, const rbo_params* p, const double* x
 #pragma omp for schedule(dynamic, 1)
     for (int64_t tr = 0; tr < T; ++tr) {
       const int r = (int)(tr / M), m = (int)(tr % M);
-      int64_t ev = 0;
+      int64_t ev[3] = {0, 0, 0};
       const int st = run_trajectory(&in, r, m, x0s + (int64_t)d * r, &fs, &sc, values + tr, grad_x + (int64_t)d * tr,
-                                    grad_theta + tr, policy_x, obs ? obs + (int64_t)(h + 1) * tr : NULL, &ev);
+                                    grad_theta + tr, policy_x, obs ? obs + (int64_t)(h + 1) * tr : NULL, ev);
       status[tr] = st;
-      if (evals) evals[tr] = ev;
+      if (evals) for (int k = 0; k < 3; ++k) evals[3 * tr + k] = ev[k];
     }
     scratch_free(&sc);
     fsur_free(&fs);

@@ -94,7 +94,8 @@ int rbo_eval_base(const rbo_surrogate* s, double theta, double sigma_tol, int32_
  * dual_y_dx: optional d×h×M×R uniforms (δx of solve_dual_y call j at column j-1).
  * replay_x:  optional d×h×M×R policy points injected instead of the inner solve.
  * eto: optional R×(2+2d+2) rows [μ, σ, ∇μx(d), σ∇x(d), ∇μθ, σ∇θ].
- * newton_evals: optional M×R count of full surrogate evaluations performed. */
+ * evals: optional 3×M×R inner-solve work per trajectory [gradient evals, value-only evals,
+ *        Hessians] of the lazy Newton iteration (rbo_oracle.c newton_solve). */
 int rbo_simulate_mc(const rbo_surrogate* s, const rbo_params* p, const double* x0s,
                     const double* rnstream, const double* xstarts,
                     const double* dual_y_dx, const double* replay_x,

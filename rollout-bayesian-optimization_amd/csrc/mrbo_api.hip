@@ -46,6 +46,7 @@ struct mrbo_plan {
   std::vector<double> lbs, ubs;
   int kernel = 0;
   double ell = 1, cK = 1, psi0 = 1, d2psi0 = -1, sn2 = 1e-6;
+  double gcert_mu = 0, gcert_sig = -1;
   double fmin_base = 0, fmini = 0;
   // device state
   double* dX0 = nullptr;    // [d][NR]
@@ -134,7 +135,7 @@ void launch_evalb(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, con
 // choose waves per workgroup maximising resident waves per CU (LDS + register limits)
 int pick_grid(const void* fn, size_t linv_bytes, size_t wave_bytes, int ncu, int& wpg, int& blocks, size_t& smem) {
   int best_w = 0;
-  for (int w = 1; w <= 4; ++w) {
+  for (int w = 1; w <= 8; ++w) {
     const size_t sm = linv_bytes + w * wave_bytes;
     if (sm > 160 * 1024) break;
     int nb = 0;
@@ -238,6 +239,7 @@ static void fill_common(const mrbo_plan_t* P, KParams& kp) {
   kp.d = P->d; kp.N = P->N; kp.Npad = P->Npad; kp.h = P->p.h; kp.M = P->p.M; kp.R = P->p.R;
   kp.nstarts = P->p.nstarts;
   kp.kernel = P->kernel; kp.ell = P->ell; kp.cK = P->cK; kp.psi0 = P->psi0; kp.d2psi0 = P->d2psi0; kp.sn2 = P->sn2;
+  kp.gcert_mu = P->gcert_mu; kp.gcert_sig = P->gcert_sig;
   kp.fmin_base = P->fmin_base; kp.fmini = P->fmini; kp.theta = P->p.theta;
   kp.max_iters = P->p.max_iters; kp.max_ls = P->p.max_ls;
   kp.x_tol = P->p.x_tol; kp.f_tol = P->p.f_tol; kp.g_tol = P->p.g_tol; kp.htol = P->p.htol;
@@ -347,6 +349,15 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
     default: P->cK = 1.0 / (ell * ell); P->d2psi0 = -P->cK; break;
   }
   P->psi0 = 1.0;
+  // max_ρ |ψ'(ρ)| in closed form (+1% margin) and √(ψ(0)·(−ψ''(0))) for the gradient certificate
+  switch (P->kernel) {
+    case 0: { const double s = 0.5 * (1.0 + std::sqrt(5.0));
+              P->gcert_mu = 1.01 * P->cK * (s / 3.0) * (1.0 + s) * std::exp(-s); break; }
+    case 1: P->gcert_mu = 1.01 * P->cK * std::exp(-1.0); break;
+    case 2: P->gcert_mu = 1.01 * P->cK; break;
+    default: P->gcert_mu = 1.01 * std::sqrt(P->cK) * std::exp(-0.5); break;
+  }
+  P->gcert_sig = (P->d2psi0 < 0.0) ? 1.01 * std::sqrt(P->psi0 * -P->d2psi0) : -1.0;
 
   // L0^-1 by forward substitution on the unit columns, packed column-major (Npad rows)
   const int Npad = P->Npad;
@@ -444,7 +455,7 @@ int mrbo_simulate_mc(mrbo_plan_t* P, const double* x0s, const double* rnstream, 
         sg.in(replay_x, (size_t)d * std::max(h, 1) * T, &kp.replay) || sg.out(T, values, &dvalues) ||
         sg.out((size_t)d * T, with_grad ? grad_x : nullptr, &dgx) || sg.out(T, with_grad ? grad_theta : nullptr, &dgt) ||
         sg.out(T, status, &dstatus) || sg.out((size_t)d * (h + 1) * T, policy_x, &dpol) ||
-        sg.out((size_t)(h + 1) * T, obs, &dobs) || sg.out(4 * T, evals, &devals))
+        sg.out((size_t)(h + 1) * T, obs, &dobs) || sg.out((size_t)NCOUNT * T, evals, &devals))
       return fail(MRBO_ERR_NOMEM, "staging allocation failed");
   } else {
     kp.x0s = x0s; kp.rn = rnstream; kp.xstarts = xstarts; kp.dual_y = dual_y_dx; kp.replay = replay_x;
@@ -454,8 +465,8 @@ int mrbo_simulate_mc(mrbo_plan_t* P, const double* x0s, const double* rnstream, 
   HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * 4, st));
 #ifdef MRBO_STAMPS
   static unsigned long long* dstamps = nullptr;
-  if (!dstamps) HIP_TRY(hipMalloc(&dstamps, sizeof(unsigned long long) * 16));
-  HIP_TRY(hipMemsetAsync(dstamps, 0, sizeof(unsigned long long) * 16, st));
+  if (!dstamps) HIP_TRY(hipMalloc(&dstamps, sizeof(unsigned long long) * 20));
+  HIP_TRY(hipMemsetAsync(dstamps, 0, sizeof(unsigned long long) * 20, st));
   kp.stamps = dstamps;
 #endif
   HIP_TRY(hipEventRecord(P->ev0, st));
@@ -469,8 +480,9 @@ int mrbo_simulate_mc(mrbo_plan_t* P, const double* x0s, const double* rnstream, 
     static const char* stamp_names[NSTAMP] = {"kernel rows", "forward L0^-1 B", "wave reductions", "fantasy rows+Gram+mu",
                                               "sigma+EI partials", "backward w/P", "Hessian reductions",
                                               "Hessian assembly", "Newton/draw bookkeeping (outside eval)",
-                                              "adjoint pair", "draw+condition", "resolve+adjoint setup"};
-    unsigned long long hs[16];
+                                              "adjoint pair", "draw+condition", "resolve+adjoint setup",
+                                              "Newton accept/convergence", "Newton direction", "Newton trial point"};
+    unsigned long long hs[20];
     HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipMemcpy(hs, dstamps, sizeof(hs), hipMemcpyDeviceToHost));
     double tot = 0;
@@ -490,7 +502,7 @@ int mrbo_simulate_mc(mrbo_plan_t* P, const double* x0s, const double* rnstream, 
     }
     if (policy_x) HIP_TRY(hipMemcpy(policy_x, dpol, sizeof(double) * d * (h + 1) * T, hipMemcpyDeviceToHost));
     if (obs) HIP_TRY(hipMemcpy(obs, dobs, sizeof(double) * (h + 1) * T, hipMemcpyDeviceToHost));
-    if (evals) HIP_TRY(hipMemcpy(evals, devals, sizeof(int64_t) * 4 * T, hipMemcpyDeviceToHost));
+    if (evals) HIP_TRY(hipMemcpy(evals, devals, sizeof(int64_t) * NCOUNT * T, hipMemcpyDeviceToHost));
   }
   return MRBO_OK;
 }

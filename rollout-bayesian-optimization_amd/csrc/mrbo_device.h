@@ -19,14 +19,23 @@ namespace mrbo {
 constexpr int FMAX = 6;    // fantasy points per trajectory = h+1  (h ≤ 5)
 constexpr int WAVE = 64;
 
-// evaluation modes (wave-uniform)
-enum { EV_VALUE = 0, EV_DRAW = 1, EV_FULL = 2, EV_RICH = 3 };
+// evaluation modes (wave-uniform).  The front part (kernel rows, forward product, Gram, μ, σ,
+// EI and its gradient) runs in every mode but BACK; the back part (backward product w, and
+// the Hessian for FULL / RICH / BACK) resumes from state the front part left in LDS.
+//   VALUE  α only                      GRAD  α, ∇α (Hessian deferrable: BACK may follow)
+//   DRAW   GRAD + w (condition!)       FULL  GRAD + w + Hα
+//   RICH   FULL + P = L⁻ᵀV (adjoint)   BACK  w + Hα at the point of the preceding GRAD(C)
+//   GRADC  completes a VALUE evaluation to GRAD (gradient columns only; same results)
+enum { EV_VALUE = 0, EV_GRAD = 1, EV_DRAW = 2, EV_FULL = 3, EV_RICH = 4, EV_BACK = 5, EV_GRADC = 6 };
 
 struct KParams {
   int d, N, Npad, h, M, R, nstarts;
   int kernel;
   double ell, cK, psi0, d2psi0, sn2;
   double fmin_base, fmini, theta;
+  // gradient certificate (newton_grad_certified): max_ρ |ψ'(ρ)| and √(ψ(0)·(−ψ''(0))), the
+  // latter ≤ 0 when the derivative process has no finite variance (Matérn-1/2: disabled)
+  double gcert_mu, gcert_sig;
   int max_iters, max_ls;
   double x_tol, f_tol, g_tol, htol, sigma_tol;
   unsigned long long seed;

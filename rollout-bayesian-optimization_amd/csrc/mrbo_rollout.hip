@@ -26,7 +26,11 @@ struct Lay {
   static constexpr int D1 = D + 1;
   static constexpr int BS = (D1 + 1) & ~1;         // B row stride in doubles (16-B aligned rows)
   static constexpr int NR = RPL * WAVE;            // base-row capacity of the wave
-  static constexpr int BROWS = NR + FMAX;          // base rows + fantasy rows
+  // L0⁻¹ layout (see LINV_DOUBLES below); the square layout also moves the base kernel rows
+  // out of LDS (register broadcast) and the per-wave E / C rows into LDS
+  static constexpr bool SQ = (RPL == 1);
+  static constexpr int FR0 = SQ ? 0 : NR;          // first fantasy row in B
+  static constexpr int BROWS = FR0 + FMAX;         // [base rows +] fantasy rows
   static constexpr int NG = D1 * (D1 + 1) / 2;     // Gram entries (a ≤ b)
   static constexpr int NH = D * (D + 1) / 2;       // Hessian entries (a ≤ b)
   // reduction-total layout
@@ -72,22 +76,22 @@ struct Lay {
   static constexpr int U_LB = U_NP + D;                  // box lower bounds      D
   static constexpr int U_UB = U_LB + D;                  // box upper bounds      D
   static constexpr int U_HF = U_UB + D;                  // fantasy rows: [x - X_r (D), g1, g2]  FMAX×(D+2)
-  static constexpr int U_STAMP = U_HF + FMAX * (D + 2);   // cycle accumulators (MRBO_STAMPS) 16
-  static constexpr int U_SIZE = ((U_STAMP + 16) + 1) & ~1;
-  static constexpr int G12 = 2 * NR;                     // per-lane [g1, g2] of the base rows
-  static constexpr int WAVE_LDS = BROWS * BS + REDN + U_SIZE + G12;
+  static constexpr int U_STAMP = U_HF + FMAX * (D + 2);   // cycle accumulators (MRBO_STAMPS) 20
+  static constexpr int U_SIZE = ((U_STAMP + 20) + 1) & ~1;
+  static constexpr int G12 = 3 * NR;                     // per-lane [g1, g2, Y0] of the base rows
+  static constexpr int EC = SQ ? (2 * FMAX + 1) * NR : 0;  // E (FMAX×NR) + C ((FMAX+1)×NR) in LDS
+  static constexpr int WAVE_LDS = BROWS * BS + REDN + U_SIZE + G12 + EC;
   // L0⁻¹ in LDS, shared by the waves of a workgroup.  RPL == 1: dense zero-padded square,
   // column-major with odd leading dimension LD = NR + 1, so the column walk (forward product,
   // lane i reads [i][j]) and the row walk (backward product, lane i reads [k][i]) are both
   // bank-conflict free and neither needs a triangle mask.  RPL > 1: packed triangle (the
   // square would not fit next to the per-wave areas).
-  static constexpr bool SQ = (RPL == 1);
   static constexpr int LD = NR + 1;
   static constexpr long long LINV_DOUBLES = ((SQ ? (long long)NR * LD : linv_size(NR)) + 1) & ~1LL;
 };
 // scalar slots in U_SC
 enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, SC_GSIG = 6, SC_GMUMU = 7,
-       SC_GSIGSIG = 8, SC_GMUTH = 9, SC_GSIGTH = 10, SC_FMIN = 11, SC_ST = 12 };
+       SC_GSIGSIG = 8, SC_GMUTH = 9, SC_GSIGTH = 10, SC_FMIN = 11, SC_ST = 12, SC_CABS = 13 };
 
 template <int D, int RPL>
 struct WaveCtx {
@@ -97,9 +101,9 @@ struct WaveCtx {
   double* red;          // LDS: REDN
   double* U;            // LDS: U_SIZE
   const double* Linv;   // LDS: L0⁻¹ (Lay::SQ layout)
-  double* G12;          // LDS: per-lane [g1, g2] of the base rows (FULL / RICH evaluations)
-  double* E;            // global: FMAX × NR   inverse-factor fantasy rows (base columns)
-  double* C;            // global: (FMAX+1) × NR  base part of c for surfaces -1..h
+  double* G12;          // LDS: per-lane [g1, g2, Y0] of the base rows (GRAD / FULL / RICH)
+  double* E;            // LDS (SQ) or global: FMAX × NR  inverse-factor fantasy rows (base columns)
+  double* C;            // LDS (SQ) or global: (FMAX+1) × NR  base part of c for surfaces -1..h
   double X0[RPL][D];    // own base rows
   bool valid[RPL];
   int N, Npad;
@@ -113,9 +117,11 @@ struct WaveCtx {
   }
 };
 
-// work counters per trajectory (for the algorithmic-FLOP roofline)
+// work counters per trajectory (for the algorithmic-FLOP roofline):
+// evals[NCOUNT·t + k], k = gradient evals, value evals, Hessians, adjoint rich evals, pairs
+constexpr int NCOUNT = 5;
 struct Counters {
-  long long full = 0, value = 0, rich = 0, pairs = 0;
+  long long grad = 0, value = 0, hess = 0, rich = 0, pairs = 0;
 };
 
 // Optional per-phase cycle accounting (build with -DMRBO_STAMPS): STAMP(W, k) charges the
@@ -126,7 +132,7 @@ struct Counters {
 #else
 #define STAMP(W, k) ((void)0)
 #endif
-constexpr int NSTAMP = 12;
+constexpr int NSTAMP = 15;
 
 // Per-lane results of an evaluation that later phases (conditioning, adjoint) need.
 template <int D, int RPL>
@@ -137,6 +143,10 @@ struct LaneRes {
 };
 
 #ifdef MRBO_STAMPS
+template <int D, int RPL>
+__device__ __forceinline__ void stamp_count(WaveCtx<D, RPL>& W, int k, unsigned long long v) {
+  if (W.lane == 0) reinterpret_cast<unsigned long long*>(W.U + Lay<D, RPL>::U_STAMP)[k] += v;
+}
 template <int D, int RPL>
 __device__ __forceinline__ void stamp_region(WaveCtx<D, RPL>& W, int k) {
   const unsigned long long now = __builtin_amdgcn_s_memtime();
@@ -208,7 +218,9 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   double* U = W.U;
   double* B = W.B;
   double* red = W.red;
-  const bool all_cols = (mode != EV_VALUE);
+  const bool all_cols = (mode != EV_VALUE);   // gradient columns
+  const bool do_val = (mode != EV_GRADC);     // value part: column 0, μ, σ, EI (GRADC keeps the
+                                              // preceding VALUE evaluation's, bit-identical)
   STAMP(W, 8);
 
   double x[D];
@@ -224,6 +236,9 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     for (int r = 0; r < FMAX; ++r) Ev[s][r] = (r < nf) ? W.E[(long long)r * NR + lane + WAVE * s] : 0.0;
   }
 
+  const int N = W.N;
+  double acc[RPL][D1];   // Y = L0⁻¹ [kx, ∇kx] rows owned by this lane
+  if (mode != EV_BACK) {
   // ---- 1. kernel rows B[i] = [k(x,X_i), ∇k(x - X_i)]  (eval_KxX :180-191, eval_∇KxX :193-208)
   double Bown[RPL][D1];
 #pragma unroll
@@ -237,10 +252,8 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     Bown[s][0] = v ? psi : 0.0;
 #pragma unroll
     for (int a = 0; a < D; ++a) Bown[s][1 + a] = v ? g1 * r[a] : 0.0;
-    if (mode >= EV_FULL) {  // kept for the Hessian (phase 6)
-      W.G12[2 * (lane + WAVE * s)] = g1;
-      W.G12[2 * (lane + WAVE * s) + 1] = g2;
-    }
+    W.G12[3 * (lane + WAVE * s)] = g1;       // kept for a Hessian (phase 6, maybe deferred)
+    W.G12[3 * (lane + WAVE * s) + 1] = g2;
     if constexpr (!Ly::SQ) {   // the LDS row-broadcast path reads the base rows from B
       double* row = B + (lane + WAVE * s) * BS;
       if (all_cols) {
@@ -257,11 +270,11 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     for (int a = 0; a < D; ++a) { r[a] = x[a] - U[Ly::U_XF + lane * D + a]; rho2 = fma(r[a], r[a], rho2); }
     double psi, g1, g2;
     rad_eval(W.rad, rho2, psi, g1, g2);
-    double* row = B + (NR + lane) * BS;
+    double* row = B + (Ly::FR0 + lane) * BS;
     row[0] = psi;
 #pragma unroll
     for (int a = 0; a < D; ++a) row[1 + a] = g1 * r[a];
-    if (mode >= EV_FULL) {
+    {
       double* hf = U + Ly::U_HF + lane * (D + 2);
 #pragma unroll
       for (int a = 0; a < D; ++a) hf[a] = r[a];
@@ -273,19 +286,26 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   STAMP(W, 0);
 
   // ---- 2. forward product  Y[i] = Σ_{j ≤ i} L0⁻¹[i,j] B[j]   (L\kxX' , r_b_s.jl:525-526)
-  double acc[RPL][D1];
 #pragma unroll
   for (int s = 0; s < RPL; ++s)
 #pragma unroll
     for (int c = 0; c < D1; ++c) acc[s][c] = 0.0;
-  const int N = W.N;
   if constexpr (Ly::SQ) {
     // lane i reads L0⁻¹[i][j] at j·LD + i
-    if (all_cols) bcast_product<D1, Ly::LD>(acc[0], Bown[0], W.Linv + lane, N);
-    else {
+    if (mode == EV_VALUE) {
       double a1[1] = {0.0}, v1[1] = {Bown[0][0]};
       bcast_product<1, Ly::LD>(a1, v1, W.Linv + lane, N);
       acc[0][0] = a1[0];
+    } else if (mode == EV_GRADC) {   // columns 1..d; column 0 from the VALUE pass
+      double ag[D], vg[D];
+#pragma unroll
+      for (int a = 0; a < D; ++a) { ag[a] = 0.0; vg[a] = Bown[0][1 + a]; }
+      bcast_product<D, Ly::LD>(ag, vg, W.Linv + lane, N);
+#pragma unroll
+      for (int a = 0; a < D; ++a) acc[0][1 + a] = ag[a];
+      acc[0][0] = W.G12[3 * lane + 2];
+    } else {
+      bcast_product<D1, Ly::LD>(acc[0], Bown[0], W.Linv + lane, N);
     }
   } else {
   // L0⁻¹[i][j] for this lane's rows; zero above the diagonal and on padded rows
@@ -322,9 +342,13 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   }
   }
 
+  if (do_val) {   // Y0 kept for a deferred GRADC / BACK evaluation
+#pragma unroll
+    for (int s = 0; s < RPL; ++s) W.G12[3 * (lane + WAVE * s) + 2] = acc[s][0];
+  }
   STAMP(W, 1);
   // ---- 3. per-lane products and wave reductions
-  {
+  if (do_val) {
     double v[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = 0.0;
@@ -388,11 +412,12 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
 
   // ---- 4. fantasy rows of the forward product: Yf = Fpart + Dinv · Bf   (lane = (r, c))
   {
-    const int ncol = all_cols ? D1 : 1;
+    const int c0 = do_val ? 0 : 1;
+    const int ncol = all_cols ? D1 - c0 : 1;
     if (lane < nf * ncol) {
-      const int r = lane / ncol, c = lane % ncol;
+      const int r = lane / ncol, c = c0 + lane % ncol;
       double y = (c == 0) ? red[Ly::R_VAL + 2 + r] : red[Ly::R_MF + D + r * D + (c - 1)];
-      for (int q = 0; q <= r; ++q) y = fma(U[Ly::U_DINV + r * FMAX + q], B[(NR + q) * BS + c], y);
+      for (int q = 0; q <= r; ++q) y = fma(U[Ly::U_DINV + r * FMAX + q], B[(Ly::FR0 + q) * BS + c], y);
       U[Ly::U_YFV + r * D1 + c] = y;
     }
   }
@@ -400,7 +425,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   // ---- Gram (incl. fantasy rows) and μ, ∇μ  (lanes own entries)
   {
     const int ng = all_cols ? Ly::NG : 1;
-    if (lane < ng) {
+    if (lane < ng && (do_val || lane > 0)) {
       int a = 0, rem = lane;
 #pragma unroll
       for (int aa = 0; aa < D1; ++aa) if (a == aa && rem >= D1 - aa) { rem -= D1 - aa; a = aa + 1; }
@@ -411,10 +436,10 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       U[Ly::U_G + b * D1 + a] = g;
     }
     const int nm = all_cols ? D1 : 1;
-    if (lane >= 48 && lane < 48 + nm) {
+    if (lane >= (do_val ? 48 : 49) && lane < 48 + nm) {
       const int c = lane - 48;
       double mu = (c == 0) ? red[Ly::R_VAL + 1] : red[Ly::R_MF + c - 1];
-      for (int r = 0; r < nf; ++r) mu = fma(U[Ly::U_CF + (S + 1) * FMAX + r], B[(NR + r) * BS + c], mu);
+      for (int r = 0; r < nf; ++r) mu = fma(U[Ly::U_CF + (S + 1) * FMAX + r], B[(Ly::FR0 + r) * BS + c], mu);
       if (c == 0) U[Ly::U_SC + SC_MU] = mu; else U[Ly::U_GMU + c - 1] = mu;
     }
   }
@@ -422,6 +447,9 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   STAMP(W, 3);
 
   // ---- σ, EI partials (all lanes, wave-uniform values)
+  double sig_f;
+  EIp e_f;
+  if (do_val) {
   const double mu = U[Ly::U_SC + SC_MU];
   const double g00 = U[Ly::U_G];
   const double var = kp.psi0 - g00;
@@ -441,13 +469,38 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     U[Ly::U_SC + SC_FMIN] = fmin;
   }
   if (mode == EV_VALUE) { wave_sync(); STAMP(W, 4); return; }
+  sig_f = sig;
+  e_f = e;
+  } else {   // GRADC: σ and the EI partials of the VALUE pass at this point
+    sig_f = U[Ly::U_SC + SC_SIG];
+    e_f.gmu = U[Ly::U_SC + SC_GMU];
+    e_f.gsig = U[Ly::U_SC + SC_GSIG];
+    e_f.gmuth = U[Ly::U_SC + SC_GMUTH];
+    e_f.gsigth = U[Ly::U_SC + SC_GSIGTH];
+  }
   if (lane < D) {
-    const double gs = -U[Ly::U_G + (1 + lane) * D1] * (1.0 / sig);  // ∇σ = -(∇kx·w)/σ
+    const double gs = -U[Ly::U_G + (1 + lane) * D1] * (1.0 / sig_f);  // ∇σ = -(∇kx·w)/σ
     const double gm = U[Ly::U_GMU + lane];
     U[Ly::U_GSIG + lane] = gs;
-    U[Ly::U_GAL + lane] = e.gmu * gm + e.gsig * gs;                // ∇αx :567
-    U[Ly::U_MIX + lane] = gm * e.gmuth + gs * e.gsigth;            // d2α_dxdθ :575-577
+    U[Ly::U_GAL + lane] = e_f.gmu * gm + e_f.gsig * gs;                // ∇αx :567
+    U[Ly::U_MIX + lane] = gm * e_f.gmuth + gs * e_f.gsigth;            // d2α_dxdθ :575-577
   }
+  if (mode == EV_GRAD || mode == EV_GRADC) {   // a BACK evaluation may follow
+    wave_sync();
+    STAMP(W, 4);
+    return;
+  }
+  } else {   // EV_BACK: resume at the point of the preceding GRAD evaluation
+#pragma unroll
+    for (int s = 0; s < RPL; ++s) acc[s][0] = W.G12[3 * (lane + WAVE * s) + 2];
+  }
+  wave_sync();   // U_SC / gradients of the front part visible to all lanes
+  const double sig = U[Ly::U_SC + SC_SIG];
+  EIp e;
+  e.gmu = U[Ly::U_SC + SC_GMU];
+  e.gsig = U[Ly::U_SC + SC_GSIG];
+  e.gmumu = U[Ly::U_SC + SC_GMUMU];
+  e.gsigsig = U[Ly::U_SC + SC_GSIGSIG];
 
   STAMP(W, 4);
   // ---- 5. backward product w = L⁻ᵀ v (and P = L⁻ᵀ V for the adjoint)
@@ -568,8 +621,8 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
 #pragma unroll
       for (int a = 0; a < D; ++a) nv[s][a] = x[a] - W.X0[s][a];
       const double coef = W.valid[s] ? (e.gmu * lr.cb[s] - gsig_over * lr.w[s]) : 0.0;
-      ca[s] = coef * W.G12[2 * (lane + WAVE * s) + 1];
-      tb[s] = coef * W.G12[2 * (lane + WAVE * s)];
+      ca[s] = coef * W.G12[3 * (lane + WAVE * s) + 1];
+      tb[s] = coef * W.G12[3 * (lane + WAVE * s)];
     }
     wave_sync();  // previous users of red are done (all lanes passed phase 4)
 #pragma unroll
@@ -740,6 +793,21 @@ __device__ __forceinline__ bool chol_packed(double (&A)[D * (D + 1) / 2], double
   return ok;
 }
 
+// Projected-gradient test of the Newton iteration: max |g_a| over the free coordinates > g_tol.
+template <int D, int RPL>
+__device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL>& W, const KParams& kp) {
+  using Ly = Lay<D, RPL>;
+  const double* U = W.U;
+  double pg = 0.0;
+#pragma unroll
+  for (int a = 0; a < D; ++a) {
+    const double xa = U[Ly::U_NX + a], ga = U[Ly::U_NG + a];
+    const bool act = (xa <= U[Ly::U_LB + a] && ga > 0.0) || (xa >= U[Ly::U_UB + a] && ga < 0.0);
+    if (!act) pg = fmax(pg, fabs(ga));
+  }
+  return pg > kp.g_tol;
+}
+
 // One projected-Newton direction from the state in U (x = U_NX, g = U_NG, H = U_H).
 // Returns false when the iteration must stop (stationary).  Writes p to U_NP.
 template <int D, int RPL>
@@ -756,6 +824,13 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
     if (!act) pg = fmax(pg, fabs(ga));
   }
   if (!(pg > kp.g_tol)) return false;
+  // lower triangle of Hα, read unconditionally (a load under a select becomes a branch with a
+  // full LDS round trip per element)
+  double Hl[D * (D + 1) / 2];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) Hl[i * (i + 1) / 2 + j] = U[Ly::U_H + i * D + j];
   // masked reduced Hessian of f = -α (identity on the active set), packed lower
   double A[D * (D + 1) / 2];
   {
@@ -764,7 +839,7 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
     for (int i = 0; i < D; ++i)
 #pragma unroll
       for (int j = 0; j <= i; ++j) {
-        A[t] = (fr[i] && fr[j]) ? -U[Ly::U_H + i * D + j] : ((i == j) ? 1.0 : 0.0);
+        A[t] = (fr[i] && fr[j]) ? -Hl[t] : ((i == j) ? 1.0 : 0.0);
         ++t;
       }
   }
@@ -774,16 +849,15 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
     double tau = 0.0, hmax = 0.0;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-      if (!fr[i]) continue;
       double off = 0.0;
 #pragma unroll
       for (int j = 0; j < D; ++j) {
-        if (j == i || !fr[j]) continue;
-        off += fabs(U[Ly::U_H + i * D + j]);
+        const double hij = (j <= i) ? Hl[i * (i + 1) / 2 + j] : Hl[j * (j + 1) / 2 + i];
+        off += (j == i || !fr[j]) ? 0.0 : fabs(hij);
       }
-      const double hii = -U[Ly::U_H + i * D + i];
-      tau = fmax(tau, off - hii);
-      hmax = fmax(hmax, fabs(hii));
+      const double hii = -Hl[i * (i + 1) / 2 + i];
+      tau = fr[i] ? fmax(tau, off - hii) : tau;
+      hmax = fr[i] ? fmax(hmax, fabs(hii)) : hmax;
     }
     tau += 1e-8 * (1.0 + hmax);
     int t = 0;
@@ -791,7 +865,7 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
     for (int i = 0; i < D; ++i)
 #pragma unroll
       for (int j = 0; j <= i; ++j) {
-        A[t] = (fr[i] && fr[j]) ? -U[Ly::U_H + i * D + j] + ((i == j) ? tau : 0.0) : ((i == j) ? 1.0 : 0.0);
+        A[t] = (fr[i] && fr[j]) ? -Hl[t] + ((i == j) ? tau : 0.0) : ((i == j) ? 1.0 : 0.0);
         ++t;
       }
     ok = chol_packed<D>(A, idg);
@@ -850,51 +924,85 @@ __device__ __forceinline__ double newton_trial_point(WaveCtx<D, RPL>& W, double 
   return dec;
 }
 
-// Deterministic projected Newton (DESIGN.md §4) on f = -α over the box, from start k.
-// A state machine around ONE evaluate() call site.  Result: x in U_NX, f returned.
+// Gradient certificate at a point whose VALUE evaluation is in U: true when ‖∇α‖∞ ≤ g_tol is
+// guaranteed, so the Newton iteration stops there whatever the gradient columns hold.
+//   ∇α = gμ ∇μ + gσ ∇σ,  |∂_a μ| ≤ Σ|c| max|ψ'|,
+//   |∂_a σ| = |kxᵀK⁻¹∂_a kx| / σ ≤ √(kxᵀK⁻¹kx · ∂_a kxᵀK⁻¹∂_a kx) / σ ≤ √(ψ(0)(−ψ''(0))) / σ
+// (posterior variances of f and ∂_a f are ≥ 0).  A factor 4 covers rounding.  gμ = gσ = 0
+// (σ < σtol, or Φ and φ underflowed) makes ∇α zero or NaN, which also stops the iteration.
+template <int D, int RPL>
+__device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const KParams& kp) {
+  using Ly = Lay<D, RPL>;
+  const double* U = W.U;
+  const double gm = U[Ly::U_SC + SC_GMU], gs = U[Ly::U_SC + SC_GSIG];
+  if (gm == 0.0 && gs == 0.0) return true;
+  if (!(kp.gcert_sig > 0.0)) return false;
+  const double bound = fabs(gm) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + gs * kp.gcert_sig / U[Ly::U_SC + SC_SIG];
+  return bound <= 0.25 * kp.g_tol;
+}
+
+// Deterministic projected Newton (DESIGN.md §3) on f = -α over the box, from start k.
+// A state machine around ONE evaluate() call site.  Work is lazy, decisions are not: every
+// point gets a value-only evaluation; the gradient columns are completed (GRADC) only where
+// the certificate cannot rule out a step, the backward product and Hα (BACK) only where a
+// step is taken.  Values and gradients are bit-identical to a FULL evaluation at the same
+// point (same code path), so the iterates are those of the eager iteration, and the work
+// counts equal the oracle's (rbo_oracle.c newton_solve).  Result: x in U_NX, f returned.
 template <int D, int RPL>
 __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, int S, int k, Counters& nevals,
                                          int& st, LaneRes<D, RPL>& lr) {
   using Ly = Lay<D, RPL>;
   double* U = W.U;
   const int lane = W.ln();
-  enum { P_INIT = 0, P_TRIAL = 1, P_REFULL = 2 };
+  enum { P_VAL = 0, P_TRIAL = 1, P_GRAD = 2, P_HESS = 3 };
   if (lane < D) {
     const double xa = clampd(kp.xstarts[(long long)k * D + lane], U[Ly::U_LB + lane], U[Ly::U_UB + lane]);
     U[Ly::U_NX + lane] = xa;
     U[Ly::U_X + lane] = xa;
   }
   wave_sync();
-  int phase = P_INIT, mode = EV_FULL, it = 0, ls = 0;
+  int phase = P_VAL, mode = EV_VALUE, it = 0, ls = 0;
   double f = 0.0, ft = 0.0, t = 1.0, dec = 0.0;
   for (;;) {
     evaluate<D, RPL>(W, kp, S, mode, lr);
-    if (mode == EV_VALUE) ++nevals.value; else ++nevals.full;
-    if (U[Ly::U_SC + SC_VAR] < 0.0) st |= 1;
-    const double fe = -U[Ly::U_SC + SC_ALPHA];
-    bool accept_now = false;
-    if (phase == P_INIT) {
-      f = fe;
+    if (mode == EV_VALUE) ++nevals.value;
+    else if (mode == EV_GRADC) ++nevals.grad;
+    else ++nevals.hess;
+    if (phase == P_HESS) {                 // Hα at x ready: step
+      STAMP(W, 12);
+      const bool go = newton_direction<D, RPL>(W, kp);
+      STAMP(W, 13);
+      if (!go) break;
+      t = 1.0;
+      ls = 0;
+      dec = newton_trial_point<D, RPL>(W, t);
+      STAMP(W, 14);
+      phase = P_TRIAL;
+      mode = EV_VALUE;
+      continue;
+    }
+    if (phase == P_GRAD) {                 // ∇α at x ready
       if (lane < D) U[Ly::U_NG + lane] = -U[Ly::U_GAL + lane];
       wave_sync();
-    } else if (phase == P_TRIAL) {
+      if (!newton_pg_ok<D, RPL>(W, kp)) break;     // stationary
+      STAMP(W, 12);
+      phase = P_HESS;
+      mode = EV_BACK;
+      continue;
+    }
+    // a VALUE evaluation: the start point (P_VAL) or a line-search trial (P_TRIAL)
+    if (U[Ly::U_SC + SC_VAR] < 0.0) st |= 1;
+    const double fe = -U[Ly::U_SC + SC_ALPHA];
+    if (phase == P_TRIAL) {
       ft = fe;
-      if (ft == ft && ft <= f + 1e-4 * dec) {
-        if (ls == 0) accept_now = true;
-        else { phase = P_REFULL; mode = EV_FULL; continue; }   // full eval at the accepted point
-      } else {
+      if (!(ft == ft && ft <= f + 1e-4 * dec)) {   // projected Armijo, backtrack
         ++ls;
-        if (ls >= kp.max_ls) break;                            // no acceptable step
+        if (ls >= kp.max_ls) break;                // no acceptable step
         t *= 0.5;
         dec = newton_trial_point<D, RPL>(W, t);
-        mode = EV_VALUE;
         continue;
       }
-    } else {
-      accept_now = true;
-    }
-    if (accept_now) {
-      double dx = 0.0, mine = 0.0;
+      double dx = 0.0, mine = 0.0;                 // accept x_t
 #pragma unroll
       for (int a = 0; a < D; ++a) {
         const double xt = U[Ly::U_X + a];
@@ -903,20 +1011,21 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
       }
       const double df = fabs(ft - f);
       wave_sync();
-      if (lane < D) { U[Ly::U_NX + lane] = mine; U[Ly::U_NG + lane] = -U[Ly::U_GAL + lane]; }
+      if (lane < D) U[Ly::U_NX + lane] = mine;
       wave_sync();
       f = ft;
       ++it;
       if (dx <= kp.x_tol || df <= kp.f_tol * fabs(f)) break;
+    } else {
+      f = fe;
     }
+    // decision point at x = U_NX (= U_X), whose VALUE evaluation is in U
     if (it >= kp.max_iters) break;
     if (f != f) break;
-    if (!newton_direction<D, RPL>(W, kp)) break;
-    t = 1.0;
-    ls = 0;
-    dec = newton_trial_point<D, RPL>(W, t);
-    phase = P_TRIAL;
-    mode = EV_FULL;
+    if (grad_certified<D, RPL>(W, kp)) break;     // ‖∇α‖ ≤ g_tol guaranteed: stationary
+    STAMP(W, 12);
+    phase = P_GRAD;
+    mode = EV_GRADC;
   }
   wave_sync();
   return f;
@@ -933,6 +1042,18 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
   int best = -1;
   bool best_nan = false;
   double bestf = 0.0;
+  {   // Σ|c| of surface S (base + fantasy coefficients) for the gradient certificate
+    double v[1] = {0.0};
+#pragma unroll
+    for (int s = 0; s < RPL; ++s) v[0] += fabs(W.C[(long long)(S + 1) * Ly::NR + lane + WAVE * s]);
+    wave_sync();
+    wave_reduce<1>(v, W.red, lane);
+    wave_sync();
+    double cabs = W.red[0];
+    for (int r = 0; r <= S; ++r) cabs += fabs(U[Ly::U_CF + (S + 1) * FMAX + r]);
+    if (lane == 0) U[Ly::U_SC + SC_CABS] = cabs;
+    wave_sync();
+  }
   for (int k = 0; k < kp.nstarts; ++k) {
     const double fo = newton<D, RPL>(W, kp, S, k, nevals, st, lr);
     bool xnan = false;
@@ -1217,8 +1338,9 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
   const long long oidx = (long long)m + (long long)M * r;
   if (kp.obs && lane <= h) kp.obs[oidx * (h + 1) + lane] = st ? NAN : U[Ly::U_YF + lane];
   if (kp.evals && lane == 0) {
-    kp.evals[4 * oidx + 0] = nevals.full;
-    kp.evals[4 * oidx + 1] = nevals.value;
+    kp.evals[NCOUNT * oidx + 0] = nevals.grad;
+    kp.evals[NCOUNT * oidx + 1] = nevals.value;
+    kp.evals[NCOUNT * oidx + 2] = nevals.hess;
   }
   if (st) {
     if (lane == 0) { kp.values[oidx] = NAN; kp.status[oidx] = st; if (kp.grad_theta) kp.grad_theta[oidx] = NAN; }
@@ -1322,8 +1444,8 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
   }
   if (st && lane == 0) kp.values[base] = NAN;
   if (kp.evals && lane == 0) {
-    kp.evals[4 * base + 2] = nevals.rich;
-    kp.evals[4 * base + 3] = nevals.pairs;
+    kp.evals[NCOUNT * base + 3] = nevals.rich;
+    kp.evals[NCOUNT * base + 4] = nevals.pairs;
   }
   wave_sync();
   STAMP(W, 11);
@@ -1343,7 +1465,8 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
   W.G12 = W.U + Ly::U_SIZE;
   W.Linv = smem;
   const long long slot = (long long)blockIdx.x * (blockDim.x / WAVE) + wave_in_block;
-  W.E = kp.work + slot * kp.work_stride;
+  if constexpr (Ly::SQ) W.E = W.G12 + Ly::G12;
+  else W.E = kp.work + slot * kp.work_stride;
   W.C = W.E + (long long)FMAX * Ly::NR;
   W.N = kp.N;
   W.Npad = kp.Npad;
@@ -1361,7 +1484,7 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
 }
 
 template <int D, int RPL>
-__global__ void __launch_bounds__(256, MRBO_WAVES_PER_SIMD) rollout_kernel(KParams kp) {
+__global__ void __launch_bounds__(512, MRBO_WAVES_PER_SIMD) rollout_kernel(KParams kp) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // stage L0⁻¹ once per workgroup (the only block-wide barrier)
   using Ly = Lay<D, RPL>;
@@ -1382,14 +1505,14 @@ __global__ void __launch_bounds__(256, MRBO_WAVES_PER_SIMD) rollout_kernel(KPara
   }
 #ifdef MRBO_STAMPS
   if (kp.stamps && W.lane == 0)
-    for (int k = 0; k < NSTAMP; ++k)
+    for (int k = 0; k < 20; ++k)
       atomicAdd(kp.stamps + k, reinterpret_cast<unsigned long long*>(W.U + Lay<D, RPL>::U_STAMP)[k]);
 #endif
 }
 
 // eval(s, x, θ) on the base surrogate for P points (fixture / primitive parity path)
 template <int D, int RPL>
-__global__ void __launch_bounds__(256, MRBO_WAVES_PER_SIMD) eval_base_kernel(KParams kp) {
+__global__ void __launch_bounds__(512, MRBO_WAVES_PER_SIMD) eval_base_kernel(KParams kp) {
   using Ly = Lay<D, RPL>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   for (int q = threadIdx.x; q < (int)Ly::LINV_DOUBLES; q += blockDim.x) smem[q] = kp.Linv[q];

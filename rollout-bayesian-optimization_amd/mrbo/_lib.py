@@ -15,6 +15,9 @@ _vp = ctypes.c_void_p
 
 MRBO_FLAG_HOST_POINTERS = 1
 MRBO_FLAG_NO_GRADIENT = 2
+# per-trajectory work counters of mrbo_simulate_mc `evals` (MRBO_NCOUNTERS in include/mrbo.h)
+NCOUNTERS = 5
+COUNTER_NAMES = ("grad_evals", "value_evals", "hessians", "rich_evals", "pairs")
 
 STATUS_BITS = {
     1: "DomainError: sqrt of a negative posterior variance (radial_basis_surrogates.jl:528)",

@@ -89,7 +89,7 @@ class RolloutPlan:
         if want_obs:
             out["obs"] = torch.empty((self.h + 1) * T, dtype=torch.float64, device=dev)
         if want_evals:
-            out["evals"] = torch.empty(4 * T, dtype=torch.int64, device=dev)
+            out["evals"] = torch.empty(_lib.NCOUNTERS * T, dtype=torch.int64, device=dev)
         return out
 
     def simulate(self, x0s, rnstream, xstarts, out, dual_y_dx=None, replay_x=None, stream=None):

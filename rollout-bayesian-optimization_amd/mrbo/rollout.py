@@ -59,7 +59,7 @@ class BatchResult:
         if "obs" in o:
             res["obs"] = from_device(o["obs"], (h + 1, M, R))
         if "evals" in o:
-            res["evals"] = from_device(o["evals"], (4, M, R))
+            res["evals"] = from_device(o["evals"], (_lib.NCOUNTERS, M, R))
         if self.eto_dev is not None:
             res["eto"] = from_device(self.eto_dev, (2 + 2 * d + 2, R))
         return res

@@ -42,7 +42,7 @@ def _run(plan, g, dual=None, replay=None, want_policy=True, with_gradient=True, 
     d, M, R, h = plan.d, plan.M, plan.R, plan.h
     res = dict(values=from_device(out["values"], (M, R)), status=from_device(out["status"], (M, R)),
                obs=from_device(out["obs"], (h + 1, M, R)), eto=from_device(eto, (2 + 2 * d + 2, R)),
-               evals=from_device(out["evals"], (4, M, R)))
+               evals=from_device(out["evals"], (5, M, R)))
     if with_gradient:
         res["grad_x"] = from_device(out["grad_x"], (d, M, R))
         res["grad_theta"] = from_device(out["grad_theta"], (1, M, R))
@@ -108,7 +108,8 @@ def test_end_to_end_vs_oracle(gpu, oracle, name, M, R):
     assert same.mean() >= 0.97, same.mean()
     np.testing.assert_allclose(r["values"][same], o["values"][same], rtol=1e-8, atol=1e-11)
     _assert_grads_close(r["grad_x"][:, same], o["grad_x"][:, same])
-    np.testing.assert_array_equal(r["evals"][0][same], o["evals"][same])  # identical Newton work
+    # identical Newton work: gradient evals, value evals, Hessians (the same lazy iteration)
+    np.testing.assert_array_equal(r["evals"][:3][:, same], o["evals"][:, same])
     # replay the GPU's own policy points through the oracle: every trajectory agrees
     rp = np.asfortranarray(r["policy_x"][:, 1:])
     o2 = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),

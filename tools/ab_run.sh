@@ -1,7 +1,17 @@
-set -e
-export TMPDIR=/tmp
-for v in base inl inl_nolicm w1; do
-  MRBO_LIB=$PWD/rollout-bayesian-optimization_amd/mrbo/variants/libmrbo_$v.so timeout -k 10 120 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/ab_$v.json 2>/dev/null
+#!/bin/bash
+# A/B timing of library variants on the GPU box: bench.py per variant (+ stamps where built).
+# usage: bash tools/ab_run.sh base inl ...   (variants from tools/build_variants.sh)
+V=${GRAFT_REPO_ROOT:-$PWD}/rollout-bayesian-optimization_amd/mrbo/variants
+mkdir -p gpurun_out
+for v in "$@"; do
+  MRBO_LIB=$V/libmrbo_$v.so timeout -k 10 120 python bench.py --steps 5 --warmup 2 --no-cpu-baseline \
+    > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || { echo "variant $v failed"; exit 1; }
+  python - "$v" <<'PY'
+import json, sys
+v = sys.argv[1]
+lines = [l for l in open(f"gpurun_out/ab_{v}.json") if l.startswith("{")]
+d = json.loads(lines[-1])
+print(f"{v:12s} {d['value']:12.0f} traj/s  kernel {d['roofline']['kernel_ms']:.2f} ms  frac {d['roofline']['frac']:.4f}")
+PY
+  grep "mrbo stamps" gpurun_out/ab_$v.err | head -20
 done
-timeout -k 10 60 rocprofv3 -L > gpurun_out/counters_list.txt 2>&1
-timeout -k 10 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY --output-format csv -d gpurun_out/pmc1 -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/pmc1.log 2>&1
