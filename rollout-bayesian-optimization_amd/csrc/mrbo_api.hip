@@ -59,6 +59,8 @@ struct mrbo_plan {
   int* dqueue = nullptr;
   int wpg = 4, blocks = 0;
   size_t smem = 0;
+  int xs_lds = 0;           // rollout launches stage xstarts in LDS (≤ 8 KB)
+  int batch = 0;            // batched start-point values (start tables in LDS)
   int ewpg = 4, eblocks = 0;
   size_t esmem = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -133,10 +135,12 @@ void launch_evalb(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, con
 }
 
 // choose waves per workgroup maximising resident waves per CU (LDS + register limits)
-int pick_grid(const void* fn, size_t linv_bytes, size_t wave_bytes, int ncu, int& wpg, int& blocks, size_t& smem) {
+// fixed_bytes: per-workgroup tables; the wave areas double as prologue scratch of scratch_bytes
+int pick_grid(const void* fn, size_t fixed_bytes, size_t wave_bytes, int ncu, int& wpg, int& blocks, size_t& smem,
+              size_t scratch_bytes = 0) {
   int best_w = 0;
   for (int w = 1; w <= 8; ++w) {
-    const size_t sm = linv_bytes + w * wave_bytes;
+    const size_t sm = fixed_bytes + std::max(w * wave_bytes, scratch_bytes);
     if (sm > 160 * 1024) break;
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, w * WAVE, sm) != hipSuccess) continue;
@@ -388,7 +392,26 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete P; return fail(MRBO_ERR_HIP, "device props"); }
   const size_t linv_bytes = sizeof(double) * (size_t)ks.linv_doubles;
-  if (!pick_grid(ks.rollout, linv_bytes, ks.wave_bytes, prop.multiProcessorCount, P->wpg, P->blocks, P->smem) ||
+  const int ns = P->p.nstarts;
+  const size_t xs_bytes = sizeof(double) * (size_t)(((size_t)ns * d + 1) & ~(size_t)1);
+  P->xs_lds = xs_bytes <= 8192 ? 1 : 0;
+  // batched start values: start tables kxb (NR × ns) and y0sq (ns), square L0⁻¹ only; kept only
+  // if they cost no resident waves
+  const size_t kxb_bytes = sizeof(double) * ((((size_t)P->NR * ns + 1) & ~(size_t)1) + (((size_t)ns + 1) & ~(size_t)1));
+  const size_t fixed = linv_bytes + (P->xs_lds ? xs_bytes : 0);
+  int wpg0 = 0, blocks0 = 0;
+  size_t smem0 = 0;
+  const int waves0 = pick_grid(ks.rollout, fixed, ks.wave_bytes, prop.multiProcessorCount, wpg0, blocks0, smem0);
+  P->batch = 0;
+  if (ks.square && P->xs_lds && ns <= 64) {
+    int wpg1 = 0, blocks1 = 0;
+    size_t smem1 = 0;
+    const int waves1 = pick_grid(ks.rollout, fixed + kxb_bytes, ks.wave_bytes, prop.multiProcessorCount, wpg1, blocks1,
+                                 smem1, sizeof(double) * (size_t)P->NR * ns);
+    if (waves1 >= waves0 && waves1 > 0) { P->batch = 1; P->wpg = wpg1; P->blocks = blocks1; P->smem = smem1; }
+  }
+  if (!P->batch) { P->wpg = wpg0; P->blocks = blocks0; P->smem = smem0; }
+  if (!waves0 ||
       !pick_grid(ks.evalb, linv_bytes, ks.wave_bytes, prop.multiProcessorCount, P->ewpg, P->eblocks, P->esmem)) {
     delete P;
     return fail(MRBO_ERR_UNSUPPORTED, "no feasible launch configuration");
@@ -470,6 +493,8 @@ int mrbo_simulate_mc(mrbo_plan_t* P, const double* x0s, const double* rnstream, 
   kp.stamps = dstamps;
 #endif
   HIP_TRY(hipEventRecord(P->ev0, st));
+  kp.xs_lds = P->xs_lds;
+  kp.batch = P->batch;
   launch_rollout(d, P->RPL, dim3(P->blocks), dim3(P->wpg * WAVE), P->smem, st, kp);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(P->ev1, st));

@@ -41,6 +41,8 @@ struct KParams {
   unsigned long long seed;
   int sample_offset, samples_total;
   int with_gradient;
+  int xs_lds;           // xstarts staged in LDS after L0⁻¹ (rollout launches)
+  int batch;            // batched start-point values (needs xs_lds, RPL = 1, nstarts ≤ 64)
   const double* X0;     // [d][NR]   lane-major base covariates
   const double* c0;     // [NR]      base coefficients
   const double* Linv;   // packed L0⁻¹ (see linv_index)
@@ -271,6 +273,13 @@ __host__ __device__ __forceinline__ double dual_uniform(unsigned long long seed,
   key = splitmix64(key ^ (unsigned long long)traj);
   key = splitmix64(key ^ (((unsigned long long)(unsigned)j << 32) | (unsigned)k));
   return (double)(key >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// value of a double in lane k (wave-uniform k)
+__device__ __forceinline__ double readlane_d(double v, int k) {
+  int lo, hi;
+  dsplit(v, lo, hi);
+  return djoin(__builtin_amdgcn_readlane(lo, k), __builtin_amdgcn_readlane(hi, k));
 }
 
 __device__ __forceinline__ double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }

@@ -93,6 +93,22 @@ struct Lay {
 enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, SC_GSIG = 6, SC_GMUMU = 7,
        SC_GSIGSIG = 8, SC_GMUTH = 9, SC_GSIGTH = 10, SC_FMIN = 11, SC_ST = 12, SC_CABS = 13 };
 
+// Per-workgroup LDS after L0⁻¹: [xstarts (d×nstarts)] [kxb (NR×nstarts)] [y0sq (nstarts)],
+// each rounded to an even number of doubles; then the per-wave areas.
+template <int D, int RPL>
+struct WgTables {
+  long long xs, kxb, y0sq, end;   // offsets in doubles from smem
+  __device__ __forceinline__ WgTables(const KParams& kp) {
+    using Ly = Lay<D, RPL>;
+    xs = Ly::LINV_DOUBLES;
+    const long long nxs = kp.xs_lds ? (((long long)kp.nstarts * D + 1) & ~1LL) : 0;
+    kxb = xs + nxs;
+    const long long nk = kp.batch ? (((long long)Ly::NR * kp.nstarts + 1) & ~1LL) : 0;
+    y0sq = kxb + nk;
+    end = y0sq + (kp.batch ? ((kp.nstarts + 1) & ~1) : 0);
+  }
+};
+
 template <int D, int RPL>
 struct WaveCtx {
   using Ly = Lay<D, RPL>;
@@ -101,6 +117,9 @@ struct WaveCtx {
   double* red;          // LDS: REDN
   double* U;            // LDS: U_SIZE
   const double* Linv;   // LDS: L0⁻¹ (Lay::SQ layout)
+  const double* XS;     // inner-solve start points: LDS copy (kp.xs_lds) or kp.xstarts
+  const double* KXB;    // LDS [NR][nstarts]: ψ(|clamp(x_k) − X_i|) (kp.batch)
+  const double* Y0SQ;   // LDS [nstarts]: |L0⁻¹ kx(x_k)|² (kp.batch)
   double* G12;          // LDS: per-lane [g1, g2, Y0] of the base rows (GRAD / FULL / RICH)
   double* E;            // LDS (SQ) or global: FMAX × NR  inverse-factor fantasy rows (base columns)
   double* C;            // LDS (SQ) or global: (FMAX+1) × NR  base part of c for surfaces -1..h
@@ -410,49 +429,83 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   wave_sync();
   STAMP(W, 2);
 
-  // ---- 4. fantasy rows of the forward product: Yf = Fpart + Dinv · Bf   (lane = (r, c))
+  // ---- 4a. column 0 in every lane: fantasy rows Yf[r][0] = E_r·B0 + Σ_q Dinv[r][q] Bf[q][0],
+  // G00 = |Y0|² + Σ_r Yf[r][0]², μ = c·kx + Σ_r c_r Bf[r][0].  One batch of unconditional LDS
+  // reads instead of three dependent lane-distributed phases (same FMA order).
+  double mu_v = 0.0, g00_v = 0.0;
+  if (do_val) {
+    double bf[FMAX], yf[FMAX];
+#pragma unroll
+    for (int r = 0; r < FMAX; ++r) bf[r] = B[(Ly::FR0 + r) * BS];
+    g00_v = red[Ly::R_VAL];
+    mu_v = red[Ly::R_VAL + 1];
+#pragma unroll
+    for (int r = 0; r < FMAX; ++r) {
+      double y = red[Ly::R_VAL + 2 + r];
+#pragma unroll
+      for (int q = 0; q <= r; ++q) y = fma(U[Ly::U_DINV + r * FMAX + q], bf[q], y);
+      yf[r] = y;
+    }
+#pragma unroll
+    for (int r = 0; r < FMAX; ++r) {
+      if (r < nf) {
+        g00_v = fma(yf[r], yf[r], g00_v);
+        mu_v = fma(U[Ly::U_CF + (S + 1) * FMAX + r], bf[r], mu_v);
+      }
+    }
+    if (lane < FMAX) {
+      double mine = 0.0;
+#pragma unroll
+      for (int r = 0; r < FMAX; ++r) mine = (lane == r) ? yf[r] : mine;
+      if (lane < nf) U[Ly::U_YFV + lane * D1] = mine;
+    }
+    if (lane == 0) {
+      U[Ly::U_G] = g00_v;
+      U[Ly::U_SC + SC_MU] = mu_v;
+    }
+  }
+  // ---- 4b. gradient columns of the fantasy rows: Yf = Fpart + Dinv · Bf   (lane = (r, c), c ≥ 1)
+  if (all_cols) {
   {
-    const int c0 = do_val ? 0 : 1;
-    const int ncol = all_cols ? D1 - c0 : 1;
+    const int ncol = D;
     if (lane < nf * ncol) {
-      const int r = lane / ncol, c = c0 + lane % ncol;
-      double y = (c == 0) ? red[Ly::R_VAL + 2 + r] : red[Ly::R_MF + D + r * D + (c - 1)];
+      const int r = lane / ncol, c = 1 + lane % ncol;
+      double y = red[Ly::R_MF + D + r * D + (c - 1)];
       for (int q = 0; q <= r; ++q) y = fma(U[Ly::U_DINV + r * FMAX + q], B[(Ly::FR0 + q) * BS + c], y);
       U[Ly::U_YFV + r * D1 + c] = y;
     }
   }
   wave_sync();
-  // ---- Gram (incl. fantasy rows) and μ, ∇μ  (lanes own entries)
+  // ---- Gram (incl. fantasy rows) and ∇μ  (lanes own entries; G00 and μ above)
   {
-    const int ng = all_cols ? Ly::NG : 1;
-    if (lane < ng && (do_val || lane > 0)) {
+    const int ng = Ly::NG;
+    if (lane > 0 && lane < ng) {
       int a = 0, rem = lane;
 #pragma unroll
       for (int aa = 0; aa < D1; ++aa) if (a == aa && rem >= D1 - aa) { rem -= D1 - aa; a = aa + 1; }
       const int b = a + rem;
-      double g = (lane == 0) ? red[Ly::R_VAL] : red[Ly::R_G + lane - 1];
+      double g = red[Ly::R_G + lane - 1];
       for (int r = 0; r < nf; ++r) g = fma(U[Ly::U_YFV + r * D1 + a], U[Ly::U_YFV + r * D1 + b], g);
       U[Ly::U_G + a * D1 + b] = g;
       U[Ly::U_G + b * D1 + a] = g;
     }
-    const int nm = all_cols ? D1 : 1;
-    if (lane >= (do_val ? 48 : 49) && lane < 48 + nm) {
+    if (lane >= 49 && lane < 48 + D1) {
       const int c = lane - 48;
-      double mu = (c == 0) ? red[Ly::R_VAL + 1] : red[Ly::R_MF + c - 1];
+      double mu = red[Ly::R_MF + c - 1];
       for (int r = 0; r < nf; ++r) mu = fma(U[Ly::U_CF + (S + 1) * FMAX + r], B[(Ly::FR0 + r) * BS + c], mu);
-      if (c == 0) U[Ly::U_SC + SC_MU] = mu; else U[Ly::U_GMU + c - 1] = mu;
+      U[Ly::U_GMU + c - 1] = mu;
     }
   }
   wave_sync();
+  }
   STAMP(W, 3);
 
   // ---- σ, EI partials (all lanes, wave-uniform values)
   double sig_f;
   EIp e_f;
   if (do_val) {
-  const double mu = U[Ly::U_SC + SC_MU];
-  const double g00 = U[Ly::U_G];
-  const double var = kp.psi0 - g00;
+  const double mu = mu_v;
+  const double var = kp.psi0 - g00_v;
   const double sig = sqrt(var);
   const double fmin = U[Ly::U_FMIN + S + 1];
   const EIp e = ei_partials(mu, sig, kp.theta, fmin, kp.sigma_tol);
@@ -950,23 +1003,25 @@ __device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const K
 // counts equal the oracle's (rbo_oracle.c newton_solve).  Result: x in U_NX, f returned.
 template <int D, int RPL>
 __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, int S, int k, Counters& nevals,
-                                         int& st, LaneRes<D, RPL>& lr) {
+                                         int& st, LaneRes<D, RPL>& lr, double f0, bool have_f0) {
   using Ly = Lay<D, RPL>;
   double* U = W.U;
   const int lane = W.ln();
   enum { P_VAL = 0, P_TRIAL = 1, P_GRAD = 2, P_HESS = 3 };
   if (lane < D) {
-    const double xa = clampd(kp.xstarts[(long long)k * D + lane], U[Ly::U_LB + lane], U[Ly::U_UB + lane]);
+    const double xa = clampd(W.XS[(long long)k * D + lane], U[Ly::U_LB + lane], U[Ly::U_UB + lane]);
     U[Ly::U_NX + lane] = xa;
     U[Ly::U_X + lane] = xa;
   }
   wave_sync();
-  int phase = P_VAL, mode = EV_VALUE, it = 0, ls = 0;
-  double f = 0.0, ft = 0.0, t = 1.0, dec = 0.0;
+  // have_f0: the start's value (and certificate) came from batch_start_values and did not
+  // stop the iteration, so it begins with the gradient at x_start
+  int phase = have_f0 ? P_GRAD : P_VAL, mode = have_f0 ? EV_GRAD : EV_VALUE, it = 0, ls = 0;
+  double f = have_f0 ? f0 : 0.0, ft = 0.0, t = 1.0, dec = 0.0;
   for (;;) {
     evaluate<D, RPL>(W, kp, S, mode, lr);
     if (mode == EV_VALUE) ++nevals.value;
-    else if (mode == EV_GRADC) ++nevals.grad;
+    else if (mode == EV_GRADC || mode == EV_GRAD) ++nevals.grad;
     else ++nevals.hess;
     if (phase == P_HESS) {                 // Hα at x ready: step
       STAMP(W, 12);
@@ -1031,6 +1086,118 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
   return f;
 }
 
+// Workgroup prologue (kp.batch): base kernel rows of the clamped start points and the squared
+// norms of their forward products -- constants of the launch shared by every multistart.
+//   kxb[i][k] = ψ(|x_k − X_i|) (0 on padded rows),  y0sq[k] = |L0⁻¹ kxb[:,k]|²
+// The per-wave areas (not yet initialised) serve as scratch for the squares.
+template <int D, int RPL>
+__device__ __forceinline__ void stage_start_tables(const KParams& kp, double* smem) {
+  using Ly = Lay<D, RPL>;
+  constexpr int NR = Ly::NR;
+  const WgTables<D, RPL> tb(kp);
+  const int ns = kp.nstarts;
+  const double* xs = smem + tb.xs;
+  double* kxb = smem + tb.kxb;
+  double* y0sq = smem + tb.y0sq;
+  double* sq = smem + tb.end;                 // scratch NR × ns (wave areas, re-zeroed by wave_setup)
+  Radial rad;
+  rad.kind = kp.kernel;
+  rad.cK = kp.cK;
+  for (int q = threadIdx.x; q < NR * ns; q += blockDim.x) {
+    const int i = q / ns, k = q - (q / ns) * ns;
+    double v = 0.0;
+    if (i < kp.N) {
+      double rho2 = 0.0;
+#pragma unroll
+      for (int a = 0; a < D; ++a) {
+        const double r = clampd(xs[k * D + a], kp.lbs[a], kp.ubs[a]) - kp.X0[(long long)a * NR + i];
+        rho2 = fma(r, r, rho2);
+      }
+      double g1, g2;
+      rad_eval(rad, rho2, v, g1, g2);
+    }
+    kxb[q] = v;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < NR * ns; q += blockDim.x) {
+    const int i = q / ns, k = q - (q / ns) * ns;
+    double y = 0.0;
+    for (int j = 0; j <= i && j < kp.N; ++j) y = fma(smem[j * Ly::LD + i], kxb[j * ns + k], y);
+    sq[q] = y * y;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+    double t = 0.0;
+    for (int i = 0; i < kp.N; ++i) t += sq[i * ns + k];
+    y0sq[k] = t;
+  }
+  __syncthreads();
+}
+
+// Values of ALL start points of a multistart on surface S at once (kp.batch): lane k takes start
+// k.  With the launch constants kxb, y0sq only the surface-dependent parts remain:
+//   μ_k = c_S·kxb[:,k] + Σ_r c_r ψ(x_k, X_r),  Yf_r = E_r·kxb[:,k] + Σ_{q≤r} Dinv[r][q] ψ(x_k, X_q),
+//   σ_k² = ψ(0) − y0sq[k] − Σ_r Yf_r²,  then α and the gradient certificate per lane.
+// Replaces nstarts value evaluations (and their wave-redundant EI) by one pass.
+template <int D, int RPL>
+__device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KParams& kp, int S, double& f_lane,
+                                                   unsigned long long& certmask, bool& varneg) {
+  using Ly = Lay<D, RPL>;
+  constexpr int NR = Ly::NR;
+  const double* U = W.U;
+  const int lane = W.ln();
+  const int ns = kp.nstarts, nf = S + 1;
+  const bool act = lane < ns;
+  const int k = act ? lane : 0;
+  double x[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) x[a] = clampd(W.XS[k * D + a], U[Ly::U_LB + a], U[Ly::U_UB + a]);
+  double amu = 0.0, ae[FMAX];
+#pragma unroll
+  for (int r = 0; r < FMAX; ++r) ae[r] = 0.0;
+  const double* cS = W.C + (long long)(S + 1) * NR;
+#pragma unroll 4
+  for (int i = 0; i < W.N; ++i) {
+    const double kv = W.KXB[i * ns + k];
+    amu = fma(cS[i], kv, amu);
+#pragma unroll
+    for (int r = 0; r < FMAX; ++r)
+      if (r < nf) ae[r] = fma(W.E[(long long)r * NR + i], kv, ae[r]);
+  }
+  double pf[FMAX];
+#pragma unroll
+  for (int q = 0; q < FMAX; ++q) {
+    pf[q] = 0.0;
+    if (q < nf) {
+      double rho2 = 0.0;
+#pragma unroll
+      for (int a = 0; a < D; ++a) { const double r = x[a] - U[Ly::U_XF + q * D + a]; rho2 = fma(r, r, rho2); }
+      double g1, g2;
+      rad_eval(W.rad, rho2, pf[q], g1, g2);
+    }
+  }
+  double g00 = W.Y0SQ[k], mu = amu;
+#pragma unroll
+  for (int r = 0; r < FMAX; ++r) {
+    if (r < nf) {
+      double y = ae[r];
+#pragma unroll
+      for (int q = 0; q <= r; ++q) y = fma(U[Ly::U_DINV + r * FMAX + q], pf[q], y);
+      g00 = fma(y, y, g00);
+      mu = fma(U[Ly::U_CF + (S + 1) * FMAX + r], pf[r], mu);
+    }
+  }
+  const double var = kp.psi0 - g00;
+  const double sig = sqrt(var);
+  const EIp e = ei_partials(mu, sig, kp.theta, U[Ly::U_FMIN + S + 1], kp.sigma_tol);
+  bool cert = (e.gmu == 0.0 && e.gsig == 0.0);
+  if (!cert && kp.gcert_sig > 0.0)
+    cert = fabs(e.gmu) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + e.gsig * kp.gcert_sig / sig <= 0.25 * kp.g_tol;
+  f_lane = -e.g;
+  certmask = __ballot(act && cert);
+  varneg = __ballot(act && var < 0.0) != 0;
+}
+
 // multistart_base_solve!(fs, …) rbf_optim.jl:68-101 -> U[U_XB]
 template <int D, int RPL>
 __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp, int S, Counters& nevals,
@@ -1054,8 +1221,30 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
     if (lane == 0) U[Ly::U_SC + SC_CABS] = cabs;
     wave_sync();
   }
+  double f_lane = 0.0;
+  unsigned long long certmask = 0;
+  if (kp.batch) {
+    bool varneg = false;
+    batch_start_values<D, RPL>(W, kp, S, f_lane, certmask, varneg);
+    nevals.value += kp.nstarts;
+    if (varneg) st |= 1;
+    wave_sync();
+  }
   for (int k = 0; k < kp.nstarts; ++k) {
-    const double fo = newton<D, RPL>(W, kp, S, k, nevals, st, lr);
+    double fo;
+    if (kp.batch) {
+      const double fk = readlane_d(f_lane, k);
+      if (((certmask >> k) & 1ull) || fk != fk || kp.max_iters <= 0) {
+        // the iteration stops at its start point: x = clamp(x_start), f = −α(x_start)
+        if (lane < D) U[Ly::U_NX + lane] = clampd(W.XS[k * D + lane], U[Ly::U_LB + lane], U[Ly::U_UB + lane]);
+        wave_sync();
+        fo = fk;
+      } else {
+        fo = newton<D, RPL>(W, kp, S, k, nevals, st, lr, fk, true);
+      }
+    } else {
+      fo = newton<D, RPL>(W, kp, S, k, nevals, st, lr, 0.0, false);
+    }
     bool xnan = false;
 #pragma unroll
     for (int a = 0; a < D; ++a) xnan = xnan || (U[Ly::U_NX + a] != U[Ly::U_NX + a]);
@@ -1458,7 +1647,11 @@ template <int D, int RPL>
 __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp, double* smem, int wave_in_block) {
   using Ly = Lay<D, RPL>;
   W.lane = threadIdx.x & (WAVE - 1);
-  double* wbase = smem + Ly::LINV_DOUBLES + (long long)wave_in_block * Ly::WAVE_LDS;
+  const WgTables<D, RPL> tb(kp);
+  double* wbase = smem + tb.end + (long long)wave_in_block * Ly::WAVE_LDS;
+  W.XS = kp.xs_lds ? smem + tb.xs : kp.xstarts;
+  W.KXB = smem + tb.kxb;
+  W.Y0SQ = smem + tb.y0sq;
   W.B = wbase;
   W.red = wbase + Ly::BROWS * Ly::BS;
   W.U = W.red + Ly::REDN;
@@ -1486,10 +1679,15 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
 template <int D, int RPL>
 __global__ void __launch_bounds__(512, MRBO_WAVES_PER_SIMD) rollout_kernel(KParams kp) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  // stage L0⁻¹ once per workgroup (the only block-wide barrier)
+  // stage L0⁻¹ (and the inner-solve start points) once per workgroup (the only block barrier)
   using Ly = Lay<D, RPL>;
   for (int q = threadIdx.x; q < (int)Ly::LINV_DOUBLES; q += blockDim.x) smem[q] = kp.Linv[q];
+  if (kp.xs_lds)
+    for (int q = threadIdx.x; q < kp.nstarts * D; q += blockDim.x) smem[Ly::LINV_DOUBLES + q] = kp.xstarts[q];
   __syncthreads();
+  if constexpr (Ly::SQ) {
+    if (kp.batch) stage_start_tables<D, RPL>(kp, smem);
+  }
   WaveCtx<D, RPL> W;
   wave_setup<D, RPL>(W, kp, smem, threadIdx.x / WAVE);
   wave_sync();
