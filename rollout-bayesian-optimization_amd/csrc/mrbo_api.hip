@@ -506,7 +506,8 @@ int mrbo_simulate_mc(mrbo_plan_t* P, const double* x0s, const double* rnstream, 
                                               "sigma+EI partials", "backward w/P", "Hessian reductions",
                                               "Hessian assembly", "Newton/draw bookkeeping (outside eval)",
                                               "adjoint pair", "draw+condition", "resolve+adjoint setup",
-                                              "Newton accept/convergence", "Newton direction", "Newton trial point"};
+                                              "Newton accept/convergence", "Newton direction", "Newton trial point",
+                                              "batched start values", "multistart loop (certified starts)"};
     unsigned long long hs[20];
     HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipMemcpy(hs, dstamps, sizeof(hs), hipMemcpyDeviceToHost));

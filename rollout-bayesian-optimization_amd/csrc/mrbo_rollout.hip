@@ -151,7 +151,7 @@ struct Counters {
 #else
 #define STAMP(W, k) ((void)0)
 #endif
-constexpr int NSTAMP = 15;
+constexpr int NSTAMP = 17;
 
 // Per-lane results of an evaluation that later phases (conditioning, adjoint) need.
 template <int D, int RPL>
@@ -1141,7 +1141,8 @@ __device__ __forceinline__ void stage_start_tables(const KParams& kp, double* sm
 // Replaces nstarts value evaluations (and their wave-redundant EI) by one pass.
 template <int D, int RPL>
 __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KParams& kp, int S, double& f_lane,
-                                                   unsigned long long& certmask, bool& varneg) {
+                                                   unsigned long long& stopmask, unsigned long long& xnanmask,
+                                                   bool& varneg) {
   using Ly = Lay<D, RPL>;
   constexpr int NR = Ly::NR;
   const double* U = W.U;
@@ -1156,13 +1157,14 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
 #pragma unroll
   for (int r = 0; r < FMAX; ++r) ae[r] = 0.0;
   const double* cS = W.C + (long long)(S + 1) * NR;
-#pragma unroll 4
+  // all FMAX rows unconditionally (rows ≥ nf hold finite stale values, masked below): a load
+  // under a condition would become a branch with a full LDS round trip per row
+#pragma unroll 8
   for (int i = 0; i < W.N; ++i) {
     const double kv = W.KXB[i * ns + k];
     amu = fma(cS[i], kv, amu);
 #pragma unroll
-    for (int r = 0; r < FMAX; ++r)
-      if (r < nf) ae[r] = fma(W.E[(long long)r * NR + i], kv, ae[r]);
+    for (int r = 0; r < FMAX; ++r) ae[r] = fma(W.E[(long long)r * NR + i], kv, ae[r]);
   }
   double pf[FMAX];
 #pragma unroll
@@ -1194,7 +1196,13 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   if (!cert && kp.gcert_sig > 0.0)
     cert = fabs(e.gmu) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + e.gsig * kp.gcert_sig / sig <= 0.25 * kp.g_tol;
   f_lane = -e.g;
-  certmask = __ballot(act && cert);
+  // the iteration stops at the start point: certified, f NaN, or no iterations allowed
+  const bool stop = cert || (f_lane != f_lane) || kp.max_iters <= 0;
+  bool xn = false;
+#pragma unroll
+  for (int a = 0; a < D; ++a) xn = xn || (x[a] != x[a]);
+  stopmask = __ballot(act && stop);
+  xnanmask = __ballot(act && xn);
   varneg = __ballot(act && var < 0.0) != 0;
 }
 
@@ -1222,36 +1230,28 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
     wave_sync();
   }
   double f_lane = 0.0;
-  unsigned long long certmask = 0;
+  unsigned long long stopmask = 0, xnanmask = 0;
   if (kp.batch) {
     bool varneg = false;
-    batch_start_values<D, RPL>(W, kp, S, f_lane, certmask, varneg);
+    STAMP(W, 16);
+    batch_start_values<D, RPL>(W, kp, S, f_lane, stopmask, xnanmask, varneg);
+    STAMP(W, 15);
     nevals.value += kp.nstarts;
     if (varneg) st |= 1;
     wave_sync();
   }
+  // starts that need a Newton iteration, in index order (all of them without kp.batch)
   for (int k = 0; k < kp.nstarts; ++k) {
-    double fo;
-    if (kp.batch) {
-      const double fk = readlane_d(f_lane, k);
-      if (((certmask >> k) & 1ull) || fk != fk || kp.max_iters <= 0) {
-        // the iteration stops at its start point: x = clamp(x_start), f = −α(x_start)
-        if (lane < D) U[Ly::U_NX + lane] = clampd(W.XS[k * D + lane], U[Ly::U_LB + lane], U[Ly::U_UB + lane]);
-        wave_sync();
-        fo = fk;
-      } else {
-        fo = newton<D, RPL>(W, kp, S, k, nevals, st, lr, fk, true);
-      }
-    } else {
-      fo = newton<D, RPL>(W, kp, S, k, nevals, st, lr, 0.0, false);
-    }
+    if ((stopmask >> k) & 1ull) continue;
+    const double fo = kp.batch ? newton<D, RPL>(W, kp, S, k, nevals, st, lr, readlane_d(f_lane, k), true)
+                               : newton<D, RPL>(W, kp, S, k, nevals, st, lr, 0.0, false);
     bool xnan = false;
 #pragma unroll
     for (int a = 0; a < D; ++a) xnan = xnan || (U[Ly::U_NX + a] != U[Ly::U_NX + a]);
     if (xnan) continue;
     bool take = false;
     if (fo != fo) {
-      if (!best_nan) { best_nan = true; take = true; }
+      if (!best_nan) { best_nan = true; best = k; take = true; }
     } else if (!best_nan && (best < 0 || fo < bestf)) {
       best = k;
       bestf = fo;
@@ -1261,6 +1261,35 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
       if (lane < D) U[Ly::U_XB + lane] = U[Ly::U_NX + lane];
       wave_sync();
     }
+  }
+  if (stopmask) {
+    // starts that stopped at x = clamp(x_start) with f = f_lane, merged under findmin's order
+    // semantics (rbf_optim.jl:96-98): the first NaN f wins, else the first minimum; NaN x dropped
+    const int ns = kp.nstarts;
+    const bool mine = lane < ns && ((stopmask >> lane) & 1ull) && !((xnanmask >> lane) & 1ull);
+    const unsigned long long nanm = __ballot(mine && f_lane != f_lane);
+    int win = -1;
+    bool win_nan = false;
+    if (nanm) {
+      const int kn = __builtin_ctzll(nanm);
+      if (!best_nan || kn < best) { win = kn; win_nan = true; }
+    } else if (!best_nan) {
+      double m = mine ? f_lane : INFINITY;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) m = fmin(m, __shfl_xor(m, o, WAVE));
+      const unsigned long long eq = __ballot(mine && f_lane == m);
+      if (eq) {
+        const int km = __builtin_ctzll(eq);
+        if (best < 0 || m < bestf || (m == bestf && km < best)) win = km;
+      }
+    }
+    if (win >= 0) {
+      if (lane < D) U[Ly::U_XB + lane] = clampd(W.XS[win * D + lane], U[Ly::U_LB + lane], U[Ly::U_UB + lane]);
+      wave_sync();
+      best = win;
+      best_nan = best_nan || win_nan;
+    }
+    STAMP(W, 16);
   }
   if (st) return st;
   if (best < 0 && !best_nan) return 8;
