@@ -252,7 +252,9 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   for (int s = 0; s < RPL; ++s) {
     lr.cb[s] = W.C[(long long)(S + 1) * NR + lane + WAVE * s];
 #pragma unroll
-    for (int r = 0; r < FMAX; ++r) Ev[s][r] = (r < nf) ? W.E[(long long)r * NR + lane + WAVE * s] : 0.0;
+    for (int r = 0; r < FMAX; ++r) Ev[s][r] = W.E[(long long)r * NR + lane + WAVE * s];   // unconditional
+#pragma unroll
+    for (int r = 0; r < FMAX; ++r) Ev[s][r] = (r < nf) ? Ev[s][r] : 0.0;
   }
 
   const int N = W.N;
@@ -710,7 +712,8 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     const int b = a + rem;
     const double gma = U[Ly::U_GMU + a], gmb = U[Ly::U_GMU + b];
     const double gsa = U[Ly::U_GSIG + a], gsb = U[Ly::U_GSIG + b];
-    double hv = red[lane] + ((a == b) ? red[Ly::NH] : 0.0);
+    const double rdiag = red[Ly::NH];
+    double hv = red[lane] + ((a == b) ? rdiag : 0.0);
     // fantasy data points ([x − X_r, g1, g2] from phase 1)
     for (int r = 0; r < nf; ++r) {
       const double* hf = U + Ly::U_HF + r * (D + 2);
@@ -846,19 +849,40 @@ __device__ __forceinline__ bool chol_packed(double (&A)[D * (D + 1) / 2], double
   return ok;
 }
 
+// Free set of the projected Newton step and the projected-gradient norm max_F |g_a|.  All
+// operands are loaded unconditionally and combined without short-circuits: a load behind
+// && / || becomes a branch with a full LDS round trip.
+template <int D, int RPL>
+__device__ __forceinline__ double newton_free_set(const WaveCtx<D, RPL>& W, bool (&fr)[D], double (&gs)[D],
+                                                  double& box) {
+  using Ly = Lay<D, RPL>;
+  const double* U = W.U;
+  double xs[D], lb[D], ub[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) {
+    xs[a] = U[Ly::U_NX + a];
+    gs[a] = U[Ly::U_NG + a];
+    lb[a] = U[Ly::U_LB + a];
+    ub[a] = U[Ly::U_UB + a];
+  }
+  double pg = 0.0;
+  box = 0.0;
+#pragma unroll
+  for (int a = 0; a < D; ++a) {
+    const bool act = ((xs[a] <= lb[a]) & (gs[a] > 0.0)) | ((xs[a] >= ub[a]) & (gs[a] < 0.0));
+    fr[a] = !act;
+    pg = act ? pg : fmax(pg, fabs(gs[a]));
+    box = fmax(box, ub[a] - lb[a]);
+  }
+  return pg;
+}
+
 // Projected-gradient test of the Newton iteration: max |g_a| over the free coordinates > g_tol.
 template <int D, int RPL>
 __device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL>& W, const KParams& kp) {
-  using Ly = Lay<D, RPL>;
-  const double* U = W.U;
-  double pg = 0.0;
-#pragma unroll
-  for (int a = 0; a < D; ++a) {
-    const double xa = U[Ly::U_NX + a], ga = U[Ly::U_NG + a];
-    const bool act = (xa <= U[Ly::U_LB + a] && ga > 0.0) || (xa >= U[Ly::U_UB + a] && ga < 0.0);
-    if (!act) pg = fmax(pg, fabs(ga));
-  }
-  return pg > kp.g_tol;
+  bool fr[D];
+  double gs[D], box;
+  return newton_free_set<D, RPL>(W, fr, gs, box) > kp.g_tol;
 }
 
 // One projected-Newton direction from the state in U (x = U_NX, g = U_NG, H = U_H).
@@ -868,14 +892,8 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
   using Ly = Lay<D, RPL>;
   double* U = W.U;
   bool fr[D];
-  double pg = 0.0;
-#pragma unroll
-  for (int a = 0; a < D; ++a) {
-    const double xa = U[Ly::U_NX + a], ga = U[Ly::U_NG + a];
-    const bool act = (xa <= U[Ly::U_LB + a] && ga > 0.0) || (xa >= U[Ly::U_UB + a] && ga < 0.0);
-    fr[a] = !act;
-    if (!act) pg = fmax(pg, fabs(ga));
-  }
+  double gs[D], box;
+  const double pg = newton_free_set<D, RPL>(W, fr, gs, box);
   if (!(pg > kp.g_tol)) return false;
   // lower triangle of Hα, read unconditionally (a load under a select becomes a branch with a
   // full LDS round trip per element)
@@ -928,7 +946,7 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
     double t1[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-      double s = fr[i] ? U[Ly::U_NG + i] : 0.0;
+      double s = fr[i] ? gs[i] : 0.0;
 #pragma unroll
       for (int k = 0; k < i; ++k) s -= A[i * (i + 1) / 2 + k] * t1[k];
       t1[i] = s * idg[i];
@@ -944,11 +962,11 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
     for (int i = 0; i < D; ++i) p[i] = fr[i] ? -p[i] : 0.0;
   } else {
 #pragma unroll
-    for (int i = 0; i < D; ++i) p[i] = fr[i] ? -U[Ly::U_NG + i] : 0.0;
+    for (int i = 0; i < D; ++i) p[i] = fr[i] ? -gs[i] : 0.0;
   }
-  double pn = 0.0, box = 0.0;
+  double pn = 0.0;
 #pragma unroll
-  for (int i = 0; i < D; ++i) { pn = fmax(pn, fabs(p[i])); box = fmax(box, U[Ly::U_UB + i] - U[Ly::U_LB + i]); }
+  for (int i = 0; i < D; ++i) pn = fmax(pn, fabs(p[i]));
   const double sc = (pn > box) ? box / pn : 1.0;
   wave_sync();
   const int lane = W.ln();
@@ -988,10 +1006,9 @@ __device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const K
   using Ly = Lay<D, RPL>;
   const double* U = W.U;
   const double gm = U[Ly::U_SC + SC_GMU], gs = U[Ly::U_SC + SC_GSIG];
-  if (gm == 0.0 && gs == 0.0) return true;
-  if (!(kp.gcert_sig > 0.0)) return false;
-  const double bound = fabs(gm) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + gs * kp.gcert_sig / U[Ly::U_SC + SC_SIG];
-  return bound <= 0.25 * kp.g_tol;
+  const double cabs = U[Ly::U_SC + SC_CABS], sig = U[Ly::U_SC + SC_SIG];   // unconditional loads
+  const double bound = fabs(gm) * kp.gcert_mu * cabs + gs * kp.gcert_sig / sig;
+  return ((gm == 0.0) & (gs == 0.0)) | ((kp.gcert_sig > 0.0) & (bound <= 0.25 * kp.g_tol));
 }
 
 // Deterministic projected Newton on f = -α over the box, from start k.
@@ -1359,7 +1376,10 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
   // fantasy rows r ≤ S are added here (∇k(X_q − X_q) = 0 drops r = q).
   double dl[D];
 #pragma unroll
-  for (int a = 0; a < D; ++a) dl[a] = (lane == D) ? U[Ly::U_DX + a] : ((a == lane) ? 1.0 : 0.0);
+  for (int a = 0; a < D; ++a) {
+    const double dxa = U[Ly::U_DX + a];
+    dl[a] = (lane == D) ? dxa : ((a == lane) ? 1.0 : 0.0);
+  }
   double udc = 0.0, udw = 0.0, Pu[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) { udc = fma(red[k], dl[k], udc); udw = fma(red[D + k], dl[k], udw); }
