@@ -275,6 +275,18 @@ __host__ __device__ __forceinline__ double dual_uniform(unsigned long long seed,
   return (double)(key >> 11) * (1.0 / 9007199254740992.0);
 }
 
+// √s and 1/√s (s > 0) from one hardware reciprocal square root and two Newton–Raphson steps
+// y ← y(1.5 − ½s·y²): ~1 ulp, and a much shorter dependent chain than a correctly rounded
+// sqrt followed by an IEEE division (Cholesky pivots of the Newton step and of gp_draw).
+__device__ __forceinline__ void sqrt_rsqrt(double s, double& r, double& ir) {
+  const double h = 0.5 * s;
+  double y = __builtin_amdgcn_rsq(s);
+  y = fma(y, fma(-h * y, y, 0.5), y);
+  y = fma(y, fma(-h * y, y, 0.5), y);
+  ir = y;
+  r = s * y;
+}
+
 // value of a double in lane k (wave-uniform k)
 __device__ __forceinline__ double readlane_d(double v, int k) {
   int lo, hi;

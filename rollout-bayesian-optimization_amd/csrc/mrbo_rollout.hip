@@ -140,7 +140,7 @@ struct WaveCtx {
 // evals[NCOUNT·t + k], k = gradient evals, value evals, Hessians, adjoint rich evals, pairs
 constexpr int NCOUNT = 5;
 struct Counters {
-  long long grad = 0, value = 0, hess = 0, rich = 0, pairs = 0;
+  int grad = 0, value = 0, hess = 0, rich = 0, pairs = 0;
 };
 
 // Optional per-phase cycle accounting (build with -DMRBO_STAMPS): STAMP(W, k) charges the
@@ -408,6 +408,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     // ∇μ and fantasy cross products for the gradient columns
 #pragma unroll
     for (int ch = 0; ch < Ly::NMFC; ++ch) {
+      if (16 * ch >= D * (1 + nf)) break;   // fantasy rows ≥ nf carry nothing
       double v[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -791,8 +792,8 @@ __device__ __forceinline__ int draw(WaveCtx<D, RPL>& W, const KParams& kp, const
 #pragma unroll
     for (int k = 0; k < j; ++k) sdiag -= Lc[TRI(j, k)] * Lc[TRI(j, k)];
     if (!(sdiag > 0.0)) return 2;
-    const double ljj = sqrt(sdiag);
-    const double ij = 1.0 / ljj;
+    double ljj, ij;
+    sqrt_rsqrt(sdiag, ljj, ij);
     Lc[TRI(j, j)] = ljj;
 #pragma unroll
     for (int i = j + 1; i < D1; ++i) {
@@ -834,9 +835,9 @@ __device__ __forceinline__ bool chol_packed(double (&A)[D * (D + 1) / 2], double
 #pragma unroll
     for (int k = 0; k < j; ++k) s -= A[TRI(j, k)] * A[TRI(j, k)];
     ok = ok && (s > 0.0);
-    const double ljj = sqrt(s);
+    double ljj;
+    sqrt_rsqrt(s, ljj, idg[j]);
     A[TRI(j, j)] = ljj;
-    idg[j] = 1.0 / ljj;
 #pragma unroll
     for (int i = j + 1; i < D; ++i) {
       double t = A[TRI(i, j)];
@@ -1462,12 +1463,15 @@ __device__ __forceinline__ bool lu_det_solve(double (&A)[D][D], double* b, doubl
 #pragma unroll
     for (int i = k + 1; i < D; ++i) if (fabs(A[i][k]) > mx) { mx = fabs(A[i][k]); p = i; }
     piv[k] = p;
+    // row swap k <-> p as selects (a conditional swap becomes a dynamically indexed scratch array)
 #pragma unroll
-    for (int i = k + 1; i < D; ++i) {
-      if (i == p) {
+    for (int j = 0; j < D; ++j) {
+      double rowp = A[k][j];
 #pragma unroll
-        for (int j = 0; j < D; ++j) { const double t = A[k][j]; A[k][j] = A[i][j]; A[i][j] = t; }
-      }
+      for (int i = k + 1; i < D; ++i) rowp = (i == p) ? A[i][j] : rowp;
+#pragma unroll
+      for (int i = k + 1; i < D; ++i) A[i][j] = (i == p) ? A[k][j] : A[i][j];
+      A[k][j] = rowp;
     }
     if (A[k][k] == 0.0) { sing = true; continue; }
 #pragma unroll
@@ -1484,10 +1488,12 @@ __device__ __forceinline__ bool lu_det_solve(double (&A)[D][D], double* b, doubl
   if (!do_solve || sing) return !sing;
 #pragma unroll
   for (int k = 0; k < D; ++k) {
+    double bp = b[k];
 #pragma unroll
-    for (int i = k + 1; i < D; ++i) {
-      if (i == piv[k]) { const double t = b[k]; b[k] = b[i]; b[i] = t; }
-    }
+    for (int i = k + 1; i < D; ++i) bp = (i == piv[k]) ? b[i] : bp;
+#pragma unroll
+    for (int i = k + 1; i < D; ++i) b[i] = (i == piv[k]) ? b[k] : b[i];
+    b[k] = bp;
   }
 #pragma unroll
   for (int i = 0; i < D; ++i) {
