@@ -55,6 +55,7 @@ struct mrbo_plan {
   double* dlbs = nullptr;
   double* dubs = nullptr;
   double* dwork = nullptr;
+  double* dytab = nullptr;  // batched starts: per-workgroup Y0(x_start) slices
   long long work_stride = 0;
   int* dqueue = nullptr;
   int wpg = 4, blocks = 0;
@@ -251,7 +252,7 @@ static void fill_common(const mrbo_plan_t* P, KParams& kp) {
   kp.sample_offset = P->p.sample_offset;
   kp.samples_total = P->p.samples_total > 0 ? P->p.samples_total : P->p.M;
   kp.X0 = P->dX0; kp.c0 = P->dc0; kp.Linv = P->dLinv; kp.lbs = P->dlbs; kp.ubs = P->dubs;
-  kp.work = P->dwork; kp.work_stride = P->work_stride; kp.queue = P->dqueue;
+  kp.work = P->dwork; kp.work_stride = P->work_stride; kp.queue = P->dqueue; kp.ytab = P->dytab;
 }
 
 // staging helper for MRBO_FLAG_HOST_POINTERS
@@ -397,7 +398,8 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   P->xs_lds = xs_bytes <= 8192 ? 1 : 0;
   // batched start values: start tables kxb (NR × ns) and y0sq (ns), square L0⁻¹ only; kept only
   // if they cost no resident waves
-  const size_t kxb_bytes = sizeof(double) * ((((size_t)P->NR * ns + 1) & ~(size_t)1) + (((size_t)ns + 1) & ~(size_t)1));
+  const size_t ng = (size_t)(d + 1) * (d + 2) / 2;
+  const size_t kxb_bytes = sizeof(double) * ((((size_t)P->NR * ns + 1) & ~(size_t)1) + (((size_t)ns * ng + 1) & ~(size_t)1));
   const size_t fixed = linv_bytes + (P->xs_lds ? xs_bytes : 0);
   int wpg0 = 0, blocks0 = 0;
   size_t smem0 = 0;
@@ -407,7 +409,7 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
     int wpg1 = 0, blocks1 = 0;
     size_t smem1 = 0;
     const int waves1 = pick_grid(ks.rollout, fixed + kxb_bytes, ks.wave_bytes, prop.multiProcessorCount, wpg1, blocks1,
-                                 smem1, sizeof(double) * (size_t)P->NR * ns);
+                                 smem1);
     if (waves1 >= waves0 && waves1 > 0) { P->batch = 1; P->wpg = wpg1; P->blocks = blocks1; P->smem = smem1; }
   }
   if (!P->batch) { P->wpg = wpg0; P->blocks = blocks0; P->smem = smem0; }
@@ -424,6 +426,7 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
             hipMalloc(&P->dlbs, sizeof(double) * d) == hipSuccess &&
             hipMalloc(&P->dubs, sizeof(double) * d) == hipSuccess &&
             hipMalloc(&P->dwork, sizeof(double) * (size_t)slots * P->work_stride) == hipSuccess &&
+            (!P->batch || hipMalloc(&P->dytab, sizeof(double) * (size_t)P->blocks * ns * P->NR) == hipSuccess) &&
             hipMalloc(&P->dqueue, sizeof(int) * 4) == hipSuccess;
   ok = ok && hipMemcpy(P->dX0, X0.data(), sizeof(double) * X0.size(), hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(P->dc0, c0.data(), sizeof(double) * c0.size(), hipMemcpyHostToDevice) == hipSuccess &&
@@ -442,7 +445,7 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
 
 int mrbo_plan_destroy(mrbo_plan_t* P) {
   if (!P) return MRBO_OK;
-  for (void* b : {(void*)P->dX0, (void*)P->dc0, (void*)P->dLinv, (void*)P->dlbs, (void*)P->dubs, (void*)P->dwork,
+  for (void* b : {(void*)P->dX0, (void*)P->dc0, (void*)P->dLinv, (void*)P->dlbs, (void*)P->dubs, (void*)P->dwork, (void*)P->dytab,
                   (void*)P->dqueue})
     if (b) (void)hipFree(b);
   if (P->ev0) (void)hipEventDestroy(P->ev0);

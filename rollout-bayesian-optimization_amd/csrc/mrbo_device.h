@@ -26,7 +26,9 @@ constexpr int WAVE = 64;
 //   DRAW   GRAD + w (condition!)       FULL  GRAD + w + Hα
 //   RICH   FULL + P = L⁻ᵀV (adjoint)   BACK  w + Hα at the point of the preceding GRAD(C)
 //   GRADC  completes a VALUE evaluation to GRAD (gradient columns only; same results)
-enum { EV_VALUE = 0, EV_GRAD = 1, EV_DRAW = 2, EV_FULL = 3, EV_RICH = 4, EV_BACK = 5, EV_GRADC = 6 };
+//   GSTART GRAD at an inner-solve start point: the base forward product and base Gram come
+//          from the launch's start tables (stage_start_tables), only surface terms are computed
+enum { EV_VALUE = 0, EV_GRAD = 1, EV_DRAW = 2, EV_FULL = 3, EV_RICH = 4, EV_BACK = 5, EV_GRADC = 6, EV_GSTART = 7 };
 
 struct KParams {
   int d, N, Npad, h, M, R, nstarts;
@@ -62,6 +64,7 @@ struct KParams {
   long long* evals;
   double* work;         // per wave-slot global scratch
   long long work_stride;
+  double* ytab;         // kp.batch: per-workgroup slices [blockIdx][nstarts][NR] of Y0(x_start)
   int* queue;           // work-queue head (zeroed before every launch)
   long long T;          // trajectories (or points for eval_base)
   const double* pts;    // eval_base: d×P

@@ -93,19 +93,21 @@ struct Lay {
 enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, SC_GSIG = 6, SC_GMUMU = 7,
        SC_GSIGSIG = 8, SC_GMUTH = 9, SC_GSIGTH = 10, SC_FMIN = 11, SC_ST = 12, SC_CABS = 13 };
 
-// Per-workgroup LDS after L0⁻¹: [xstarts (d×nstarts)] [kxb (NR×nstarts)] [y0sq (nstarts)],
-// each rounded to an even number of doubles; then the per-wave areas.
+// Per-workgroup LDS after L0⁻¹: [xstarts (d×nstarts)] [kxb (NR×nstarts)] [gtab (nstarts×NG)],
+// each rounded to an even number of doubles; then the per-wave areas.  gtab[k] is the base
+// Gram of start k, (L0⁻¹B)ᵀ(L0⁻¹B) with B = [kx, ∇kx](x_k), upper triangle row-major; its
+// entry 0 is |L0⁻¹kx(x_k)|².
 template <int D, int RPL>
 struct WgTables {
-  long long xs, kxb, y0sq, end;   // offsets in doubles from smem
+  long long xs, kxb, gtab, end;   // offsets in doubles from smem
   __device__ __forceinline__ WgTables(const KParams& kp) {
     using Ly = Lay<D, RPL>;
     xs = Ly::LINV_DOUBLES;
     const long long nxs = kp.xs_lds ? (((long long)kp.nstarts * D + 1) & ~1LL) : 0;
     kxb = xs + nxs;
     const long long nk = kp.batch ? (((long long)Ly::NR * kp.nstarts + 1) & ~1LL) : 0;
-    y0sq = kxb + nk;
-    end = y0sq + (kp.batch ? ((kp.nstarts + 1) & ~1) : 0);
+    gtab = kxb + nk;
+    end = gtab + (kp.batch ? (((long long)kp.nstarts * Ly::NG + 1) & ~1LL) : 0);
   }
 };
 
@@ -119,7 +121,8 @@ struct WaveCtx {
   const double* Linv;   // LDS: L0⁻¹ (Lay::SQ layout)
   const double* XS;     // inner-solve start points: LDS copy (kp.xs_lds) or kp.xstarts
   const double* KXB;    // LDS [NR][nstarts]: ψ(|clamp(x_k) − X_i|) (kp.batch)
-  const double* Y0SQ;   // LDS [nstarts]: |L0⁻¹ kx(x_k)|² (kp.batch)
+  const double* GTAB;   // LDS [nstarts][NG]: base Gram of the start points (kp.batch)
+  const double* YTAB;   // global [nstarts][NR]: this workgroup's Y0(x_k) = L0⁻¹kx(x_k) (kp.batch)
   double* G12;          // LDS: per-lane [g1, g2, Y0] of the base rows (GRAD / FULL / RICH)
   double* E;            // LDS (SQ) or global: FMAX × NR  inverse-factor fantasy rows (base columns)
   double* C;            // LDS (SQ) or global: (FMAX+1) × NR  base part of c for surfaces -1..h
@@ -225,7 +228,8 @@ __device__ __forceinline__ void bcast_product(double (&acc)[K], const double (&v
 //   x is read from U[U_X].  Results land in U (lane-uniform) and `lr` (per lane).
 // ================================================================================
 template <int D, int RPL>
-__device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, int S, int mode, LaneRes<D, RPL>& lr) {
+__device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, int S, int mode, LaneRes<D, RPL>& lr,
+                                         int kst = 0) {
   using Ly = Lay<D, RPL>;
   constexpr int D1 = Ly::D1, BS = Ly::BS, NR = Ly::NR;
   // Opaque copy of the lane index: keeps the per-lane LDS/global addresses derived from it
@@ -317,6 +321,8 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       double a1[1] = {0.0}, v1[1] = {Bown[0][0]};
       bcast_product<1, Ly::LD>(a1, v1, W.Linv + lane, N);
       acc[0][0] = a1[0];
+    } else if (mode == EV_GSTART) {  // base forward product of start kst from the launch tables
+      acc[0][0] = W.YTAB[(long long)kst * NR + lane];
     } else if (mode == EV_GRADC) {   // columns 1..d; column 0 from the VALUE pass
       double ag[D], vg[D];
 #pragma unroll
@@ -384,9 +390,10 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     wave_reduce<8>(v, red + Ly::R_VAL, lane);
   }
   if (all_cols) {
-    // Gram entries (a ≤ b) except (0,0)
+    // Gram entries (a ≤ b) except (0,0); GSTART takes them from the start tables
 #pragma unroll
     for (int ch = 0; ch < Ly::NGC; ++ch) {
+      if (mode == EV_GSTART) break;
       double v[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -487,7 +494,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
 #pragma unroll
       for (int aa = 0; aa < D1; ++aa) if (a == aa && rem >= D1 - aa) { rem -= D1 - aa; a = aa + 1; }
       const int b = a + rem;
-      double g = red[Ly::R_G + lane - 1];
+      double g = (mode == EV_GSTART) ? W.GTAB[kst * Ly::NG + lane] : red[Ly::R_G + lane - 1];
       for (int r = 0; r < nf; ++r) g = fma(U[Ly::U_YFV + r * D1 + a], U[Ly::U_YFV + r * D1 + b], g);
       U[Ly::U_G + a * D1 + b] = g;
       U[Ly::U_G + b * D1 + a] = g;
@@ -541,7 +548,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     U[Ly::U_GAL + lane] = e_f.gmu * gm + e_f.gsig * gs;                // ∇αx :567
     U[Ly::U_MIX + lane] = gm * e_f.gmuth + gs * e_f.gsigth;            // d2α_dxdθ :575-577
   }
-  if (mode == EV_GRAD || mode == EV_GRADC) {   // a BACK evaluation may follow
+  if (mode == EV_GRAD || mode == EV_GRADC || mode == EV_GSTART) {   // a BACK evaluation may follow
     wave_sync();
     STAMP(W, 4);
     return;
@@ -1034,12 +1041,12 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
   wave_sync();
   // have_f0: the start's value (and certificate) came from batch_start_values and did not
   // stop the iteration, so it begins with the gradient at x_start
-  int phase = have_f0 ? P_GRAD : P_VAL, mode = have_f0 ? EV_GRAD : EV_VALUE, it = 0, ls = 0;
+  int phase = have_f0 ? P_GRAD : P_VAL, mode = have_f0 ? EV_GSTART : EV_VALUE, it = 0, ls = 0;
   double f = have_f0 ? f0 : 0.0, ft = 0.0, t = 1.0, dec = 0.0;
   for (;;) {
-    evaluate<D, RPL>(W, kp, S, mode, lr);
+    evaluate<D, RPL>(W, kp, S, mode, lr, k);
     if (mode == EV_VALUE) ++nevals.value;
-    else if (mode == EV_GRADC || mode == EV_GRAD) ++nevals.grad;
+    else if (mode == EV_GRADC || mode == EV_GRAD || mode == EV_GSTART) ++nevals.grad;
     else ++nevals.hess;
     if (phase == P_HESS) {                 // Hα at x ready: step
       STAMP(W, 12);
@@ -1106,7 +1113,8 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
 
 // Workgroup prologue (kp.batch): base kernel rows of the clamped start points and the squared
 // norms of their forward products -- constants of the launch shared by every multistart.
-//   kxb[i][k] = ψ(|x_k − X_i|) (0 on padded rows),  y0sq[k] = |L0⁻¹ kxb[:,k]|²
+//   kxb[i][k] = ψ(|x_k − X_i|) (0 on padded rows);  per start, Y = L0⁻¹[kx, ∇kx](x_k):
+//   Y0 → this workgroup's global slice kp.ytab, base Gram YᵀY → gtab (LDS)
 // The per-wave areas (not yet initialised) serve as scratch for the squares.
 template <int D, int RPL>
 __device__ __forceinline__ void stage_start_tables(const KParams& kp, double* smem) {
@@ -1116,8 +1124,6 @@ __device__ __forceinline__ void stage_start_tables(const KParams& kp, double* sm
   const int ns = kp.nstarts;
   const double* xs = smem + tb.xs;
   double* kxb = smem + tb.kxb;
-  double* y0sq = smem + tb.y0sq;
-  double* sq = smem + tb.end;                 // scratch NR × ns (wave areas, re-zeroed by wave_setup)
   Radial rad;
   rad.kind = kp.kernel;
   rad.cK = kp.cK;
@@ -1137,25 +1143,57 @@ __device__ __forceinline__ void stage_start_tables(const KParams& kp, double* sm
     kxb[q] = v;
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < NR * ns; q += blockDim.x) {
-    const int i = q / ns, k = q - (q / ns) * ns;
-    double y = 0.0;
-    for (int j = 0; j <= i && j < kp.N; ++j) y = fma(smem[j * Ly::LD + i], kxb[j * ns + k], y);
-    sq[q] = y * y;
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < ns; k += blockDim.x) {
-    double t = 0.0;
-    for (int i = 0; i < kp.N; ++i) t += sq[i * ns + k];
-    y0sq[k] = t;
+  // per start (waves in turn): Y = L0⁻¹[kx, ∇kx](x_k) by the register-broadcast product, Y0 to
+  // this workgroup's global slice, the base Gram YᵀY (upper triangle) to gtab
+  const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+  double* red = smem + tb.end + (long long)wv * Ly::WAVE_LDS;   // wave-area scratch
+  double* ytab = kp.ytab + (long long)blockIdx.x * ns * NR;
+  for (int k = wv; k < ns; k += nw) {
+    double bv[Ly::D1], acc[Ly::D1];
+    double rho2 = 0.0, r[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+      r[a] = clampd(xs[k * D + a], kp.lbs[a], kp.ubs[a]) - kp.X0[(long long)a * NR + lane];
+      rho2 = fma(r[a], r[a], rho2);
+    }
+    double psi, g1, g2;
+    rad_eval(rad, rho2, psi, g1, g2);
+    const bool v = lane < kp.N;
+    bv[0] = v ? psi : 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) bv[1 + a] = v ? g1 * r[a] : 0.0;
+#pragma unroll
+    for (int c = 0; c < Ly::D1; ++c) acc[c] = 0.0;
+    bcast_product<Ly::D1, Ly::LD>(acc, bv, smem + lane, kp.N);
+    ytab[(long long)k * NR + lane] = acc[0];
+#pragma unroll
+    for (int ch = 0; ch < (Ly::NG + 15) / 16; ++ch) {
+      double gv[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int t = 16 * ch + q;
+        double s_ = 0.0;
+        if (t < Ly::NG) {
+          int a = 0, rem = t;
+#pragma unroll
+          for (int aa = 0; aa < Ly::D1; ++aa) if (a == aa && rem >= Ly::D1 - aa) { rem -= Ly::D1 - aa; a = aa + 1; }
+          s_ = acc[a] * acc[a + rem];
+        }
+        gv[q] = s_;
+      }
+      wave_reduce<16>(gv, red + 16 * ch, lane);
+    }
+    wave_sync();
+    if (lane < Ly::NG) smem[tb.gtab + (long long)k * Ly::NG + lane] = red[lane];
+    wave_sync();
   }
   __syncthreads();
 }
 
 // Values of ALL start points of a multistart on surface S at once (kp.batch): lane k takes start
-// k.  With the launch constants kxb, y0sq only the surface-dependent parts remain:
+// k.  With the launch constants kxb, gtab only the surface-dependent parts remain:
 //   μ_k = c_S·kxb[:,k] + Σ_r c_r ψ(x_k, X_r),  Yf_r = E_r·kxb[:,k] + Σ_{q≤r} Dinv[r][q] ψ(x_k, X_q),
-//   σ_k² = ψ(0) − y0sq[k] − Σ_r Yf_r²,  then α and the gradient certificate per lane.
+//   σ_k² = ψ(0) − gtab[k][0] − Σ_r Yf_r²,  then α and the gradient certificate per lane.
 // Replaces nstarts value evaluations (and their wave-redundant EI) by one pass.
 template <int D, int RPL>
 __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KParams& kp, int S, double& f_lane,
@@ -1196,7 +1234,7 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
       rad_eval(W.rad, rho2, pf[q], g1, g2);
     }
   }
-  double g00 = W.Y0SQ[k], mu = amu;
+  double g00 = W.GTAB[k * Ly::NG], mu = amu;
 #pragma unroll
   for (int r = 0; r < FMAX; ++r) {
     if (r < nf) {
@@ -1706,7 +1744,8 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
   double* wbase = smem + tb.end + (long long)wave_in_block * Ly::WAVE_LDS;
   W.XS = kp.xs_lds ? smem + tb.xs : kp.xstarts;
   W.KXB = smem + tb.kxb;
-  W.Y0SQ = smem + tb.y0sq;
+  W.GTAB = smem + tb.gtab;
+  W.YTAB = kp.ytab + (long long)blockIdx.x * kp.nstarts * Ly::NR;
   W.B = wbase;
   W.red = wbase + Ly::BROWS * Ly::BS;
   W.U = W.red + Ly::REDN;
