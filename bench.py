@@ -56,6 +56,12 @@ def cpu_baseline(pb, M_full, R_full, budget_s):
                       nthreads=nthreads, want_policy=False)
         return time.perf_counter() - t
 
+    def run1(Ms):   # the reference itself is single-process, single-thread
+        t = time.perf_counter()
+        O.simulate_mc(osur, pb.x0s[:, :1], np.asfortranarray(rn[:Ms]), xs, pb.lbs, pb.ubs, pb.cfg.h,
+                      nthreads=1, want_policy=False)
+        return time.perf_counter() - t
+
     Ms, Rs = min(M_full, max(nthreads * 4, 32)), 1
     dt = run(Ms, Rs)
     rate = Ms * Rs / dt
@@ -64,9 +70,15 @@ def cpu_baseline(pb, M_full, R_full, budget_s):
     Rs = max(1, min(R_full, target // M_full)) if target >= M_full else 1
     Ms = M_full if target >= M_full else max(Ms, min(M_full, target))
     dt = run(Ms, Rs)
+    M1 = min(M_full, 64)
+    dt1 = run1(M1)
+    M1 = min(M_full, max(M1, int(M1 / dt1 * budget_s * 0.3)))
+    dt1 = run1(M1)
     return dict(value=Ms * Rs / dt, unit="trajectories/s", cores=nthreads, kind="port",
                 sample=f"{pb.cfg.name} workload, first {Rs} restart(s) x {Ms} MC samples "
-                       f"({Ms * Rs} trajectories, {dt:.1f} s), oracle/rbo_oracle.c OpenMP x{nthreads}")
+                       f"({Ms * Rs} trajectories, {dt:.1f} s), oracle/rbo_oracle.c OpenMP x{nthreads}",
+                single_thread={"value": M1 / dt1, "cores": 1,
+                               "sample": f"first restart x {M1} MC samples ({dt1:.1f} s), 1 thread"})
 
 
 def main():

@@ -49,7 +49,11 @@ typedef enum {
   MRBO_KERNEL_SE = 3        /* :90-96 */
 } mrbo_kernel_t;
 
-typedef enum { MRBO_RULE_EI = 0 /* decision_rules.jl:84-99 */ } mrbo_rule_t;
+typedef enum {
+  MRBO_RULE_EI = 0,   /* decision_rules.jl:84-99   expected improvement                 */
+  MRBO_RULE_POI = 1,  /* decision_rules.jl:101-115 probability of improvement           */
+  MRBO_RULE_LCB = 2   /* decision_rules.jl:117-127 θσ − μ (negated lower confidence bound) */
+} mrbo_rule_t;
 
 /* per-trajectory status bits: the reference's exceptions (SURVEY.md §8b "Errors") */
 enum {
@@ -97,7 +101,7 @@ typedef struct {
   double f_tol;         /* Optim f_tol = 1e-3                                    */
   double g_tol;         /* Optim default g_tol = 1e-8                            */
   double htol;          /* solve_dual_x det threshold (rollout.jl:156) = 1e-4    */
-  double sigma_tol;     /* EI σtol (decision_rules.jl:84) = 1e-8                 */
+  double sigma_tol;     /* EI / POI σtol (decision_rules.jl:84, :102) = 1e-8     */
   uint64_t seed;        /* δx for solve_dual_y (rollout.jl:133) when dual_y_dx == NULL */
   int32_t sample_offset;/* global index of this plan's first MC sample (multi-GPU shard), 0 */
   int32_t samples_total;/* global MC samples per restart (0 → M); keys the δx counter RNG  */

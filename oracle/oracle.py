@@ -35,7 +35,7 @@ class Params(ctypes.Structure):
                 ("x_tol", ctypes.c_double), ("f_tol", ctypes.c_double), ("g_tol", ctypes.c_double),
                 ("htol", ctypes.c_double), ("sigma_tol", ctypes.c_double), ("seed", ctypes.c_uint64),
                 ("sample_offset", ctypes.c_int32), ("samples_total", ctypes.c_int32),
-                ("with_gradient", ctypes.c_int32), ("nthreads", ctypes.c_int32)]
+                ("with_gradient", ctypes.c_int32), ("nthreads", ctypes.c_int32), ("rule", ctypes.c_int32)]
 
 
 def build():
@@ -56,7 +56,8 @@ def lib():
         L.rbo_dual_uniform.restype = ctypes.c_double
         L.rbo_testfn.argtypes = [ctypes.c_int32, ctypes.c_int32, _dp]
         L.rbo_testfn.restype = ctypes.c_double
-        L.rbo_eval_base.argtypes = [ctypes.POINTER(Surrogate), ctypes.c_double, ctypes.c_double, ctypes.c_int32, _dp, _dp]
+        L.rbo_eval_base.argtypes = [ctypes.POINTER(Surrogate), ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+                                    ctypes.c_int32, _dp, _dp]
         L.rbo_simulate_mc.argtypes = [ctypes.POINTER(Surrogate), ctypes.POINTER(Params), _dp, _dp, _dp, _dp, _dp,
                                       _dp, _dp, _dp, _ip, _dp, _dp, _dp, _lp]
         _lib = L
@@ -116,19 +117,22 @@ class OracleSurrogate:
         self.s = Surrogate(d, N, KERNELS[kernel], ell, sigma_n2, fm, _p(self.X), _p(self.L), _p(self.c), _p(self.y))
 
 
-def eval_base(osur, xs, theta=0.0, sigma_tol=1e-8):
+RULES = {"EI": 0, "POI": 1, "LCB": 2}
+
+
+def eval_base(osur, xs, theta=0.0, sigma_tol=1e-8, rule="EI"):
     xs = _f64(xs)
     d, P = xs.shape
     stride = 3 + 4 * d + d * d
     out = np.zeros((stride, P), order="F")
-    assert lib().rbo_eval_base(ctypes.byref(osur.s), theta, sigma_tol, P, _p(xs), _p(out)) == 0
+    assert lib().rbo_eval_base(ctypes.byref(osur.s), RULES[rule], theta, sigma_tol, P, _p(xs), _p(out)) == 0
     return out
 
 
 def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=None, replay_x=None,
                 max_iters=50, max_ls=20, x_tol=1e-3, f_tol=1e-3, g_tol=1e-8, htol=1e-4, sigma_tol=1e-8,
                 seed=1906, with_gradient=True, nthreads=0, want_policy=True, sample_offset=0,
-                samples_total=0):
+                samples_total=0, rule="EI"):
     """Run the oracle's simulate_trajectory_mc for every restart column of x0s (d×R)."""
     x0s, rnstream, xstarts = _f64(x0s), _f64(rnstream), _f64(xstarts)
     lbs, ubs = _f64(lbs), _f64(ubs)
@@ -136,7 +140,8 @@ def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=
     M = rnstream.shape[0]
     assert rnstream.shape == (M, d + 1, h + 1), rnstream.shape
     prm = Params(h, M, R, xstarts.shape[1], theta, _p(lbs), _p(ubs), max_iters, max_ls, x_tol, f_tol, g_tol,
-                 htol, sigma_tol, seed, sample_offset, samples_total, 1 if with_gradient else 0, nthreads)
+                 htol, sigma_tol, seed, sample_offset, samples_total, 1 if with_gradient else 0, nthreads,
+                 RULES[rule])
     values = np.zeros((M, R), order="F")
     grad_x = np.zeros((d, M, R), order="F")
     grad_t = np.zeros((1, M, R), order="F")

@@ -265,10 +265,34 @@ typedef struct { double g, gmu, gsig, gth, gmumu, gsigsig, gthth, gmuth, gsigth;
 static double normcdf(double z) { return erfc(-z * INVSQRT2) / 2; }
 static double normpdf(double z) { return exp(-(z * z) / 2) * INVSQRT2PI; }
 
-static ei_t ei_partials(double mu, double sig, double theta, double fmin, double sigma_tol) {
+/* POI (decision_rules.jl:101-115): g = Φ(z), zero for σ < σtol; closed-form partials with
+ * z_μ = z_θ = −1/σ, z_σ = −z/σ, φ' = −zφ.  LCB (:117-127): g = θσ − μ (no σtol branch). */
+static ei_t rule_partials(int rule, double mu, double sig, double theta, double fmin, double sigma_tol) {
   ei_t e;
   memset(&e, 0, sizeof e);
+  if (rule == RBO_RULE_LCB) {
+    e.g = theta * sig - mu;
+    e.gmu = -1.0;
+    e.gsig = theta;
+    e.gth = sig;
+    e.gsigth = 1.0;
+    return e;
+  }
   if (sig < sigma_tol) return e;
+  if (rule == RBO_RULE_POI) {
+    const double z = (fmin - mu - theta) / sig;
+    const double Phi = normcdf(z), phi = normpdf(z), s2 = sig * sig;
+    e.g = Phi;
+    e.gmu = -phi / sig;
+    e.gsig = -z * phi / sig;
+    e.gth = -phi / sig;
+    e.gmumu = -z * phi / s2;
+    e.gsigsig = z * phi * (2.0 - z * z) / s2;
+    e.gthth = -z * phi / s2;
+    e.gmuth = -z * phi / s2;
+    e.gsigth = phi * (1.0 - z * z) / s2;
+    return e;
+  }
   const double imp = fmin - mu - theta;
   const double z = imp / sig;
   const double Phi = normcdf(z), phi = normpdf(z);
@@ -366,10 +390,11 @@ typedef struct {
   double* y;   /* cap              */
   double* cs;  /* (h+2) × cap : cs[s+1] = coefficient vector of fantasy_index s */
   int nfant;   /* fantasies_observed */
+  int rule;    /* RBO_RULE_*: the trajectory's base decision rule */
 } fsur_t;
 
-static int fsur_alloc(fsur_t* fs, const rbo_surrogate* s, int h) {
-  fs->d = s->d; fs->N = s->N; fs->h = h; fs->cap = s->N + h + 1;
+static int fsur_alloc(fsur_t* fs, const rbo_surrogate* s, int h, int rule) {
+  fs->d = s->d; fs->N = s->N; fs->h = h; fs->cap = s->N + h + 1; fs->rule = rule;
   fs->k.kind = s->kernel; fs->k.ell = s->ell; fs->sn2 = s->sigma_n2;
   fs->X = (double*)calloc((size_t)fs->d * fs->cap, sizeof(double));
   fs->L = (double*)calloc((size_t)fs->cap * fs->cap, sizeof(double));
@@ -477,7 +502,7 @@ static void fsur_eval(const fsur_t* fs, const double* x, double theta, double si
   double fmin = fs->y[0];
   for (int j = 1; j < n; ++j) if (fs->y[j] < fmin) fmin = fs->y[j];
   sx->fmin = fmin;
-  sx->e = ei_partials(sx->mu, sx->sigma, theta, fmin, sigma_tol);
+  sx->e = rule_partials(fs->rule, sx->mu, sx->sigma, theta, fmin, sigma_tol);
   sx->alpha = sx->e.g;
   if (value_only) return;
   /* ∇μ, Dw, ∇σ */
@@ -604,7 +629,7 @@ static int grad_certified(const solve_ctx* cx, const sx_t* sx) {
   double cmu, csig;
   k_gcert(&cx->fs->k, &cmu, &csig);
   if (!(csig > 0.0)) return 0;
-  const double bound = fabs(gm) * cmu * cx->cabs + gs * csig / sx->sigma;
+  const double bound = fabs(gm) * cmu * cx->cabs + fabs(gs) * csig / sx->sigma;
   return bound <= 0.25 * cx->p->g_tol;
 }
 
@@ -804,7 +829,7 @@ static void perturb_grad(const fsur_t* fs, const sx_t* sx, int S, int q, const d
     dgsig[a] = (t1 - t2 - t3 - dsig * sx->gsig[a]) / sx->sigma;
   }
   /* δsx.dg_dμ / dg_dσ: first partials evaluated at (δμ, δσ)  (Q7, Q8) */
-  const ei_t de = ei_partials(dmu, dsig, theta, sx->fmin, sigma_tol);
+  const ei_t de = rule_partials(fs->rule, dmu, dsig, theta, sx->fmin, sigma_tol);
   for (int a = 0; a < d; ++a) {
     if (data)
       out[a] = sx->e.gmu * dgmu[a] + de.gmu * sx->gmu[a] + de.gsig * sx->gsig[a];
@@ -994,7 +1019,7 @@ int rbo_simulate_mc(const rbo_surrogate* s, const rbo_params* p, const double* x
   {
     fsur_t fs;
     scratch_t sc;
-    fsur_alloc(&fs, s, h);
+    fsur_alloc(&fs, s, h, p->rule);
     scratch_alloc(&sc, fs.cap, d);
 #pragma omp for schedule(dynamic, 1)
     for (int64_t tr = 0; tr < T; ++tr) {
@@ -1044,10 +1069,12 @@ int rbo_simulate_mc(const rbo_surrogate* s, const rbo_params* p, const double* x
 }
 
 /* base-surrogate evaluation for primitive parity (a6/a7/a8 at fantasy_index = -1) */
-int rbo_eval_base(const rbo_surrogate* s, double theta, double sigma_tol, int32_t P, const double* xs, double* out) {
+int rbo_eval_base(const rbo_surrogate* s, int32_t rule, double theta, double sigma_tol, int32_t P, const double* xs,
+                  double* out) {
   fsur_t fs;
   scratch_t sc;
-  if (fsur_alloc(&fs, s, 0)) return -2;
+  if (rule < 0 || rule > RBO_RULE_LCB) return -1;
+  if (fsur_alloc(&fs, s, 0, rule)) return -2;
   scratch_alloc(&sc, fs.cap, s->d);
   const int d = s->d, stride = 3 + 4 * d + d * d;
   sx_t sx;

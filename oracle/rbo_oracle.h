@@ -10,7 +10,7 @@
  *   radial_basis_surrogates.jl   Surrogate/FantasySurrogate eval, condition!, gp_draw,
  *                                Spatial/DataPerturbationSurrogate (dense δK, as written)
  *   radial_basis_functions.jl    Matern52/32/12, SquaredExponential and their ρ-derivatives
- *   decision_rules.jl:84-99      EI and its partials (closed forms of the ForwardDiff partials)
+ *   decision_rules.jl:84-127     EI, POI, LCB and their partials (closed forms of the ForwardDiff partials)
  *   observables.jl:83-124        StochasticObservable (gp_draw with gradient)
  *   utils.jl:4-74,145-153        Sobol uniforms, Box–Muller(log10), rnstream reshape, inner starts
  *   low_discrepancy.jl:7-28      kronecker_quasirand
@@ -68,7 +68,11 @@ typedef struct {
   int32_t samples_total;   /* global samples per restart keying the δx RNG (0 → M)    */
   int32_t with_gradient;
   int32_t nthreads;        /* OpenMP threads for the (restart, sample) loop      */
+  int32_t rule;            /* RBO_RULE_* base decision rule of the trajectory    */
 } rbo_params;
+
+/* base decision rules (decision_rules.jl:84-127) */
+enum { RBO_RULE_EI = 0, RBO_RULE_POI = 1, RBO_RULE_LCB = 2 };
 
 /* utils.jl:4-13: D×samples Sobol uniforms (zero point skipped), column-major. */
 int rbo_gen_uniform(int32_t samples, int32_t dim, double* out);
@@ -84,7 +88,7 @@ double rbo_dual_uniform(uint64_t seed, int64_t traj, int32_t j, int32_t k);
 /* Evaluate the base surrogate (fantasy_index = -1) at P points: per point writes
  * out[0]=μ, [1]=σ, [2]=α, [3..3+d)=∇μ, [3+d..3+2d)=∇σ, [3+2d..3+3d)=∇α,
  * [3+3d..3+3d+d²)=Hα (col-major), then d2α/dxdθ (d).  stride = 3+4d+d². */
-int rbo_eval_base(const rbo_surrogate* s, double theta, double sigma_tol, int32_t P,
+int rbo_eval_base(const rbo_surrogate* s, int32_t rule, double theta, double sigma_tol, int32_t P,
                   const double* xs, double* out);
 
 /* simulate_trajectory_mc (rollout.jl:279-340) for R restarts x0s (d×R).

@@ -243,7 +243,7 @@ static void fill_common(const mrbo_plan_t* P, KParams& kp) {
   memset(&kp, 0, sizeof kp);
   kp.d = P->d; kp.N = P->N; kp.Npad = P->Npad; kp.h = P->p.h; kp.M = P->p.M; kp.R = P->p.R;
   kp.nstarts = P->p.nstarts;
-  kp.kernel = P->kernel; kp.ell = P->ell; kp.cK = P->cK; kp.psi0 = P->psi0; kp.d2psi0 = P->d2psi0; kp.sn2 = P->sn2;
+  kp.kernel = P->kernel; kp.rule = P->p.rule; kp.ell = P->ell; kp.cK = P->cK; kp.psi0 = P->psi0; kp.d2psi0 = P->d2psi0; kp.sn2 = P->sn2;
   kp.gcert_mu = P->gcert_mu; kp.gcert_sig = P->gcert_sig;
   kp.fmin_base = P->fmin_base; kp.fmini = P->fmini; kp.theta = P->p.theta;
   kp.max_iters = P->p.max_iters; kp.max_ls = P->p.max_ls;
@@ -324,7 +324,8 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   if (N > 128) return fail(MRBO_ERR_UNSUPPORTED, "N=%d > 128 not supported (LDS-resident L0^-1)", N);
   if (p->h < 0 || p->h > FMAX - 1) return fail(MRBO_ERR_UNSUPPORTED, "h=%d outside [0,%d]", p->h, FMAX - 1);
   if (p->M < 1 || p->R < 1 || p->nstarts < 1 || !p->lbs || !p->ubs) return fail(MRBO_ERR_ARG, "bad params");
-  if (p->rule != MRBO_RULE_EI) return fail(MRBO_ERR_UNSUPPORTED, "only the EI base rule is compiled");
+  if (p->rule != MRBO_RULE_EI && p->rule != MRBO_RULE_POI && p->rule != MRBO_RULE_LCB)
+    return fail(MRBO_ERR_ARG, "unknown decision rule %d", (int)p->rule);
   if (s->kernel < 0 || s->kernel > 3) return fail(MRBO_ERR_ARG, "kernel id %d", s->kernel);
   const int ldL = s->ldL > 0 ? s->ldL : N;
 

@@ -33,6 +33,7 @@ enum { EV_VALUE = 0, EV_GRAD = 1, EV_DRAW = 2, EV_FULL = 3, EV_RICH = 4, EV_BACK
 struct KParams {
   int d, N, Npad, h, M, R, nstarts;
   int kernel;
+  int rule;             // mrbo_rule_t: EI, POI, LCB
   double ell, cK, psi0, d2psi0, sn2;
   double fmin_base, fmini, theta;
   // gradient certificate (newton_grad_certified): max_ρ |ψ'(ρ)| and √(ψ(0)·(−ψ''(0))), the
@@ -230,12 +231,26 @@ __device__ __forceinline__ void rad_eval(const Radial& k, double rho2, double& p
   }
 }
 
-// EI and its partials (decision_rules.jl:84-99); zero when σ < σtol.
+// The base decision rule g(μ, σ, θ) and the partials DecisionRule takes by ForwardDiff
+// (decision_rules.jl:23-34), in closed form.
+//   EI  (:84-99)   g = IΦ(z) + σφ(z), I = fmin − μ − θ, z = I/σ; zero when σ < σtol
+//   POI (:101-115) g = Φ(z); zero when σ < σtol
+//   LCB (:117-127) g = θσ − μ (no σtol branch)
 struct EIp {
   double g, gmu, gsig, gmumu, gsigsig, gmuth, gsigth;
 };
-__device__ __forceinline__ EIp ei_partials(double mu, double sig, double theta, double fmin, double sigma_tol) {
+enum { RULE_EI = 0, RULE_POI = 1, RULE_LCB = 2 };
+__device__ __forceinline__ EIp rule_partials(int rule, double mu, double sig, double theta, double fmin,
+                                             double sigma_tol) {
   EIp e;
+  if (rule == RULE_LCB) {
+    e.g = theta * sig - mu;
+    e.gmu = -1.0;
+    e.gsig = theta;
+    e.gmumu = e.gsigsig = e.gmuth = 0.0;
+    e.gsigth = 1.0;
+    return e;
+  }
   if (!(sig >= sigma_tol) && !(sig != sig)) {  // σ < σtol (NaN falls through, as in Julia)
     e.g = e.gmu = e.gsig = e.gmumu = e.gsigsig = e.gmuth = e.gsigth = 0.0;
     return e;
@@ -243,9 +258,20 @@ __device__ __forceinline__ EIp ei_partials(double mu, double sig, double theta, 
   const double imp = fmin - mu - theta;
   const double isig = 1.0 / sig;
   const double z = imp * isig;
-  const double Phi = 0.5 * xerfc(-z * 0.7071067811865476);
   const double phi = xexp(-0.5 * (z * z)) * 0.3989422804014327;
+  const double Phi = 0.5 * xerfc(-z * 0.7071067811865476);
   const double pis = phi * isig;
+  if (rule == RULE_POI) {
+    const double pis2 = pis * isig;
+    e.g = Phi;
+    e.gmu = -pis;
+    e.gsig = -z * pis;
+    e.gmumu = -z * pis2;
+    e.gsigsig = z * (2.0 - z * z) * pis2;
+    e.gmuth = -z * pis2;
+    e.gsigth = (1.0 - z * z) * pis2;
+    return e;
+  }
   e.g = imp * Phi + sig * phi;
   e.gmu = -Phi;
   e.gsig = phi;
@@ -256,12 +282,11 @@ __device__ __forceinline__ EIp ei_partials(double mu, double sig, double theta, 
   return e;
 }
 // first partials only, at (μ', σ') -- the perturbation "second-order" coefficients (Q7, Q8)
-__device__ __forceinline__ void ei_first(double mu, double sig, double theta, double fmin, double sigma_tol,
-                                         double& gmu, double& gsig) {
-  if (!(sig >= sigma_tol) && !(sig != sig)) { gmu = 0.0; gsig = 0.0; return; }
-  const double z = (fmin - mu - theta) / sig;
-  gmu = -(xerfc(-z * 0.7071067811865476) / 2.0);
-  gsig = xexp(-(z * z) / 2.0) * 0.3989422804014327;
+__device__ __forceinline__ void rule_first(int rule, double mu, double sig, double theta, double fmin, double sigma_tol,
+                                           double& gmu, double& gsig) {
+  const EIp e = rule_partials(rule, mu, sig, theta, fmin, sigma_tol);
+  gmu = e.gmu;
+  gsig = e.gsig;
 }
 
 // counter-based uniform (bit-identical to the host / oracle version)

@@ -518,7 +518,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   const double var = kp.psi0 - g00_v;
   const double sig = sqrt(var);
   const double fmin = U[Ly::U_FMIN + S + 1];
-  const EIp e = ei_partials(mu, sig, kp.theta, fmin, kp.sigma_tol);
+  const EIp e = rule_partials(kp.rule, mu, sig, kp.theta, fmin, kp.sigma_tol);
   if (lane == 0) {
     U[Ly::U_SC + SC_SIG] = sig;
     U[Ly::U_SC + SC_VAR] = var;
@@ -1015,7 +1015,7 @@ __device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const K
   const double* U = W.U;
   const double gm = U[Ly::U_SC + SC_GMU], gs = U[Ly::U_SC + SC_GSIG];
   const double cabs = U[Ly::U_SC + SC_CABS], sig = U[Ly::U_SC + SC_SIG];   // unconditional loads
-  const double bound = fabs(gm) * kp.gcert_mu * cabs + gs * kp.gcert_sig / sig;
+  const double bound = fabs(gm) * kp.gcert_mu * cabs + fabs(gs) * kp.gcert_sig / sig;
   return ((gm == 0.0) & (gs == 0.0)) | ((kp.gcert_sig > 0.0) & (bound <= 0.25 * kp.g_tol));
 }
 
@@ -1247,10 +1247,10 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   }
   const double var = kp.psi0 - g00;
   const double sig = sqrt(var);
-  const EIp e = ei_partials(mu, sig, kp.theta, U[Ly::U_FMIN + S + 1], kp.sigma_tol);
+  const EIp e = rule_partials(kp.rule, mu, sig, kp.theta, U[Ly::U_FMIN + S + 1], kp.sigma_tol);
   bool cert = (e.gmu == 0.0 && e.gsig == 0.0);
   if (!cert && kp.gcert_sig > 0.0)
-    cert = fabs(e.gmu) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + e.gsig * kp.gcert_sig / sig <= 0.25 * kp.g_tol;
+    cert = fabs(e.gmu) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + fabs(e.gsig) * kp.gcert_sig / sig <= 0.25 * kp.g_tol;
   f_lane = -e.g;
   // the iteration stops at the start point: certified, f NaN, or no iterations allowed
   const bool stop = cert || (f_lane != f_lane) || kp.max_iters <= 0;
@@ -1469,7 +1469,7 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
   const double isig = 1.0 / sig;
   const double dsig = wq * (udw - dkx) * isig;
   double dgm, dgs;
-  ei_first(dmu, dsig, kp.theta, U[Ly::U_SC + SC_FMIN], kp.sigma_tol, dgm, dgs);
+  rule_first(kp.rule, dmu, dsig, kp.theta, U[Ly::U_SC + SC_FMIN], kp.sigma_tol, dgm, dgs);
   double contrib = 0.0;
 #pragma unroll
   for (int a = 0; a < D; ++a) {

@@ -2,13 +2,13 @@
 
 A DecisionRule names the base acquisition g(μ, σ, θ, sx) whose value, gradient and Hessian
 the device kernel evaluates in closed form (the reference takes the 8 partials by
-ForwardDiff, decision_rules.jl:23-34).  EI is the rule compiled into libmrbo.so; POI, LCB
-and Random are declared for API parity and rejected by the rollout plan.
+ForwardDiff, decision_rules.jl:23-34).  EI, POI and LCB are compiled into libmrbo.so
+(mrbo_rule_t); Random (g ≡ 0) is declared for API parity and rejected by the rollout plan.
 """
 import numpy as np
 from scipy.special import erfc
 
-RULES = {"EI": 0}
+RULES = {"EI": 0, "POI": 1, "LCB": 2}   # mrbo_rule_t (include/mrbo.h)
 
 
 class DecisionRule:
@@ -19,15 +19,25 @@ class DecisionRule:
     def __repr__(self):
         return f"DecisionRule{{{self.name}}}"
 
+    @property
+    def rule_id(self):
+        """mrbo_rule_t of this rule (KeyError for rules the kernel does not compile)."""
+        return RULES[self.name]
+
     # Host-side closed-form value (for tests and docs; the rollout path never calls this).
     def __call__(self, μ, σ, θ, fmini):
-        if self.name != "EI":
-            raise NotImplementedError(self.name)
+        if self.name == "LCB":
+            return θ[0] * σ - μ
+        if self.name == "Random":
+            return 0.0
         if σ < self.σtol:
             return 0.0
         imp = fmini - μ - θ[0]
         z = imp / σ
-        return imp * (erfc(-z / np.sqrt(2.0)) / 2.0) + σ * np.exp(-(z * z) / 2.0) / np.sqrt(2.0 * np.pi)
+        Φ = erfc(-z / np.sqrt(2.0)) / 2.0
+        if self.name == "POI":
+            return Φ
+        return imp * Φ + σ * np.exp(-(z * z) / 2.0) / np.sqrt(2.0 * np.pi)
 
 
 def get_name(dr):
@@ -40,12 +50,12 @@ def EI(σtol=1e-8):
 
 
 def POI(σtol=1e-8):
-    """decision_rules.jl:101-115 (declared; not compiled into the rollout kernel)"""
+    """decision_rules.jl:101-115"""
     return DecisionRule("POI", σtol)
 
 
 def LCB():
-    """decision_rules.jl:117-127 (declared; not compiled into the rollout kernel)"""
+    """decision_rules.jl:117-127"""
     return DecisionRule("LCB")
 
 

@@ -55,7 +55,8 @@ class RolloutPlan:
         sd = _lib.SurrogateDesc(self.d, self.N, int(kernel), float(lengthscale), float(sigma_n2), float(fmini),
                                 self._X.ctypes.data_as(dp), self._L.ctypes.data_as(dp), self.N,
                                 self._c.ctypes.data_as(dp), self._y.ctypes.data_as(dp))
-        pd = _lib.ParamsDesc(self.h, self.M, self.R, self.nstarts, 0, self.theta, self._lbs.ctypes.data_as(dp),
+        pd = _lib.ParamsDesc(self.h, self.M, self.R, self.nstarts, int(o.get("rule", 0)), self.theta,
+                             self._lbs.ctypes.data_as(dp),
                              self._ubs.ctypes.data_as(dp), int(o["max_iters"]), int(o["max_ls"]), float(o["x_tol"]),
                              float(o["f_tol"]), float(o["g_tol"]), float(o["htol"]), float(o["sigma_tol"]),
                              int(o["seed"]), int(o.get("sample_offset", 0)), int(o.get("samples_total", 0)))

@@ -16,6 +16,10 @@ _PLANS = {}
 
 
 def _plan_for(s, h, M, R, nstarts, lbs, ubs, theta, device, opts):
+    g = s.get_decision_rule()
+    opts = dict(opts)
+    opts.setdefault("rule", g.rule_id)       # the surrogate's base decision rule (Q12: T.θ)
+    opts.setdefault("sigma_tol", g.σtol)
     key = (id(s), s.version, h, M, R, nstarts, tuple(np.asarray(lbs).ravel()), tuple(np.asarray(ubs).ravel()),
            float(theta), device, tuple(sorted(opts.items())))
     p = _PLANS.get(key)

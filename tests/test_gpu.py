@@ -18,13 +18,13 @@ from conftest import GOLDEN_CASES, load_golden
 pytestmark = pytest.mark.gpu
 
 
-def _plan(g, M=None, R=None, h=None, nstarts=None, kernel=0, **opts):
+def _plan(g, M=None, R=None, h=None, nstarts=None, kernel=0, theta=0.0, **opts):
     from mrbo.engine import RolloutPlan
     M = M or g["rnstream"].shape[0]
     R = R or g["x0s"].shape[1]
     h = int(g["h"]) if h is None else h
     return RolloutPlan(g["X"], g["L"], g["c"], g["y"], kernel, 1.0, 1e-6, float(g["fmini"]), h, M, R,
-                       nstarts or g["xstarts"].shape[1], g["lbs"], g["ubs"], 0.0, **opts)
+                       nstarts or g["xstarts"].shape[1], g["lbs"], g["ubs"], theta, **opts)
 
 
 def _run(plan, g, dual=None, replay=None, want_policy=True, with_gradient=True, rn=None, x0s=None):
@@ -116,6 +116,34 @@ def test_end_to_end_vs_oracle(gpu, oracle, name, M, R):
                             replay_x=rp, nthreads=8)
     np.testing.assert_allclose(r["values"], o2["values"], rtol=1e-8, atol=1e-11)
     _assert_grads_close(r["grad_x"], o2["grad_x"])
+
+
+@pytest.mark.parametrize("rule,rid,theta", [("POI", 1, 0.0), ("POI", 1, 0.05), ("LCB", 2, 2.0)])
+def test_other_rules_vs_oracle(gpu, oracle, rule, rid, theta):
+    """POI / LCB base rules (decision_rules.jl:101-127): primitives, then full rollouts with the
+    inner Newton solves on both sides, and a replay of the GPU's policy points."""
+    g = _problem_arrays("C2", 32, 4)
+    p = _plan(g, theta=theta, rule=rid)
+    osur = _osur(oracle, g)
+    pts = np.asfortranarray(g["xstarts"][:, :8] * 0.9 + 0.05)
+    np.testing.assert_allclose(p.eval_base(pts), oracle.eval_base(osur, pts, theta=theta, rule=rule),
+                               rtol=1e-9, atol=1e-12)
+    r = _run(p, g)
+    o = oracle.simulate_mc(osur, g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
+                           theta=theta, rule=rule, nthreads=8)
+    assert (r["status"] == o["status"]).all()
+    ok = r["status"] == 0
+    same = ok & np.all(np.abs(r["policy_x"] - o["policy_x"]) <= 1e-6 * (1 + np.abs(o["policy_x"])), axis=(0, 1))
+    assert same.sum() >= 0.97 * ok.sum(), (same.sum(), ok.sum())
+    np.testing.assert_allclose(r["values"][same], o["values"][same], rtol=1e-8, atol=1e-11)
+    _assert_grads_close(r["grad_x"][:, same], o["grad_x"][:, same], rtol=1e-5)
+    np.testing.assert_array_equal(r["evals"][:3][:, same], o["evals"][:, same])
+    rp = np.asfortranarray(r["policy_x"][:, 1:])
+    o2 = oracle.simulate_mc(osur, g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
+                            theta=theta, rule=rule, replay_x=rp, nthreads=8)
+    np.testing.assert_allclose(r["values"][ok], o2["values"][ok], rtol=1e-8, atol=1e-11)
+    _assert_grads_close(r["grad_x"][:, ok], o2["grad_x"][:, ok], rtol=1e-5)
+    _assert_grads_close(r["grad_theta"][:, ok], o2["grad_theta"][:, ok], rtol=1e-5)
 
 
 @pytest.mark.parametrize("kernel,kid", [("matern32", 1), ("matern12", 2), ("se", 3)])

@@ -111,6 +111,31 @@ def test_eval_base_derivatives_fd(oracle):
     _ = erfc
 
 
+@pytest.mark.parametrize("rule,theta", [("POI", 0.05), ("LCB", 2.0), ("EI", 0.1)])
+def test_rule_partials_fd(oracle, rule, theta):
+    """POI / LCB / EI (decision_rules.jl:84-127): ∇α, Hα (+ the omitted Q11 μσ cross term) and
+    d²α/dxdθ against central differences of the oracle's own values."""
+    g = load_golden("c2near")
+    s = _osur(oracle, g)
+    d = g["X"].shape[0]
+    x = g["x0s"][:, 0] + 0.3
+    col = lambda xx, th=theta: oracle.eval_base(s, xx.reshape(-1, 1), theta=th, rule=rule)[:, 0]
+    o = col(x)
+    mu, sig = o[0], o[1]
+    gmu, gsig, galpha = o[3:3 + d], o[3 + d:3 + 2 * d], o[3 + 2 * d:3 + 3 * d]
+    H = o[3 + 3 * d:3 + 3 * d + d * d].reshape(d, d, order="F")
+    mixed = o[3 + 3 * d + d * d:]
+    np.testing.assert_allclose(galpha, _fd(lambda xx: col(xx)[2], x), rtol=1e-6, atol=1e-10)
+    z = (np.min(g["y"]) - mu - theta) / sig
+    phi = np.exp(-z * z / 2) / np.sqrt(2 * np.pi)
+    gmusig = {"EI": z * phi / sig, "POI": phi * (1 - z * z) / sig ** 2, "LCB": 0.0}[rule]
+    Hfd = np.column_stack([_fd(lambda xx: col(xx)[3 + 2 * d + a], x) for a in range(d)])
+    np.testing.assert_allclose(H + gmusig * (np.outer(gmu, gsig) + np.outer(gsig, gmu)), Hfd, rtol=1e-5, atol=1e-8)
+    th_fd = np.array([(col(x, theta + 1e-6)[3 + 2 * d + a] - col(x, theta - 1e-6)[3 + 2 * d + a]) / 2e-6
+                      for a in range(d)])
+    np.testing.assert_allclose(mixed, th_fd, rtol=1e-5, atol=1e-9)
+
+
 def test_replay_mode_reproduces_own_policy(oracle):
     """Replaying the oracle's own policy points reproduces the normal run exactly."""
     g = load_golden("c2")
