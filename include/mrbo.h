@@ -142,6 +142,19 @@ int mrbo_simulate_mc(mrbo_plan_t* plan, const double* x0s, const double* rnstrea
 
 #define MRBO_NCOUNTERS 5
 
+/* simulate_trajectory_ghq(T, tp; inner_solve_xstarts, resolutions, nodes, weights, indices, …)
+ * rollout.jl:409-467 — the Gauss–Hermite estimator.  Sample m (of M = length(indices)) uses the
+ * node vector nodes[m, 0..h] = nodes[indices[m]] and weights[m, 0..h] = weights[indices[m]]
+ * (M×(h+1), column-major; generate_indices utils.jl:217-221 builds the tensor product): step k
+ * observes y = μ + √2·σ·t_k with recorded gradient weights[k]·(∇μ + √2·∇σ·t_k)
+ * (GaussHermiteObservable observables.jl:32-81, get_gradient :157) and the resolution is
+ * weights[best]·max(fmini − y_best, 0)/√π.  All other arguments and outputs as mrbo_simulate_mc
+ * (the plan's M is the number of node vectors).                                              */
+int mrbo_simulate_ghq(mrbo_plan_t* plan, const double* x0s, const double* nodes, const double* weights,
+                      const double* xstarts, const double* dual_y_dx, const double* replay_x, double* values,
+                      double* grad_x, double* grad_theta, int32_t* status, double* policy_x, double* obs,
+                      int64_t* evals, uint32_t flags, void* stream);
+
 /* ExpectedTrajectoryOutput per restart: eto R×W (row-major per restart, W = 2+2d+2):
  * [μxθ, σ_μxθ, ∇μx(d), σ_∇μx(d), ∇μθ, σ_∇μθ]; std uses n-1 (Q14).                     */
 int mrbo_eto_reduce(mrbo_plan_t* plan, const double* values, const double* grad_x, const double* grad_theta,

@@ -60,6 +60,8 @@ def lib():
                                     ctypes.c_int32, _dp, _dp]
         L.rbo_simulate_mc.argtypes = [ctypes.POINTER(Surrogate), ctypes.POINTER(Params), _dp, _dp, _dp, _dp, _dp,
                                       _dp, _dp, _dp, _ip, _dp, _dp, _dp, _lp]
+        L.rbo_simulate_ghq.argtypes = [ctypes.POINTER(Surrogate), ctypes.POINTER(Params), _dp, _dp, _dp, _dp, _dp,
+                                       _dp, _dp, _dp, _dp, _ip, _dp, _dp, _dp, _lp]
         _lib = L
     return _lib
 
@@ -132,13 +134,21 @@ def eval_base(osur, xs, theta=0.0, sigma_tol=1e-8, rule="EI"):
 def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=None, replay_x=None,
                 max_iters=50, max_ls=20, x_tol=1e-3, f_tol=1e-3, g_tol=1e-8, htol=1e-4, sigma_tol=1e-8,
                 seed=1906, with_gradient=True, nthreads=0, want_policy=True, sample_offset=0,
-                samples_total=0, rule="EI"):
-    """Run the oracle's simulate_trajectory_mc for every restart column of x0s (d×R)."""
-    x0s, rnstream, xstarts = _f64(x0s), _f64(rnstream), _f64(xstarts)
+                samples_total=0, rule="EI", ghq=None):
+    """Run the oracle's simulate_trajectory_mc for every restart column of x0s (d×R).
+    ghq=(nodes, weights), each M×(h+1): the Gauss–Hermite estimator (rbo_simulate_ghq) instead
+    of the rnstream draws (rnstream is then only used for its M)."""
+    x0s, xstarts = _f64(x0s), _f64(xstarts)
     lbs, ubs = _f64(lbs), _f64(ubs)
     d, R = x0s.shape
-    M = rnstream.shape[0]
-    assert rnstream.shape == (M, d + 1, h + 1), rnstream.shape
+    if ghq is not None:
+        nodes, weights = _f64(ghq[0]), _f64(ghq[1])
+        M = nodes.shape[0]
+        assert nodes.shape == (M, h + 1) and weights.shape == (M, h + 1), (nodes.shape, weights.shape)
+    else:
+        rnstream = _f64(rnstream)
+        M = rnstream.shape[0]
+        assert rnstream.shape == (M, d + 1, h + 1), rnstream.shape
     prm = Params(h, M, R, xstarts.shape[1], theta, _p(lbs), _p(ubs), max_iters, max_ls, x_tol, f_tol, g_tol,
                  htol, sigma_tol, seed, sample_offset, samples_total, 1 if with_gradient else 0, nthreads,
                  RULES[rule])
@@ -152,10 +162,16 @@ def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=
     evals = np.zeros((3, M, R), dtype=np.int64, order="F")   # [grad, value, hess] per trajectory
     dy = None if dual_y_dx is None else _f64(dual_y_dx)
     rp = None if replay_x is None else _f64(replay_x)
-    rc = lib().rbo_simulate_mc(ctypes.byref(osur.s), ctypes.byref(prm), _p(x0s), _p(rnstream), _p(xstarts),
-                               _p(dy), _p(rp), _p(values), _p(grad_x), _p(grad_t),
-                               status.ctypes.data_as(_ip), _p(policy), _p(obs), _p(eto),
-                               evals.ctypes.data_as(_lp))
+    if ghq is not None:
+        rc = lib().rbo_simulate_ghq(ctypes.byref(osur.s), ctypes.byref(prm), _p(x0s), _p(nodes), _p(weights),
+                                    _p(xstarts), _p(dy), _p(rp), _p(values), _p(grad_x), _p(grad_t),
+                                    status.ctypes.data_as(_ip), _p(policy), _p(obs), _p(eto),
+                                    evals.ctypes.data_as(_lp))
+    else:
+        rc = lib().rbo_simulate_mc(ctypes.byref(osur.s), ctypes.byref(prm), _p(x0s), _p(rnstream), _p(xstarts),
+                                   _p(dy), _p(rp), _p(values), _p(grad_x), _p(grad_t),
+                                   status.ctypes.data_as(_ip), _p(policy), _p(obs), _p(eto),
+                                   evals.ctypes.data_as(_lp))
     assert rc == 0, rc
     return dict(values=values, grad_x=grad_x, grad_theta=grad_t, status=status, policy_x=policy, obs=obs,
                 eto=eto, evals=evals)

@@ -20,6 +20,8 @@
 
 #define JL_PI 3.141592653589793           /* Julia π as Float64                       */
 #define INVSQRT2 0.7071067811865476        /* StatsFuns.invsqrt2                       */
+#define SQRT2 1.4142135623730951
+#define SQRTPI 1.7724538509055159
 #define INVSQRT2PI 0.3989422804014327      /* StatsFuns.invsqrt2π                      */
 
 /* ------------------------------------------------------------------------------------
@@ -848,6 +850,8 @@ typedef struct {
   const double* xstarts;
   const double* dual_y_dx;
   const double* replay_x;
+  const double* ghq_nodes; /* M×(h+1) Gauss–Hermite nodes per sample, or NULL (Monte Carlo) */
+  const double* ghq_w;     /* M×(h+1) their weights                                        */
 } traj_in;
 
 static int run_trajectory(const traj_in* in, int r, int m, const double* x0, fsur_t* fs, scratch_t* sc,
@@ -876,8 +880,19 @@ static int run_trajectory(const traj_in* in, int r, int m, const double* x0, fsu
       xk = xnext;
     }
     if (pol) memcpy(pol + (int64_t)d * (k + (int64_t)(h + 1) * (m + (int64_t)M * r)), xk, sizeof(double) * d);
-    for (int a = 0; a < D1; ++a) z[a] = in->rnstream[(int64_t)m + (int64_t)M * a + (int64_t)M * D1 * k];
-    st |= fsur_draw(fs, xk, p->theta, p->sigma_tol, k - 1, z, &obs[k], grads + d * k, &sx, sc);
+    if (in->ghq_w) {
+      /* GaussHermiteObservable (observables.jl:58-66): y = μ + √2 σ t_k, ∇y = ∇μ + √2 ∇σ t_k on
+       * fantasy_index k-1; the recorded gradient is get_gradient's weights[k]·∇y (the later
+       * override at observables.jl:157 is the one Julia dispatches to). */
+      const double tk = in->ghq_nodes[(int64_t)m + (int64_t)M * k], wk = in->ghq_w[(int64_t)m + (int64_t)M * k];
+      fsur_eval(fs, xk, p->theta, p->sigma_tol, k - 1, 0, &sx, sc);
+      st |= sx.status;
+      obs[k] = sx.mu + SQRT2 * sx.sigma * tk;
+      for (int a = 0; a < d; ++a) grads[a + d * k] = wk * (sx.gmu[a] + SQRT2 * sx.gsig[a] * tk);
+    } else {
+      for (int a = 0; a < D1; ++a) z[a] = in->rnstream[(int64_t)m + (int64_t)M * a + (int64_t)M * D1 * k];
+      st |= fsur_draw(fs, xk, p->theta, p->sigma_tol, k - 1, z, &obs[k], grads + d * k, &sx, sc);
+    }
     if (st) break;
     st |= fsur_condition(fs, xk, obs[k], sc->tmp);
     if (st) break;
@@ -897,6 +912,8 @@ static int run_trajectory(const traj_in* in, int r, int m, const double* x0, fsu
   int t = 0;
   for (int k = 1; k <= h; ++k) if (obs[k] < bo) { bo = obs[k]; t = k; }
   *value = fmax(in->s->fmini - bo, 0.0);
+  /* resolve(gho; fmini) observables.jl:66-72: weight of the best step, / √π */
+  if (in->ghq_w) *value *= in->ghq_w[(int64_t)m + (int64_t)M * t] / SQRTPI;
   for (int a = 0; a < d; ++a) gx[a] = 0;
   *gth = 0;
   if (!p->with_gradient) return 0;
@@ -1004,14 +1021,14 @@ static int run_trajectory(const traj_in* in, int r, int m, const double* x0, fsu
   return st;
 }
 
-int rbo_simulate_mc(const rbo_surrogate* s, const rbo_params* p, const double* x0s, const double* rnstream,
-                    const double* xstarts, const double* dual_y_dx, const double* replay_x, double* values,
-                    double* grad_x, double* grad_theta, int32_t* status, double* policy_x, double* obs,
-                    double* eto, int64_t* evals) {
+static int simulate_impl(const rbo_surrogate* s, const rbo_params* p, const double* x0s, const double* rnstream,
+                         const double* ghq_nodes, const double* ghq_w, const double* xstarts, const double* dual_y_dx,
+                         const double* replay_x, double* values, double* grad_x, double* grad_theta, int32_t* status,
+                         double* policy_x, double* obs, double* eto, int64_t* evals) {
   if (!s || !p || s->d < 1 || s->d > 16 || p->h < 0 || p->h > 60 || p->M < 1 || p->R < 1) return -1;
   const int d = s->d, M = p->M, R = p->R, h = p->h;
   const int64_t T = (int64_t)M * R;
-  traj_in in = {s, p, rnstream, xstarts, dual_y_dx, replay_x};
+  traj_in in = {s, p, rnstream, xstarts, dual_y_dx, replay_x, ghq_nodes, ghq_w};
 #ifdef _OPENMP
   if (p->nthreads > 0) omp_set_num_threads(p->nthreads);
 #endif
@@ -1069,6 +1086,24 @@ int rbo_simulate_mc(const rbo_surrogate* s, const rbo_params* p, const double* x
 }
 
 /* base-surrogate evaluation for primitive parity (a6/a7/a8 at fantasy_index = -1) */
+int rbo_simulate_mc(const rbo_surrogate* s, const rbo_params* p, const double* x0s, const double* rnstream,
+                    const double* xstarts, const double* dual_y_dx, const double* replay_x, double* values,
+                    double* grad_x, double* grad_theta, int32_t* status, double* policy_x, double* obs,
+                    double* eto, int64_t* evals) {
+  if (!rnstream) return -1;
+  return simulate_impl(s, p, x0s, rnstream, NULL, NULL, xstarts, dual_y_dx, replay_x, values, grad_x, grad_theta,
+                       status, policy_x, obs, eto, evals);
+}
+
+int rbo_simulate_ghq(const rbo_surrogate* s, const rbo_params* p, const double* x0s, const double* nodes,
+                     const double* weights, const double* xstarts, const double* dual_y_dx, const double* replay_x,
+                     double* values, double* grad_x, double* grad_theta, int32_t* status, double* policy_x,
+                     double* obs, double* eto, int64_t* evals) {
+  if (!nodes || !weights) return -1;
+  return simulate_impl(s, p, x0s, NULL, nodes, weights, xstarts, dual_y_dx, replay_x, values, grad_x, grad_theta,
+                       status, policy_x, obs, eto, evals);
+}
+
 int rbo_eval_base(const rbo_surrogate* s, int32_t rule, double theta, double sigma_tol, int32_t P, const double* xs,
                   double* out) {
   fsur_t fs;

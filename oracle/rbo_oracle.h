@@ -106,6 +106,16 @@ int rbo_simulate_mc(const rbo_surrogate* s, const rbo_params* p, const double* x
                     double* values, double* grad_x, double* grad_theta, int32_t* status,
                     double* policy_x, double* obs, double* eto, int64_t* evals);
 
+/* simulate_trajectory_ghq (rollout.jl:409-467): the Gauss–Hermite estimator.  Sample m uses the
+ * node vector nodes[m, 0..h] and weights[m, 0..h] (M×(h+1), column-major), i.e. the caller's
+ * nodes[indices[m]] / weights[indices[m]] (generate_indices, utils.jl:217-221); observations
+ * y = μ + √2σ t (GaussHermiteObservable, observables.jl:32-81, 157); values weighted by
+ * weights[best]/√π.  Other arguments and outputs as rbo_simulate_mc. */
+int rbo_simulate_ghq(const rbo_surrogate* s, const rbo_params* p, const double* x0s, const double* nodes,
+                     const double* weights, const double* xstarts, const double* dual_y_dx, const double* replay_x,
+                     double* values, double* grad_x, double* grad_theta, int32_t* status, double* policy_x,
+                     double* obs, double* eto, int64_t* evals);
+
 /* Test functions (testfns.jl) used to make base data y. id: 0 GramacyLee, 1 BraninHoo,
  * 2 Hartmann6D, 3 Ackley(d), 4 Rosenbrock, 5 Rastrigin(d). */
 double rbo_testfn(int32_t id, int32_t d, const double* x);

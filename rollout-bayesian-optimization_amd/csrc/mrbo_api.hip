@@ -455,11 +455,15 @@ int mrbo_plan_destroy(mrbo_plan_t* P) {
   return MRBO_OK;
 }
 
-int mrbo_simulate_mc(mrbo_plan_t* P, const double* x0s, const double* rnstream, const double* xstarts,
-                     const double* dual_y_dx, const double* replay_x, double* values, double* grad_x,
-                     double* grad_theta, int32_t* status, double* policy_x, double* obs, int64_t* evals,
-                     uint32_t flags, void* stream) {
-  if (!P || !x0s || !rnstream || !xstarts || !values || !status) return fail(MRBO_ERR_ARG, "null argument");
+// one launch of the rollout kernel: Monte-Carlo draws from rnstream, or the Gauss–Hermite
+// observable from (ghq_nodes, ghq_w) when those are given
+static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnstream, const double* ghq_nodes,
+                           const double* ghq_w, const double* xstarts, const double* dual_y_dx,
+                           const double* replay_x, double* values, double* grad_x, double* grad_theta,
+                           int32_t* status, double* policy_x, double* obs, int64_t* evals, uint32_t flags,
+                           void* stream) {
+  if (!P || !x0s || !(rnstream || (ghq_nodes && ghq_w)) || !xstarts || !values || !status)
+    return fail(MRBO_ERR_ARG, "null argument");
   const bool with_grad = !(flags & MRBO_FLAG_NO_GRADIENT);
   if (with_grad && (!grad_x || !grad_theta)) return fail(MRBO_ERR_ARG, "gradient containers required");
   hipStream_t st = (hipStream_t)stream;
@@ -477,6 +481,7 @@ int mrbo_simulate_mc(mrbo_plan_t* P, const double* x0s, const double* rnstream, 
   int64_t* devals = evals;
   if (host) {
     if (sg.in(x0s, (size_t)d * R, &kp.x0s) || sg.in(rnstream, (size_t)M * (d + 1) * (h + 1), &kp.rn) ||
+        sg.in(ghq_nodes, (size_t)M * (h + 1), &kp.ghq_nodes) || sg.in(ghq_w, (size_t)M * (h + 1), &kp.ghq_w) ||
         sg.in(xstarts, (size_t)d * P->p.nstarts, &kp.xstarts) ||
         sg.in(dual_y_dx, (size_t)d * std::max(h, 1) * T, &kp.dual_y) ||
         sg.in(replay_x, (size_t)d * std::max(h, 1) * T, &kp.replay) || sg.out(T, values, &dvalues) ||
@@ -486,6 +491,7 @@ int mrbo_simulate_mc(mrbo_plan_t* P, const double* x0s, const double* rnstream, 
       return fail(MRBO_ERR_NOMEM, "staging allocation failed");
   } else {
     kp.x0s = x0s; kp.rn = rnstream; kp.xstarts = xstarts; kp.dual_y = dual_y_dx; kp.replay = replay_x;
+    kp.ghq_nodes = ghq_nodes; kp.ghq_w = ghq_w;
   }
   kp.values = dvalues; kp.grad_x = with_grad ? dgx : nullptr; kp.grad_theta = with_grad ? dgt : nullptr;
   kp.status = (int*)dstatus; kp.policy = dpol; kp.obs = dobs; kp.evals = (long long*)devals;
@@ -535,6 +541,24 @@ int mrbo_simulate_mc(mrbo_plan_t* P, const double* x0s, const double* rnstream, 
     if (evals) HIP_TRY(hipMemcpy(evals, devals, sizeof(int64_t) * NCOUNT * T, hipMemcpyDeviceToHost));
   }
   return MRBO_OK;
+}
+
+int mrbo_simulate_mc(mrbo_plan_t* P, const double* x0s, const double* rnstream, const double* xstarts,
+                     const double* dual_y_dx, const double* replay_x, double* values, double* grad_x,
+                     double* grad_theta, int32_t* status, double* policy_x, double* obs, int64_t* evals,
+                     uint32_t flags, void* stream) {
+  if (!rnstream) return fail(MRBO_ERR_ARG, "null rnstream");
+  return simulate_common(P, x0s, rnstream, nullptr, nullptr, xstarts, dual_y_dx, replay_x, values, grad_x,
+                         grad_theta, status, policy_x, obs, evals, flags, stream);
+}
+
+int mrbo_simulate_ghq(mrbo_plan_t* P, const double* x0s, const double* nodes, const double* weights,
+                      const double* xstarts, const double* dual_y_dx, const double* replay_x, double* values,
+                      double* grad_x, double* grad_theta, int32_t* status, double* policy_x, double* obs,
+                      int64_t* evals, uint32_t flags, void* stream) {
+  if (!nodes || !weights) return fail(MRBO_ERR_ARG, "null nodes / weights");
+  return simulate_common(P, x0s, nullptr, nodes, weights, xstarts, dual_y_dx, replay_x, values, grad_x, grad_theta,
+                         status, policy_x, obs, evals, flags, stream);
 }
 
 int mrbo_eto_reduce(mrbo_plan_t* P, const double* values, const double* grad_x, const double* grad_theta,

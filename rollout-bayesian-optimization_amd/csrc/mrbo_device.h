@@ -66,6 +66,8 @@ struct KParams {
   double* work;         // per wave-slot global scratch
   long long work_stride;
   double* ytab;         // kp.batch: per-workgroup slices [blockIdx][nstarts][NR] of Y0(x_start)
+  const double* ghq_nodes;  // Gauss–Hermite estimator: M×(h+1) nodes and weights per sample (else null)
+  const double* ghq_w;
   int* queue;           // work-queue head (zeroed before every launch)
   long long T;          // trajectories (or points for eval_base)
   const double* pts;    // eval_base: d×P

@@ -1606,11 +1606,22 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
     evaluate<D, RPL>(W, kp, S, EV_DRAW, lr);
     if (U[Ly::U_SC + SC_VAR] < 0.0) { st |= 1; break; }
     if (k == 0 && lane < D) U[Ly::U_GMU0 + lane] = U[Ly::U_GMU + lane];
-    double z[D1], yv, gy[D];
+    double yv, gy[D];
+    if (kp.ghq_w) {
+      // GaussHermiteObservable (observables.jl:58-66): y = μ + √2σ t_k, ∇y = ∇μ + √2∇σ t_k; the
+      // gradient recorded for the adjoint is get_gradient's weights[k]·∇y (observables.jl:157)
+      const long long ik = (long long)m + (long long)M * k;
+      const double tk = kp.ghq_nodes[ik], wk = kp.ghq_w[ik];
+      yv = U[Ly::U_SC + SC_MU] + 1.4142135623730951 * U[Ly::U_SC + SC_SIG] * tk;
 #pragma unroll
-    for (int a = 0; a < D1; ++a) z[a] = kp.rn[(long long)m + (long long)M * a + (long long)M * D1 * k];
-    st |= draw<D, RPL>(W, kp, z, yv, gy);
-    if (st) break;
+      for (int a = 0; a < D; ++a) gy[a] = wk * (U[Ly::U_GMU + a] + 1.4142135623730951 * U[Ly::U_GSIG + a] * tk);
+    } else {
+      double z[D1];
+#pragma unroll
+      for (int a = 0; a < D1; ++a) z[a] = kp.rn[(long long)m + (long long)M * a + (long long)M * D1 * k];
+      st |= draw<D, RPL>(W, kp, z, yv, gy);
+      if (st) break;
+    }
     wave_sync();
     st |= condition<D, RPL>(W, kp, S, yv, gy, lr);
     STAMP(W, 10);
@@ -1634,7 +1645,9 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
   double bo = U[Ly::U_YF];
   int t = 0;
   for (int k = 1; k <= h; ++k) { const double yk = U[Ly::U_YF + k]; if (yk < bo) { bo = yk; t = k; } }
-  const double value = fmax(kp.fmini - bo, 0.0);
+  double value = fmax(kp.fmini - bo, 0.0);
+  // resolve(gho; fmini) observables.jl:66-72: the best step's weight / √π
+  if (kp.ghq_w) value *= kp.ghq_w[(long long)m + (long long)M * t] * 0.5641895835477563;
   double gth = 0.0;
   bool grad_zero = true;
 #ifndef MRBO_EXP_NO_ADJOINT

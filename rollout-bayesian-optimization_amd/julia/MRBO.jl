@@ -75,8 +75,11 @@ function check(rc)
     error("libmrbo error $rc: $msg")
 end
 
+rule_id(g) = get_name(g) == "EI" ? 0 : get_name(g) == "POI" ? 1 : get_name(g) == "LCB" ? 2 :
+             error("decision rule not compiled into libmrbo")
+
 function MrboPlan(s::Surrogate, tp::TrajectoryParameters, θ::Vector{Float64}, nstarts::Int;
-                  device::Int = 0, max_iters = 50, max_ls = 20, seed = 1906)
+                  device::Int = 0, max_iters = 50, max_ls = 20, seed = 1906, M::Int = tp.mc_iters)
     N = get_observed(s)
     X = Matrix(get_active_covariates(s))
     L = Matrix(get_active_cholesky(s))
@@ -87,13 +90,13 @@ function MrboPlan(s::Surrogate, tp::TrajectoryParameters, θ::Vector{Float64}, n
     GC.@preserve X L c y lbs ubs begin
         sd = MrboSurrogateC(size(X, 1), N, kernel_id(get_kernel(s)), get_kernel(s).θ[1], s.σn2, fmini,
                             pointer(X), pointer(L), N, pointer(c), pointer(y))
-        pd = MrboParamsC(tp.horizon, tp.mc_iters, 1, nstarts, 0, θ[1], pointer(lbs), pointer(ubs),
+        pd = MrboParamsC(tp.horizon, M, 1, nstarts, rule_id(get_decision_rule(s)), θ[1], pointer(lbs), pointer(ubs),
                          max_iters, max_ls, 1e-3, 1e-3, 1e-8, 1e-4, 1e-8, seed, 0, 0)
         h = Ref{Ptr{Cvoid}}(C_NULL)
         check(ccall((:mrbo_plan_create, libmrbo), Cint,
                     (Ref{MrboSurrogateC}, Ref{MrboParamsC}, Cint, Ref{Ptr{Cvoid}}), sd, pd, device, h))
     end
-    plan = MrboPlan(h[], size(X, 1), tp.mc_iters, 1, tp.horizon)
+    plan = MrboPlan(h[], size(X, 1), M, 1, tp.horizon)
     finalizer(p -> ccall((:mrbo_plan_destroy, libmrbo), Cint, (Ptr{Cvoid},), p.handle), plan)
     return plan
 end
@@ -119,6 +122,46 @@ function simulate_trajectory_mc(T::Trajectory, tp::TrajectoryParameters, backend
                 plan.handle, x0, rns, inner_solve_xstarts, C_NULL, C_NULL, resolutions, gx, gθ, status,
                 C_NULL, C_NULL, C_NULL, flags, C_NULL))
     any(!=(0), status) && throw(ErrorException("rollout failed on $(count(!=(0), status)) trajectories (status bits $(reduce(|, status)))"))
+    μxθ = Distributions.mean(resolutions)
+    σ_μxθ = Distributions.std(resolutions, mean=μxθ)
+    with_grad || return ExpectedTrajectoryOutput(μxθ=μxθ, σ_μxθ=σ_μxθ)
+    ∇μx = vec(Distributions.mean(spatial_gradients_container, dims=2))
+    σ_∇μx = vec(Distributions.std(spatial_gradients_container, dims=2, mean=∇μx))
+    ∇μθ = vec(Distributions.mean(hyperparameter_gradients_container, dims=2))
+    σ_∇μθ = vec(Distributions.std(hyperparameter_gradients_container, dims=2, mean=∇μθ))
+    return ExpectedTrajectoryOutput(μxθ=μxθ, σ_μxθ=σ_μxθ, ∇μx=∇μx, σ_∇μx=σ_∇μx, ∇μθ=∇μθ, σ_∇μθ=σ_∇μθ)
+end
+
+# The GPU method of simulate_trajectory_ghq (rollout.jl:409-467): node vectors nodes[indices[m]]
+# and weights[indices[m]] as M×(h+1) matrices for mrbo_simulate_ghq.
+function simulate_trajectory_ghq(T::Trajectory, tp::TrajectoryParameters, backend::MrboBackend;
+                                 inner_solve_xstarts::Matrix{Float64}, resolutions::Vector{Float64},
+                                 nodes::Vector{Float64}, weights::Vector{Float64}, indices,
+                                 spatial_gradients_container::Union{Nothing, Matrix{Float64}} = nothing,
+                                 hyperparameter_gradients_container::Union{Nothing, Matrix{Float64}} = nothing)
+    set_start!(T, get_starting_point(tp))
+    M = length(indices)
+    depth = length(first(indices))
+    tn = Matrix{Float64}(undef, M, depth)
+    tw = Matrix{Float64}(undef, M, depth)
+    for m in 1:M
+        tn[m, :] .= nodes[indices[m]]
+        tw[m, :] .= weights[indices[m]]
+    end
+    plan = MrboPlan(get_base_surrogate(T), tp, T.θ, size(inner_solve_xstarts, 2); device = backend.device, M = M)
+    with_grad = !isnothing(spatial_gradients_container) && !isnothing(hyperparameter_gradients_container)
+    x0 = copy(T.x0)
+    status = zeros(Int32, M)
+    gx = with_grad ? spatial_gradients_container : C_NULL
+    gθ = with_grad ? hyperparameter_gradients_container : C_NULL
+    flags = MRBO_FLAG_HOST_POINTERS | (with_grad ? UInt32(0) : MRBO_FLAG_NO_GRADIENT)
+    check(ccall((:mrbo_simulate_ghq, libmrbo), Cint,
+                (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Ptr{Float64},
+                 Ptr{Int64}, UInt32, Ptr{Cvoid}),
+                plan.handle, x0, tn, tw, inner_solve_xstarts, C_NULL, C_NULL, resolutions, gx, gθ, status,
+                C_NULL, C_NULL, C_NULL, flags, C_NULL))
+    any(!=(0), status) && throw(ErrorException("rollout failed on $(count(!=(0), status)) trajectories"))
     μxθ = Distributions.mean(resolutions)
     σ_μxθ = Distributions.std(resolutions, mean=μxθ)
     with_grad || return ExpectedTrajectoryOutput(μxθ=μxθ, σ_μxθ=σ_μxθ)

@@ -12,10 +12,12 @@ Compute runs in libmrbo.so (hand-written HIP for gfx950); see include/mrbo.h.
 from .decision_rules import EI, LCB, POI, DecisionRule, RandomAcquisition, get_name
 from .kernels import Matern12, Matern32, Matern52, SquaredExponential, eval_KxX, eval_KXX
 from .optimizers import Adam, StandardSGA, update
-from .rollout import simulate_trajectory_mc, simulate_trajectory_mc_batch
+from .rollout import (simulate_trajectory_ghq, simulate_trajectory_ghq_batch, simulate_trajectory_mc,
+                      simulate_trajectory_mc_batch)
 from .surrogates import DEFAULT_CAPACITY, GROUND_TRUTH_OBSERVATIONS, FantasySurrogate, Surrogate
 from .trajectory import ExpectedTrajectoryOutput, Trajectory, TrajectoryParameters, gen_low_discrepancy_sequence
-from .utils import (ExperimentSetup, eswavs, generate_batch, generate_initial_guesses, kronecker_quasirand,
-                    stochastic_solve, stochastic_solve_batch)
+from .utils import (ExperimentSetup, GaussHermiteObservable, eswavs, gauss_hermite, generate_batch,
+                    generate_indices, generate_initial_guesses, kronecker_quasirand, stochastic_solve,
+                    stochastic_solve_batch)
 
 __version__ = "0.1.0"

@@ -30,7 +30,7 @@ STATUS_BITS = {
 # exported symbols of include/mrbo.h (the library must export all of them)
 EXPORTS = [
     "mrbo_version", "mrbo_last_error", "mrbo_device_count", "mrbo_plan_create", "mrbo_plan_destroy",
-    "mrbo_simulate_mc", "mrbo_eto_reduce", "mrbo_partial_sums", "mrbo_eval_base", "mrbo_rnstream",
+    "mrbo_simulate_mc", "mrbo_simulate_ghq", "mrbo_eto_reduce", "mrbo_partial_sums", "mrbo_eval_base", "mrbo_rnstream",
     "mrbo_initial_guesses", "mrbo_dual_uniform", "mrbo_last_kernel_ms",
 ]
 
@@ -72,6 +72,7 @@ def load():
                                    ctypes.POINTER(_vp)]
     L.mrbo_plan_destroy.argtypes = [_vp]
     L.mrbo_simulate_mc.argtypes = [_vp] + [_vp] * 12 + [ctypes.c_uint32, _vp]
+    L.mrbo_simulate_ghq.argtypes = [_vp] + [_vp] * 13 + [ctypes.c_uint32, _vp]
     L.mrbo_eto_reduce.argtypes = [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]
     L.mrbo_partial_sums.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_int32, _vp, ctypes.c_uint32, _vp]
     L.mrbo_eval_base.argtypes = [_vp, ctypes.c_int32, _vp, _vp, ctypes.c_uint32, _vp]

@@ -105,6 +105,18 @@ class RolloutPlan:
             p(out.get("obs")), p(out.get("evals")), flags, ctypes.c_void_p(st.cuda_stream)))
         return out
 
+    def simulate_ghq(self, x0s, nodes, weights, xstarts, out, dual_y_dx=None, replay_x=None, stream=None):
+        """Launch mrbo_simulate_ghq: nodes / weights are M×(h+1) device tensors (flat, column-major)."""
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        flags = 0 if "grad_x" in out else _lib.MRBO_FLAG_NO_GRADIENT
+        _lib.check(self.lib.mrbo_simulate_ghq(
+            self.handle, p(x0s), p(nodes), p(weights), p(xstarts), p(dual_y_dx), p(replay_x), p(out["values"]),
+            p(out.get("grad_x")), p(out.get("grad_theta")), p(out["status"]), p(out.get("policy_x")),
+            p(out.get("obs")), p(out.get("evals")), flags, ctypes.c_void_p(st.cuda_stream)))
+        return out
+
     def eto(self, out, stream=None):
         torch = _torch()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)

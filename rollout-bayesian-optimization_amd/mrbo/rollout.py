@@ -113,6 +113,54 @@ def simulate_trajectory_mc(T, tp, inner_solve_xstarts, resolutions, spatial_grad
     return ExpectedTrajectoryOutput.from_row(res["eto"][:, 0], T.x0.size, with_gradient)
 
 
+def ghq_node_arrays(nodes, weights, indices):
+    """nodes[indices[m]], weights[indices[m]] as M×depth column-major arrays (the sampler state
+    set_nodes!/set_weights! receives per sample, rollout.jl:431-432)."""
+    idx = np.asarray([np.asarray(ix, dtype=np.int64) for ix in indices])
+    nodes = np.asarray(nodes, dtype=np.float64)
+    weights = np.asarray(weights, dtype=np.float64)
+    return np.asfortranarray(nodes[idx]), np.asfortranarray(weights[idx])
+
+
+def simulate_trajectory_ghq_batch(T, tp, x0s, inner_solve_xstarts, nodes, weights, indices, with_gradient=True,
+                                  dual_y_dx=None, replay_x=None, want_policy=False, want_obs=False, device=0, **opts):
+    """Gauss–Hermite estimator for R restarts (columns of x0s) × len(indices) node vectors."""
+    x0s = np.asarray(x0s, dtype=np.float64)
+    if x0s.ndim == 1:
+        x0s = x0s.reshape(-1, 1)
+    d, R = x0s.shape
+    tn, tw = ghq_node_arrays(nodes, weights, indices)
+    M, depth = tn.shape
+    if depth != tp.horizon + 1:   # GaussHermiteObservable max_invocations (observables.jl:59 assertion)
+        raise ValueError(f"node vectors of depth {depth}; the rollout observes horizon+1 = {tp.horizon + 1} times")
+    lbs, ubs = tp.get_spatial_bounds()
+    plan = _plan_for(T.s, tp.horizon, M, R, inner_solve_xstarts.shape[1], lbs, ubs, T.θ[0], device, opts)
+    dev = f"cuda:{device}"
+    out = plan.alloc_outputs(with_gradient=with_gradient, want_policy=want_policy, want_obs=want_obs)
+    plan.simulate_ghq(to_device(x0s, dev), to_device(tn, dev), to_device(tw, dev), to_device(inner_solve_xstarts, dev),
+                      out, dual_y_dx=None if dual_y_dx is None else to_device(dual_y_dx, dev),
+                      replay_x=None if replay_x is None else to_device(replay_x, dev))
+    return BatchResult(plan, out, plan.eto(out))
+
+
+def simulate_trajectory_ghq(T, tp, inner_solve_xstarts, resolutions, nodes, weights, indices,
+                            spatial_gradients_container=None, hyperparameter_gradients_container=None, device=0,
+                            **opts):
+    """rollout.jl:409-467 (the reference signature): ETO of the Gauss–Hermite resolutions, mean and
+    n−1 std exactly as the Monte-Carlo version (:452-466)."""
+    T.set_start(tp.get_starting_point())
+    with_gradient = spatial_gradients_container is not None and hyperparameter_gradients_container is not None
+    br = simulate_trajectory_ghq_batch(T, tp, T.x0.reshape(-1, 1), np.asarray(inner_solve_xstarts), nodes, weights,
+                                       indices, with_gradient=with_gradient, device=device, **opts)
+    res = br.numpy()
+    raise_on_status(res["status"])
+    resolutions[:] = res["values"][:, 0]
+    if with_gradient:
+        spatial_gradients_container[:, :] = res["grad_x"][:, :, 0]
+        hyperparameter_gradients_container[:, :] = res["grad_theta"][:, :, 0]
+    return ExpectedTrajectoryOutput.from_row(res["eto"][:, 0], T.x0.size, with_gradient)
+
+
 class SurrogateEval:
     """The lazily-forced quantities of eval(s, x, θ) (radial_basis_surrogates.jl:224-310)."""
 

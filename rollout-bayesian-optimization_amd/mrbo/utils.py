@@ -32,6 +32,35 @@ def generate_batch(N, lbs, ubs, ϵinterior=1e-2):
     return B
 
 
+def generate_indices(num_nodes, max_depth):
+    """utils.jl:217-221: every node-index vector of length max_depth, in Julia's
+    `collect(product(fill(1:n, depth)...))` order (first position fastest); 0-based."""
+    import itertools
+    return [tuple(reversed(p)) for p in itertools.product(range(num_nodes), repeat=max_depth)]
+
+
+def gauss_hermite(n):
+    """Physicists' Gauss–Hermite rule: ∫ e^{−t²} f(t) dt ≈ Σ w_i f(t_i) (the √2 / √π scalings of
+    GaussHermiteObservable, observables.jl:58-72, assume this rule)."""
+    return np.polynomial.hermite.hermgauss(n)
+
+
+class GaussHermiteObservable:
+    """observables.jl:32-81 — host-side description of the sampler; the device kernel computes the
+    observations (y = μ + √2σt, ∇y = ∇μ + √2∇σt) and weighted resolutions."""
+
+    def __init__(self, nodes, weights, max_invocations):
+        self.nodes = np.array(nodes, dtype=np.float64)
+        self.weights = np.array(weights, dtype=np.float64)
+        self.trajectory_length = int(max_invocations)
+
+    def set_nodes(self, nodes):
+        self.nodes[:] = nodes
+
+    def set_weights(self, weights):
+        self.weights[:] = weights
+
+
 def early_stopping_without_a_validation_set(grad_f, var_grad_f, sample_size):
     """utils.jl:114-123 (Mahsereci et al.); NaN ratios keep iterating, as in Julia."""
     grad_f = np.asarray(grad_f, dtype=np.float64)

@@ -178,3 +178,35 @@ def test_eto_corrected_std(oracle):
         assert o["eto"][0, r] == pytest.approx(v.mean(), rel=1e-14)
         assert o["eto"][1, r] == pytest.approx(v.std(ddof=1), rel=1e-12)  # Q14: n-1
         np.testing.assert_allclose(o["eto"][2:2 + d, r], o["grad_x"][:, :, r].mean(axis=1), rtol=1e-13, atol=1e-300)
+
+
+# --------------- Gauss–Hermite estimator (rollout.jl:409-467, observables.jl:32-81, 157) ---------
+def test_ghq_horizon0_closed_form(oracle):
+    """h = 0: one observation y = μ + √2σt at x0, so every sample's resolution and gradient are
+    closed forms of the base posterior: w·max(fmini − y, 0)/√π and −w(∇μ + √2∇σ t)."""
+    g = load_golden("c2")
+    s = _osur(oracle, g)
+    d = g["X"].shape[0]
+    t, w = np.polynomial.hermite.hermgauss(12)
+    nodes, weights = np.asfortranarray(t.reshape(-1, 1)), np.asfortranarray(w.reshape(-1, 1))
+    x0 = np.asfortranarray(g["x0s"][:, :1])
+    r = oracle.simulate_mc(s, x0, None, g["xstarts"], g["lbs"], g["ubs"], 0, ghq=(nodes, weights))
+    prim = oracle.eval_base(s, x0)[:, 0]
+    mu, sig, gmu, gsig = prim[0], prim[1], prim[3:3 + d], prim[3 + d:3 + 2 * d]
+    y = mu + np.sqrt(2) * sig * t
+    fmini = float(g["fmini"])
+    np.testing.assert_allclose(r["values"][:, 0], w * np.maximum(fmini - y, 0) / np.sqrt(np.pi), rtol=1e-12,
+                               atol=1e-300)
+    improving = fmini > y
+    expect = -(w[None, :] * (gmu[:, None] + np.sqrt(2) * gsig[:, None] * t[None, :]))
+    np.testing.assert_allclose(r["grad_x"][:, improving, 0], expect[:, improving], rtol=1e-12, atol=1e-15)
+    assert (r["grad_x"][:, ~improving, 0] == 0).all()
+
+
+def test_generate_indices_order():
+    """utils.jl:217-221 ordering: Julia's product iterates the first position fastest."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "rollout-bayesian-optimization_amd"))
+    from mrbo.utils import generate_indices
+    ix = generate_indices(3, 2)
+    assert ix[:4] == [(0, 0), (1, 0), (2, 0), (0, 1)] and len(ix) == 9
