@@ -193,11 +193,14 @@ def main():
                                f"18 inner starts, forward rollout + adjoint gradient per trajectory",
                    "trajectories_per_step": world * (hi - lo) * R, "M_per_gpu": hi - lo, "R": R, "h": h,
                    "N": cfg.N, "d": d, "parallelism": f"mc-shard x{world}"},
-        "roofline": {"bound": "fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": "rollout_kernel<6,1>", "kernel_ms": kms, "flops_per_launch": fl,
-                     "note": "compute-bound fp64 FMA (VALU); algorithmic FLOP model in DESIGN.md §5; "
-                             "HBM algorithmic bytes/traj ~0.3 KB so an HBM roofline does not bind"},
+                     "note": "compute-bound fp64: peak = the dense fp64 matrix peak, equal to the fp64 vector "
+                             "peak on MI355X; the kernel issues VALU v_fma_f64 (matrix-vector work, not "
+                             "GEMM-shaped); algorithmic FLOP model in DESIGN.md §5; HBM algorithmic "
+                             "bytes/traj ~0.3 KB so an HBM roofline does not bind; traffic = PMC bytes per "
+                             "launch from profiles/traffic_<config>.json"},
         "status_errors": int((st != 0).sum()),
         "work_per_traj": {"grad_evals": float(ev[0].mean()), "value_evals": float(ev[1].mean()),
                           "hessians": float(ev[2].mean()), "rich_evals": float(ev[3].mean()),
