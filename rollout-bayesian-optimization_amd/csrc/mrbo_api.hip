@@ -12,7 +12,7 @@
 #include <vector>
 
 #include "../../include/mrbo.h"
-#include "mrbo_rollout.hip"
+#include "mrbo_dispatch.h"
 #include "sobol_table.h"
 
 using namespace mrbo;
@@ -70,33 +70,10 @@ struct mrbo_plan {
 
 namespace {
 
-// ---- kernel dispatch tables -----------------------------------------------------------
-typedef void (*kfun_t)(KParams);
-
-template <int D, int RPL>
-size_t wave_lds_bytes() { return sizeof(double) * Lay<D, RPL>::WAVE_LDS; }
-
-struct KernelSet {
-  const void* rollout;
-  const void* evalb;
-  size_t wave_bytes;
-  bool square;              // L0⁻¹ layout: dense square (ld) or packed triangle
-  int ld;
-  long long linv_doubles;
-};
-
-template <int D, int RPL>
-KernelSet kset() {
-  using Ly = Lay<D, RPL>;
-  return KernelSet{(const void*)&rollout_kernel<D, RPL>, (const void*)&eval_base_kernel<D, RPL>, wave_lds_bytes<D, RPL>(),
-                   Ly::SQ, Ly::LD, Ly::LINV_DOUBLES};
-}
-
+// ---- kernel dispatch: one translation unit per input dimension (mrbo_kernels.hip) -------
 bool get_kset(int d, int rpl, KernelSet& ks) {
-#define CASE(DD)                                        \
-  case DD:                                              \
-    ks = (rpl == 1) ? kset<DD, 1>() : kset<DD, 2>();    \
-    return true;
+#define CASE(DD) \
+  case DD: return kset_d##DD(rpl, ks);
   switch (d) {
 #ifdef MRBO_ONLY_D
     CASE(MRBO_ONLY_D)
@@ -109,11 +86,8 @@ bool get_kset(int d, int rpl, KernelSet& ks) {
 }
 
 void launch_rollout(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
-#define CASE(DD)                                                                           \
-  case DD:                                                                                 \
-    if (rpl == 1) hipLaunchKernelGGL((rollout_kernel<DD, 1>), g, b, sm, st, kp);           \
-    else hipLaunchKernelGGL((rollout_kernel<DD, 2>), g, b, sm, st, kp);                    \
-    break;
+#define CASE(DD) \
+  case DD: launch_rollout_d##DD(rpl, g, b, sm, st, kp); break;
 #ifdef MRBO_ONLY_D
   switch (d) { CASE(MRBO_ONLY_D) }
 #else
@@ -122,11 +96,8 @@ void launch_rollout(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, c
 #undef CASE
 }
 void launch_evalb(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
-#define CASE(DD)                                                                           \
-  case DD:                                                                                 \
-    if (rpl == 1) hipLaunchKernelGGL((eval_base_kernel<DD, 1>), g, b, sm, st, kp);         \
-    else hipLaunchKernelGGL((eval_base_kernel<DD, 2>), g, b, sm, st, kp);                  \
-    break;
+#define CASE(DD) \
+  case DD: launch_evalb_d##DD(rpl, g, b, sm, st, kp); break;
 #ifdef MRBO_ONLY_D
   switch (d) { CASE(MRBO_ONLY_D) }
 #else
@@ -138,9 +109,9 @@ void launch_evalb(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, con
 // choose waves per workgroup maximising resident waves per CU (LDS + register limits)
 // fixed_bytes: per-workgroup tables; the wave areas double as prologue scratch of scratch_bytes
 int pick_grid(const void* fn, size_t fixed_bytes, size_t wave_bytes, int ncu, int& wpg, int& blocks, size_t& smem,
-              size_t scratch_bytes = 0) {
+              size_t scratch_bytes = 0, int maxw = 8) {
   int best_w = 0;
-  for (int w = 1; w <= 8; ++w) {
+  for (int w = 1; w <= maxw; ++w) {
     const size_t sm = fixed_bytes + std::max(w * wave_bytes, scratch_bytes);
     if (sm > 160 * 1024) break;
     int nb = 0;
@@ -321,7 +292,7 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   const int d = s->d, N = s->N;
   if (d < 1 || N < 1 || !s->X || !s->L || !s->c || !s->y) return fail(MRBO_ERR_ARG, "bad surrogate (d=%d N=%d)", d, N);
   if (d > 8) return fail(MRBO_ERR_UNSUPPORTED, "d=%d > 8 not compiled", d);
-  if (N > 128) return fail(MRBO_ERR_UNSUPPORTED, "N=%d > 128 not supported (LDS-resident L0^-1)", N);
+  if (N > 256) return fail(MRBO_ERR_UNSUPPORTED, "N=%d > 256 not compiled", N);
   if (p->h < 0 || p->h > FMAX - 1) return fail(MRBO_ERR_UNSUPPORTED, "h=%d outside [0,%d]", p->h, FMAX - 1);
   if (p->M < 1 || p->R < 1 || p->nstarts < 1 || !p->lbs || !p->ubs) return fail(MRBO_ERR_ARG, "bad params");
   if (p->rule != MRBO_RULE_EI && p->rule != MRBO_RULE_POI && p->rule != MRBO_RULE_LCB)
@@ -333,7 +304,7 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   P->device = device;
   P->d = d;
   P->N = N;
-  P->RPL = (N <= 64) ? 1 : 2;
+  P->RPL = (N <= 64) ? 1 : (N <= 128) ? 2 : 4;
   P->NR = 64 * P->RPL;
   P->Npad = P->NR;
   P->p = *p;
@@ -386,11 +357,14 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   if (e != hipSuccess) { delete P; return fail(MRBO_ERR_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e)); }
   KernelSet ks;
   get_kset(d, P->RPL, ks);
-  // the kernel's LDS image of L0⁻¹ (zero above the diagonal and on padded rows)
-  std::vector<double> packed((size_t)ks.linv_doubles, 0.0);
+  // the kernel's image of L0⁻¹ (zero above the diagonal and on padded rows); the global
+  // variant appends a row-packed copy (row k: columns 0..k) for the backward product
+  std::vector<double> packed((size_t)ks.linv_dev, 0.0);
   for (int j = 0; j < N; ++j)
-    for (int i = j; i < N; ++i)
+    for (int i = j; i < N; ++i) {
       packed[ks.square ? (size_t)j * ks.ld + i : (size_t)linv_colstart(j, Npad) + (i - j)] = Li[i + (size_t)N * j];
+      if (ks.gl) packed[(size_t)linv_size(Npad) + (size_t)i * (i + 1) / 2 + j] = Li[i + (size_t)N * j];
+    }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete P; return fail(MRBO_ERR_HIP, "device props"); }
   const size_t linv_bytes = sizeof(double) * (size_t)ks.linv_doubles;
@@ -404,7 +378,9 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   const size_t fixed = linv_bytes + (P->xs_lds ? xs_bytes : 0);
   int wpg0 = 0, blocks0 = 0;
   size_t smem0 = 0;
-  const int waves0 = pick_grid(ks.rollout, fixed, ks.wave_bytes, prop.multiProcessorCount, wpg0, blocks0, smem0);
+  const int maxw = ks.max_threads / WAVE;
+  const int waves0 =
+      pick_grid(ks.rollout, fixed, ks.wave_bytes, prop.multiProcessorCount, wpg0, blocks0, smem0, 0, maxw);
   P->batch = 0;
   if (ks.square && P->xs_lds && ns <= 64) {
     int wpg1 = 0, blocks1 = 0;
@@ -415,7 +391,8 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   }
   if (!P->batch) { P->wpg = wpg0; P->blocks = blocks0; P->smem = smem0; }
   if (!waves0 ||
-      !pick_grid(ks.evalb, linv_bytes, ks.wave_bytes, prop.multiProcessorCount, P->ewpg, P->eblocks, P->esmem)) {
+      !pick_grid(ks.evalb, linv_bytes, ks.wave_bytes, prop.multiProcessorCount, P->ewpg, P->eblocks, P->esmem, 0,
+                 maxw)) {
     delete P;
     return fail(MRBO_ERR_UNSUPPORTED, "no feasible launch configuration");
   }

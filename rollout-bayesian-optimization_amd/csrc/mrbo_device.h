@@ -16,6 +16,10 @@
 
 namespace mrbo {
 
+// work counters per trajectory (for the algorithmic-FLOP roofline):
+// evals[NCOUNT·t + k], k = gradient evals, value evals, Hessians, adjoint rich evals, pairs
+constexpr int NCOUNT = 5;
+constexpr int NSTAMP = 17;  // MRBO_STAMPS regions (names in mrbo_api.hip)
 constexpr int FMAX = 6;    // fantasy points per trajectory = h+1  (h ≤ 5)
 constexpr int WAVE = 64;
 

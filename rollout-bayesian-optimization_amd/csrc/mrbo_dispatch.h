@@ -1,0 +1,31 @@
+// mrbo_dispatch.h -- interface between the host API (mrbo_api.hip) and the per-dimension
+// kernel translation units (mrbo_kernels.hip compiled once per d = 1..8 with -DMRBO_D=d).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "mrbo_device.h"
+
+namespace mrbo {
+
+// launch geometry and L0⁻¹ image of one rollout_kernel<D, RPL> / eval_base_kernel<D, RPL> pair
+struct KernelSet {
+  const void* rollout;
+  const void* evalb;
+  size_t wave_bytes;        // per-wave LDS
+  bool square;              // L0⁻¹ layout: dense square (ld) or packed triangle
+  int ld;
+  long long linv_doubles;   // LDS-resident L0⁻¹ (0 when it stays in global memory)
+  bool gl;                  // L0⁻¹ in global memory: packed by columns, then packed by rows
+  long long linv_dev;       // doubles of the device image
+  int max_threads;          // launch bound (threads per workgroup)
+};
+
+#define MRBO_DECLARE_D(DD)                                                                      \
+  bool kset_d##DD(int rpl, KernelSet& ks);                                                      \
+  void launch_rollout_d##DD(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp); \
+  void launch_evalb_d##DD(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp);
+MRBO_DECLARE_D(1) MRBO_DECLARE_D(2) MRBO_DECLARE_D(3) MRBO_DECLARE_D(4)
+MRBO_DECLARE_D(5) MRBO_DECLARE_D(6) MRBO_DECLARE_D(7) MRBO_DECLARE_D(8)
+#undef MRBO_DECLARE_D
+
+}  // namespace mrbo

@@ -87,7 +87,13 @@ struct Lay {
   // bank-conflict free and neither needs a triangle mask.  RPL > 1: packed triangle (the
   // square would not fit next to the per-wave areas).
   static constexpr int LD = NR + 1;
-  static constexpr long long LINV_DOUBLES = ((SQ ? (long long)NR * LD : linv_size(NR)) + 1) & ~1LL;
+  // RPL > 2 (N ≤ 256): L0⁻¹ does not fit in LDS next to the wave areas (263 KB packed); it stays
+  // in global memory (L2-resident, shared by every wave of the XCD) as two packed copies --
+  // by columns for the forward product, by rows for the backward one -- so that both row walks
+  // are coalesced 512-byte loads
+  static constexpr bool GL = (RPL > 2);
+  static constexpr long long LINV_DOUBLES = GL ? 0 : (((SQ ? (long long)NR * LD : linv_size(NR)) + 1) & ~1LL);
+  static constexpr long long LINV_GLOBAL = GL ? 2 * linv_size(NR) : LINV_DOUBLES;  // device image
 };
 // scalar slots in U_SC
 enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, SC_GSIG = 6, SC_GMUMU = 7,
@@ -118,7 +124,8 @@ struct WaveCtx {
   double* B;            // LDS: BROWS × BS
   double* red;          // LDS: REDN
   double* U;            // LDS: U_SIZE
-  const double* Linv;   // LDS: L0⁻¹ (Lay::SQ layout)
+  const double* Linv;   // L0⁻¹: LDS (Lay::SQ square or packed columns) or global packed columns (GL)
+  const double* LinvT;  // GL: global L0⁻¹ packed by rows (row k: entries 0..k)
   const double* XS;     // inner-solve start points: LDS copy (kp.xs_lds) or kp.xstarts
   const double* KXB;    // LDS [NR][nstarts]: ψ(|clamp(x_k) − X_i|) (kp.batch)
   const double* GTAB;   // LDS [nstarts][NG]: base Gram of the start points (kp.batch)
@@ -139,9 +146,7 @@ struct WaveCtx {
   }
 };
 
-// work counters per trajectory (for the algorithmic-FLOP roofline):
-// evals[NCOUNT·t + k], k = gradient evals, value evals, Hessians, adjoint rich evals, pairs
-constexpr int NCOUNT = 5;
+// work counters per trajectory (NCOUNT, mrbo_device.h)
 struct Counters {
   int grad = 0, value = 0, hess = 0, rich = 0, pairs = 0;
 };
@@ -154,7 +159,6 @@ struct Counters {
 #else
 #define STAMP(W, k) ((void)0)
 #endif
-constexpr int NSTAMP = 17;
 
 // Per-lane results of an evaluation that later phases (conditioning, adjoint) need.
 template <int D, int RPL>
@@ -335,36 +339,43 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       bcast_product<D1, Ly::LD>(acc[0], Bown[0], W.Linv + lane, N);
     }
   } else {
-  // L0⁻¹[i][j] for this lane's rows; zero above the diagonal and on padded rows
-  auto lfwd = [&](int s, int j) -> double {
-    if constexpr (Ly::SQ) {
-      return W.Linv[j * Ly::LD + lane];
-    } else {
-      const int i = lane + WAVE * s;
-      const double l = W.Linv[linv_colstart(j, W.Npad) - j + (i > j ? i : j)];
-      return (i >= j) ? l : 0.0;
-    }
+  // L0⁻¹[i][j] for this lane's row i = lane + 64s.  Row block s needs columns j < 64(s+1) only
+  // (j-blocks jb ≤ s); inside the diagonal block the entries above the diagonal read as zero.
+  // Skipping the all-zero blocks leaves every accumulation order unchanged.
+  auto lfwd = [&](int s, int jb, int j) -> double {
+    const int i = lane + WAVE * s;
+    if (s > jb) return W.Linv[linv_colstart(j, W.Npad) - j + i];
+    const double l = W.Linv[linv_colstart(j, W.Npad) - j + (i > j ? i : j)];
+    return (i >= j) ? l : 0.0;
   };
   if (all_cols) {
+#pragma unroll
+    for (int jb = 0; jb < RPL; ++jb) {
+      const int j1 = (N < WAVE * (jb + 1)) ? N : WAVE * (jb + 1);
 #pragma unroll 4
-    for (int j = 0; j < N; ++j) {
-      const double* bj = B + j * BS;
-      double bv[D1];
+      for (int j = WAVE * jb; j < j1; ++j) {
+        const double* bj = B + j * BS;
+        double bv[D1];
 #pragma unroll
-      for (int c = 0; c < D1; ++c) bv[c] = bj[c];
+        for (int c = 0; c < D1; ++c) bv[c] = bj[c];
 #pragma unroll
-      for (int s = 0; s < RPL; ++s) {
-        const double l = lfwd(s, j);
+        for (int s = jb; s < RPL; ++s) {
+          const double l = lfwd(s, jb, j);
 #pragma unroll
-        for (int c = 0; c < D1; ++c) acc[s][c] = fma(l, bv[c], acc[s][c]);
+          for (int c = 0; c < D1; ++c) acc[s][c] = fma(l, bv[c], acc[s][c]);
+        }
       }
     }
   } else {
-#pragma unroll 8
-    for (int j = 0; j < N; ++j) {
-      const double b0 = B[j * BS];
 #pragma unroll
-      for (int s = 0; s < RPL; ++s) acc[s][0] = fma(lfwd(s, j), b0, acc[s][0]);
+    for (int jb = 0; jb < RPL; ++jb) {
+      const int j1 = (N < WAVE * (jb + 1)) ? N : WAVE * (jb + 1);
+#pragma unroll 8
+      for (int j = WAVE * jb; j < j1; ++j) {
+        const double b0 = B[j * BS];
+#pragma unroll
+        for (int s = jb; s < RPL; ++s) acc[s][0] = fma(lfwd(s, jb, j), b0, acc[s][0]);
+      }
     }
   }
   }
@@ -606,37 +617,50 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       }
     } else {
     // lane i walks column i of L0⁻¹ (= row i of L0⁻ᵀ) in a wave-uniform k loop; Y[k] is an
-    // LDS broadcast.  L0⁻¹[k][i] is zero for k < i and on padded rows.
-    auto lbwd = [&](int s, int k) -> double {
-      if constexpr (Ly::SQ) {
-        return W.Linv[lane * Ly::LD + k];
+    // LDS broadcast.  Row block s needs k ≥ 64s only (k-blocks kb ≥ s); L0⁻¹[k][i] is zero for
+    // k < i and on padded rows.  GL reads the row-packed global copy (coalesced in i).
+    auto lbwd = [&](int s, int kb, int k) -> double {
+      const int i = lane + WAVE * s;
+      if constexpr (Ly::GL) {
+        const long long rs = (long long)k * (k + 1) / 2;
+        if (s < kb) return W.LinvT[rs + i];
+        const double l = W.LinvT[rs + (i < k ? i : k)];
+        return (k >= i) ? l : 0.0;
       } else {
-        const int i = lane + WAVE * s;
+        if (s < kb) return W.Linv[linv_colstart(i, W.Npad) - i + k];
         const double l = W.Linv[linv_colstart(i, W.Npad) - i + (k > i ? k : i)];
         return (k >= i) ? l : 0.0;
       }
     };
     if (rich) {
+#pragma unroll
+      for (int kb = 0; kb < RPL; ++kb) {
+        const int k1 = (N < WAVE * (kb + 1)) ? N : WAVE * (kb + 1);
 #pragma unroll 2
-      for (int k = 0; k < N; ++k) {
-        const double* yk = B + k * BS;
-        double yv[D1];
+        for (int k = WAVE * kb; k < k1; ++k) {
+          const double* yk = B + k * BS;
+          double yv[D1];
 #pragma unroll
-        for (int c = 0; c < D1; ++c) yv[c] = yk[c];
+          for (int c = 0; c < D1; ++c) yv[c] = yk[c];
 #pragma unroll
-        for (int s = 0; s < RPL; ++s) {
-          const double l = lbwd(s, k);
-          wv[s] = fma(l, yv[0], wv[s]);
+          for (int s = 0; s <= kb; ++s) {
+            const double l = lbwd(s, kb, k);
+            wv[s] = fma(l, yv[0], wv[s]);
 #pragma unroll
-          for (int a = 0; a < D; ++a) pv[s][a] = fma(l, yv[1 + a], pv[s][a]);
+            for (int a = 0; a < D; ++a) pv[s][a] = fma(l, yv[1 + a], pv[s][a]);
+          }
         }
       }
     } else {
-#pragma unroll 8
-      for (int k = 0; k < N; ++k) {
-        const double y0 = B[k * BS];
 #pragma unroll
-        for (int s = 0; s < RPL; ++s) wv[s] = fma(lbwd(s, k), y0, wv[s]);
+      for (int kb = 0; kb < RPL; ++kb) {
+        const int k1 = (N < WAVE * (kb + 1)) ? N : WAVE * (kb + 1);
+#pragma unroll 8
+        for (int k = WAVE * kb; k < k1; ++k) {
+          const double y0 = B[k * BS];
+#pragma unroll
+          for (int s = 0; s <= kb; ++s) wv[s] = fma(lbwd(s, kb, k), y0, wv[s]);
+        }
       }
     }
     }
@@ -1749,6 +1773,14 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
 // ================================================================================
 // Kernels
 // ================================================================================
+// launch bounds: 2 waves per SIMD (256 VGPRs each) up to N = 128; the N ≤ 256 variant runs one
+// wave per SIMD, whose 512-entry register file (256 VGPRs + 256 AGPRs) holds the four-row state
+template <int RPL>
+struct KBounds {
+  static constexpr int threads = RPL > 2 ? 256 : 512;
+  static constexpr int waves_per_simd = RPL > 2 ? 1 : MRBO_WAVES_PER_SIMD;
+};
+
 template <int D, int RPL>
 __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp, double* smem, int wave_in_block) {
   using Ly = Lay<D, RPL>;
@@ -1763,7 +1795,8 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
   W.red = wbase + Ly::BROWS * Ly::BS;
   W.U = W.red + Ly::REDN;
   W.G12 = W.U + Ly::U_SIZE;
-  W.Linv = smem;
+  W.Linv = Ly::GL ? kp.Linv : smem;
+  W.LinvT = kp.Linv + linv_size(Ly::NR);
   const long long slot = (long long)blockIdx.x * (blockDim.x / WAVE) + wave_in_block;
   if constexpr (Ly::SQ) W.E = W.G12 + Ly::G12;
   else W.E = kp.work + slot * kp.work_stride;
@@ -1784,7 +1817,7 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
 }
 
 template <int D, int RPL>
-__global__ void __launch_bounds__(512, MRBO_WAVES_PER_SIMD) rollout_kernel(KParams kp) {
+__global__ void __launch_bounds__(KBounds<RPL>::threads, KBounds<RPL>::waves_per_simd) rollout_kernel(KParams kp) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // stage L0⁻¹ (and the inner-solve start points) once per workgroup (the only block barrier)
   using Ly = Lay<D, RPL>;
@@ -1817,7 +1850,7 @@ __global__ void __launch_bounds__(512, MRBO_WAVES_PER_SIMD) rollout_kernel(KPara
 
 // eval(s, x, θ) on the base surrogate for P points (fixture / primitive parity path)
 template <int D, int RPL>
-__global__ void __launch_bounds__(512, MRBO_WAVES_PER_SIMD) eval_base_kernel(KParams kp) {
+__global__ void __launch_bounds__(KBounds<RPL>::threads, KBounds<RPL>::waves_per_simd) eval_base_kernel(KParams kp) {
   using Ly = Lay<D, RPL>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   for (int q = threadIdx.x; q < (int)Ly::LINV_DOUBLES; q += blockDim.x) smem[q] = kp.Linv[q];

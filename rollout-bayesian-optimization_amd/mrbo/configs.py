@@ -35,6 +35,10 @@ CONFIGS = {
     "C2": Config("C2", "braninhoo", 2, 2, 256, 16, 32, 1, "2D Branin, h=2, 256 MC x 16 restarts, n=32"),
     "C3": Config("C3", "hartmann6d", 6, 3, 1024, 64, 64, 1, "6D Hartmann, h=3, 1024 MC x 64 restarts, n=64 (headline)"),
     "C4": Config("C4", "hartmann6d", 6, 4, 8192, 256, 128, 8, "6D Hartmann, h=4, 8192 MC x 256 restarts, n=128"),
+    # BASELINE names "8D Ackley + NonUniformCost": NonUniformCost (cost_functions.jl:5-20) is
+    # referenced by no decision rule, surrogate or trajectory (SURVEY.md §0 finding 5), so the
+    # rollout path is the plain EI one; the cost enters nothing here either
+    "C5": Config("C5", "ackley", 8, 5, 16384, 512, 256, 8, "8D Ackley, h=5, 16384 MC x 512 restarts, n=256"),
 }
 
 

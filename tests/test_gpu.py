@@ -23,7 +23,7 @@ def _plan(g, M=None, R=None, h=None, nstarts=None, kernel=0, theta=0.0, **opts):
     M = M or g["rnstream"].shape[0]
     R = R or g["x0s"].shape[1]
     h = int(g["h"]) if h is None else h
-    return RolloutPlan(g["X"], g["L"], g["c"], g["y"], kernel, 1.0, 1e-6, float(g["fmini"]), h, M, R,
+    return RolloutPlan(g["X"], g["L"], g["c"], g["y"], kernel, float(g.get("ell", 1.0)), 1e-6, float(g["fmini"]), h, M, R,
                        nstarts or g["xstarts"].shape[1], g["lbs"], g["ubs"], theta, **opts)
 
 
@@ -52,7 +52,8 @@ def _run(plan, g, dual=None, replay=None, want_policy=True, with_gradient=True, 
 
 
 def _osur(oracle, g, kernel="matern52"):
-    return oracle.OracleSurrogate(g["X"], g["L"], g["c"], g["y"], kernel=kernel, fmini=float(g["fmini"]))
+    return oracle.OracleSurrogate(g["X"], g["L"], g["c"], g["y"], kernel=kernel, ell=float(g.get("ell", 1.0)),
+                                  fmini=float(g["fmini"]))
 
 
 def _assert_grads_close(a, b, rtol=1e-6):
@@ -80,9 +81,9 @@ def test_replay_vs_golden(gpu, case):
     _assert_grads_close(r["grad_theta"], g["grad_theta"])
 
 
-def _problem_arrays(name, M, R, kernel=None, testfn=None, d=None, N=None, h=None):
+def _problem_arrays(name, M, R, kernel=None, testfn=None, d=None, N=None, h=None, ell=None):
     from mrbo import configs
-    from mrbo.kernels import Matern12, Matern32, SquaredExponential
+    from mrbo.kernels import Matern12, Matern32, Matern52, SquaredExponential
     if testfn is not None:
         cfg = configs.Config(f"T{testfn}{d}", testfn, d, h, M, R, N, 1)
         pb = configs.Problem(cfg)
@@ -91,15 +92,20 @@ def _problem_arrays(name, M, R, kernel=None, testfn=None, d=None, N=None, h=None
     s = pb.surrogate
     if kernel is not None:
         s.set_kernel({"matern32": Matern32(), "matern12": Matern12(), "se": SquaredExponential()}[kernel])
+    if ell is not None:
+        s.set_kernel(Matern52([ell]))
     n = s.observed
     return dict(X=s.X[:, :n], L=s.L[:n, :n], c=s.c[:n], y=s.y[:n], fmini=s.fmini(), lbs=pb.lbs, ubs=pb.ubs,
-                x0s=pb.x0s, rnstream=pb.tp.rnstream_sequence, xstarts=pb.es.get_starts(), h=pb.cfg.h)
+                x0s=pb.x0s, rnstream=pb.tp.rnstream_sequence, xstarts=pb.es.get_starts(), h=pb.cfg.h,
+                ell=1.0 if ell is None else ell)
 
 
-@pytest.mark.parametrize("name,M,R", [("C1", 32, 4), ("C2", 32, 4), ("C3", 32, 4)])
-def test_end_to_end_vs_oracle(gpu, oracle, name, M, R):
-    """Both sides run the full rollout including the inner Newton solves."""
-    g = _problem_arrays(name, M, R)
+@pytest.mark.parametrize("name,M,R,ell", [("C1", 32, 4, None), ("C2", 32, 4, None), ("C3", 32, 4, None),
+                                         ("C4", 8, 2, None), ("C5", 4, 2, None), ("C5", 4, 2, 20.0)])
+def test_end_to_end_vs_oracle(gpu, oracle, name, M, R, ell):
+    """Both sides run the full rollout including the inner Newton solves.  C5 also runs with a
+    lengthscale at the design spacing (dense K; at ℓ = 1 its K is nearly the identity)."""
+    g = _problem_arrays(name, M, R, ell=ell)
     r = _run(_plan(g), g)
     o = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
                            nthreads=8)
@@ -201,11 +207,18 @@ def test_other_kernels_replay_vs_oracle(gpu, oracle, kernel, kid):
 
 
 @pytest.mark.parametrize("d,N,h", [(1, 12, 2), (3, 24, 2), (4, 40, 3), (5, 30, 2), (7, 48, 2), (8, 64, 3), (3, 96, 2),
-                                   (6, 128, 4)])
+                                   (6, 128, 4), (3, 150, 2), (5, 200, 5), (8, 256, 3)])
 def test_dimensions_and_sizes_replay_vs_oracle(gpu, oracle, d, N, h):
-    """d = 1..8 and N up to 128 (two data rows per lane) on Ackley(d)."""
-    g = _problem_arrays(None, 8, 2, testfn="ackley", d=d, N=N, h=h)
-    r = _run(_plan(g), g)
+    """d = 1..8 and N up to 256 on Ackley(d): one data row per lane (N ≤ 64, L0⁻¹ square in
+    LDS), two (N ≤ 128, packed in LDS), four (N ≤ 256, L0⁻¹ in global memory); ragged N.  The
+    lengthscale tracks the design spacing (0.6 · width · N^(-1/d)) so that K is dense: with ℓ = 1
+    on Ackley's 65-wide box K ≈ I and the triangular products would multiply zeros."""
+    ell = 0.6 * 65.536 * N ** (-1.0 / d)
+    g = _problem_arrays(None, 8, 2, testfn="ackley", d=d, N=N, h=h, ell=ell)
+    p = _plan(g)
+    pts = np.asfortranarray(g["xstarts"][:, :6] * 0.9 + 0.05 * g["x0s"][:, :1])
+    np.testing.assert_allclose(p.eval_base(pts), oracle.eval_base(_osur(oracle, g), pts), rtol=1e-9, atol=1e-12)
+    r = _run(p, g)
     assert (r["status"] == 0).all()
     rp = np.asfortranarray(r["policy_x"][:, 1:])
     o = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], h,

@@ -2,13 +2,17 @@
 # Build A/B variants of libmrbo.so (d=6 only) into mrbo/variants/ for timing on the GPU box.
 # usage: tools/build_variants.sh name:"-DFLAG ..." [name:"..."] ...   (default: base + stamps)
 set -e
-cd "$(dirname "$0")/../rollout-bayesian-optimization_amd"
-mkdir -p mrbo/variants
+cd "$(dirname "$0")/.."
+mkdir -p rollout-bayesian-optimization_amd/mrbo/variants
 [ $# -eq 0 ] && set -- "base:" "stamps:-DMRBO_STAMPS"
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DMRBO_ONLY_D=6 $flags \
-    -o mrbo/variants/libmrbo_$name.so csrc/mrbo_api.hip &
+  python3 - "$name" "$flags" <<'PY' &
+import shlex, sys
+import __graft_entry__ as g
+name, flags = sys.argv[1], sys.argv[2]
+g.compile_lib(f"{g.PKG}/mrbo/variants/libmrbo_{name}.so", extra=shlex.split(flags), dims=[6], jobs=2)
+PY
 done
 wait
-ls -la mrbo/variants
+ls -la rollout-bayesian-optimization_amd/mrbo/variants
