@@ -34,6 +34,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C3")
+    ap.add_argument("--mc-per-gpu", type=int, default=0,
+                    help="MC samples per GPU (default: the config's M; the metric config is C3 at M=1024)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--eta", type=float, default=0.5, help="StandardSGA step (optimizers.jl:6-23)")
@@ -106,7 +108,7 @@ def main():
         else:
             dist.init_process_group(backend)
     cfg = configs.CONFIGS[args.config]
-    M_local, R, d, h = cfg.M, cfg.R, cfg.d, cfg.h
+    M_local, R, d, h = (args.mc_per_gpu or cfg.M), cfg.R, cfg.d, cfg.h
     M_total = M_local * world
     lo, hi = parallel.shard(M_total, world, rank)
     pb = configs.problem(args.config, M=M_total)
@@ -195,7 +197,7 @@ def main():
                    "N": cfg.N, "d": d, "parallelism": f"mc-shard x{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": "rollout_kernel<6,1>", "kernel_ms": kms, "flops_per_launch": fl,
+                     "kernel": f"rollout_kernel<{d},{1 if cfg.N <= 64 else 2 if cfg.N <= 128 else 4}>", "kernel_ms": kms, "flops_per_launch": fl,
                      "note": "compute-bound fp64: peak = the dense fp64 matrix peak, equal to the fp64 vector "
                              "peak on MI355X; the kernel issues VALU v_fma_f64 (matrix-vector work, not "
                              "GEMM-shaped); algorithmic FLOP model in DESIGN.md §5; HBM algorithmic "

@@ -13,6 +13,9 @@
  *   mrbo_eval_base         eval(s::Surrogate, x, θ) radial_basis_surrogates.jl:224-310 (μ, σ, ∇, Hα)
  *   mrbo_rnstream          gen_low_discrepancy_sequence utils.jl:65-74 (Sobol→Box–Muller(log10))
  *   mrbo_initial_guesses   generate_initial_guesses utils.jl:145-153
+ *   mrbo_gp_fit            Surrogate(ψ, X, y) radial_basis_surrogates.jl:77-118 and its
+ *                          log_likelihood / ∇log_likelihood (:770-799) for a batch of
+ *                          lengthscales -- the evaluations behind optimize! (:805-829)
  *
  * Conventions
  *   - Plain pointers and sizes; matrices are column-major with the reference's (Julia) shapes.
@@ -168,6 +171,17 @@ int mrbo_partial_sums(mrbo_plan_t* plan, const double* values, const double* gra
 /* eval(s, x, θ) of the base surrogate at P points xs (d×P); out stride 3+4d+d²:
  * [μ, σ, α, ∇μ(d), ∇σ(d), ∇α(d), Hα(d×d col-major), d2α/dxdθ(d)].                       */
 int mrbo_eval_base(mrbo_plan_t* plan, int32_t P, const double* xs, double* out, uint32_t flags, void* stream);
+
+/* Base-GP fit at P lengthscales ells[p] (kernel, σn2, X d×N, y N from s; s->L, s->c unused):
+ * K = Ψ(‖Xi−Xj‖)+σn2·I, L = chol(K), c = L'\(L\y), and
+ *   ll[p]  = log_likelihood = −yᵀc/2 − Σ log L_ii − N·log(2π)/2
+ *   dll[p] = ∂ll/∂ℓ = (cᵀ δK c − tr(L'\(L\δK)))/2,  δK = eval_Dθ_KXX(ψ, X, [1])
+ * status[p] = 0, or 1 when cholesky throws PosDefException (ll, dll = NaN).  L_out (N×N×P,
+ * lower, zeros above) and c_out (N×P) are optional (NULL).  ells / ll / dll / status / L_out /
+ * c_out are device pointers unless MRBO_FLAG_HOST_POINTERS; N ≤ 256.  Allocates its
+ * workspace (3·N²·P doubles) on the stream.                                                */
+int mrbo_gp_fit(const mrbo_surrogate_t* s, int32_t P, const double* ells, double* ll, double* dll, int32_t* status,
+                double* L_out, double* c_out, uint32_t flags, void* stream);
 
 /* Host helpers (HOST memory). */
 int mrbo_rnstream(int32_t M, int32_t d, int32_t H, double* out);                 /* M×(d+1)×H */

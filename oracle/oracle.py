@@ -60,6 +60,8 @@ def lib():
                                     ctypes.c_int32, _dp, _dp]
         L.rbo_simulate_mc.argtypes = [ctypes.POINTER(Surrogate), ctypes.POINTER(Params), _dp, _dp, _dp, _dp, _dp,
                                       _dp, _dp, _dp, _ip, _dp, _dp, _dp, _lp]
+        L.rbo_log_likelihood.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_double,
+                                         ctypes.c_double, _dp, _dp, _dp, _dp, _dp, _dp]
         L.rbo_simulate_ghq.argtypes = [ctypes.POINTER(Surrogate), ctypes.POINTER(Params), _dp, _dp, _dp, _dp, _dp,
                                        _dp, _dp, _dp, _dp, _ip, _dp, _dp, _dp, _lp]
         _lib = L
@@ -120,6 +122,18 @@ class OracleSurrogate:
 
 
 RULES = {"EI": 0, "POI": 1, "LCB": 2}
+
+
+def log_likelihood(X, y, kernel="matern52", ell=1.0, sigma_n2=1e-6, want_fit=False):
+    """(ll, dll[, L, c]) of the GP refit at lengthscale ell; NaNs on PosDefException."""
+    X, y = _f64(X), _f64(y).ravel()
+    d, N = X.shape
+    ll, dll = ctypes.c_double(), ctypes.c_double()
+    L = np.zeros((N, N), order="F")
+    c = np.zeros(N)
+    lib().rbo_log_likelihood(d, N, KERNELS[kernel], float(ell), float(sigma_n2), _p(X), _p(y), ctypes.byref(ll),
+                             ctypes.byref(dll), _p(L), _p(c))
+    return (ll.value, dll.value, L, c) if want_fit else (ll.value, dll.value)
 
 
 def eval_base(osur, xs, theta=0.0, sigma_tol=1e-8, rule="EI"):

@@ -1104,6 +1104,66 @@ int rbo_simulate_ghq(const rbo_surrogate* s, const rbo_params* p, const double* 
                        status, policy_x, obs, eto, evals);
 }
 
+/* ------------------------------------------------------------------------------------
+ * Base-GP fit and marginal likelihood (between-step surrogate maintenance)
+ *   Surrogate ctor           radial_basis_surrogates.jl:77-118 (K, L = cholesky(K), c = L'\(L\y))
+ *   log_likelihood           :770-776   −y'c/2 − Σ log diag(L) − n log(2π)/2
+ *   δlog_likelihood          :778-785   (c'δK c − tr(L'\(L\δK)))/2
+ *   ∇log_likelihood          :787-799   δθ = e_1 (one lengthscale)
+ *   eval_Dθ_KXX              radial_basis_functions.jl:264-284 (δK_jj = ∇θψ(0)'δθ = 0)
+ * ∇θ_ψ (ForwardDiff there, :43) in closed form.
+ * ---------------------------------------------------------------------------------- */
+static double k_dpsi_dell(const kern_t* k, double rho) {
+  switch (k->kind) {
+    case RBO_K_MATERN52: { const double s = sqrt(5.0) / k->ell * rho; return (s * s / 3.0) * (1 + s) * exp(-s) / k->ell; }
+    case RBO_K_MATERN32: { const double s = sqrt(3.0) / k->ell * rho; return s * s * exp(-s) / k->ell; }
+    case RBO_K_MATERN12: { const double s = rho / k->ell; return s * exp(-s) / k->ell; }
+    default: { const double t = rho * rho / (k->ell * k->ell); return exp(-t / 2) * t / k->ell; }
+  }
+}
+
+int rbo_log_likelihood(int32_t d, int32_t N, int32_t kernel, double ell, double sigma_n2, const double* X,
+                       const double* y, double* ll, double* dll, double* L_out, double* c_out) {
+  const kern_t k = {kernel, ell};
+  const int64_t NN = (int64_t)N * N;
+  double* K = (double*)calloc((size_t)NN, sizeof(double));
+  double* dK = (double*)calloc((size_t)NN, sizeof(double));
+  double* L = (double*)malloc(sizeof(double) * NN);
+  double* c = (double*)malloc(sizeof(double) * N);
+  double* col = (double*)malloc(sizeof(double) * N);
+  double* tmp = (double*)malloc(sizeof(double) * N);
+  double r[64];
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < N; ++i) {
+      for (int a = 0; a < d; ++a) r[a] = X[a + (int64_t)d * i] - X[a + (int64_t)d * j];
+      const double rho = vnorm(r, d);
+      K[i + (int64_t)N * j] = (i == j) ? k_psi(&k, 0.0) + sigma_n2 : k_psi(&k, rho);
+      dK[i + (int64_t)N * j] = (i == j) ? 0.0 : k_dpsi_dell(&k, rho);
+    }
+  int rc = chol_small(K, N, L);
+  if (rc == 0) {
+    kinv(L, N, N, y, c, tmp);
+    double yc = 0, ld = 0, cgc = 0, tr = 0;
+    for (int i = 0; i < N; ++i) { yc += y[i] * c[i]; ld += log(L[i + (int64_t)N * i]); }
+    for (int j = 0; j < N; ++j) {
+      double sj = 0;
+      for (int i = 0; i < N; ++i) sj += dK[i + (int64_t)N * j] * c[i];
+      cgc += c[j] * sj;
+      kinv(L, N, N, dK + (int64_t)N * j, col, tmp);   /* column j of L'\(L\δK) */
+      tr += col[j];
+    }
+    *ll = -yc / 2 - ld - N * log(2 * JL_PI) / 2;
+    *dll = (cgc - tr) / 2;
+    if (L_out) memcpy(L_out, L, sizeof(double) * NN);
+    if (c_out) memcpy(c_out, c, sizeof(double) * N);
+  } else {
+    *ll = NAN;
+    *dll = NAN;
+  }
+  free(K); free(dK); free(L); free(c); free(col); free(tmp);
+  return rc == 0 ? 0 : 1;
+}
+
 int rbo_eval_base(const rbo_surrogate* s, int32_t rule, double theta, double sigma_tol, int32_t P, const double* xs,
                   double* out) {
   fsur_t fs;

@@ -8,6 +8,7 @@
  * It restates, in plain C and in the reference's own (column-major, Julia) layout:
  *   rollout.jl:39-340            rollout!, resolve, gradient (adjoint), simulate_trajectory_mc
  *   radial_basis_surrogates.jl   Surrogate/FantasySurrogate eval, condition!, gp_draw,
+ *                                log_likelihood / ∇log_likelihood (:770-799),
  *                                Spatial/DataPerturbationSurrogate (dense δK, as written)
  *   radial_basis_functions.jl    Matern52/32/12, SquaredExponential and their ρ-derivatives
  *   decision_rules.jl:84-127     EI, POI, LCB and their partials (closed forms of the ForwardDiff partials)
@@ -115,6 +116,12 @@ int rbo_simulate_ghq(const rbo_surrogate* s, const rbo_params* p, const double* 
                      const double* weights, const double* xstarts, const double* dual_y_dx, const double* replay_x,
                      double* values, double* grad_x, double* grad_theta, int32_t* status, double* policy_x,
                      double* obs, double* eto, int64_t* evals);
+
+/* Base-GP refit at lengthscale ell (Surrogate ctor, radial_basis_surrogates.jl:77-118) and its
+ * log_likelihood (:770-776) and ∂/∂ℓ (∇log_likelihood :787-799 via δlog_likelihood :778-785).
+ * Returns 1 (ll = dll = NaN) on PosDefException.  L_out (N×N, lower) and c_out optional. */
+int rbo_log_likelihood(int32_t d, int32_t N, int32_t kernel, double ell, double sigma_n2, const double* X,
+                       const double* y, double* ll, double* dll, double* L_out, double* c_out);
 
 /* Test functions (testfns.jl) used to make base data y. id: 0 GramacyLee, 1 BraninHoo,
  * 2 Hartmann6D, 3 Ackley(d), 4 Rosenbrock, 5 Rastrigin(d). */

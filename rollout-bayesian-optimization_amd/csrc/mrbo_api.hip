@@ -576,6 +576,44 @@ int mrbo_eval_base(mrbo_plan_t* P, int32_t npts, const double* xs, double* out, 
   return MRBO_OK;
 }
 
+int mrbo_gp_fit(const mrbo_surrogate_t* s, int32_t np, const double* ells, double* ll, double* dll, int32_t* status,
+                double* L_out, double* c_out, uint32_t flags, void* stream) {
+  if (!s || !ells || !ll || !dll || !status || np < 1) return fail(MRBO_ERR_ARG, "null argument");
+  const int d = s->d, N = s->N;
+  if (d < 1 || N < 1 || !s->X || !s->y) return fail(MRBO_ERR_ARG, "bad surrogate (d=%d N=%d)", d, N);
+  if (N > 256) return fail(MRBO_ERR_UNSUPPORTED, "N=%d > 256", N);
+  if (s->kernel < 0 || s->kernel > 3) return fail(MRBO_ERR_ARG, "kernel id %d", s->kernel);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t P = (size_t)np, NN = (size_t)N * N;
+  Stage sg;
+  const double* dells = ells;
+  double *dll_ = ll, *ddll = dll, *dL = L_out, *dc = c_out;
+  int32_t* dst = status;
+  if (flags & MRBO_FLAG_HOST_POINTERS) {
+    if (sg.in(ells, P, &dells) || sg.out(P, ll, &dll_) || sg.out(P, dll, &ddll) || sg.out(P, status, &dst) ||
+        sg.out(NN * P, L_out, &dL) || sg.out((size_t)N * P, c_out, &dc))
+      return fail(MRBO_ERR_NOMEM, "staging allocation failed");
+  }
+  const double *dX = nullptr, *dy = nullptr;
+  if (sg.in(s->X, (size_t)d * N, &dX) || sg.in(s->y, (size_t)N, &dy)) return fail(MRBO_ERR_NOMEM, "staging X, y");
+  double* work = nullptr;
+  if (hipMalloc(&work, sizeof(double) * 3 * NN * P) != hipSuccess) return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
+  sg.bufs.push_back(work);
+  GpFitParams q{d, N, s->kernel, s->sigma_n2, dX, dy, dells, dll_, ddll, (int*)dst, dL, dc, work};
+  launch_gpfit(np, st, q);
+  HIP_TRY(hipGetLastError());
+  // the staging buffers and the workspace are freed on return: finish the launch first
+  HIP_TRY(hipStreamSynchronize(st));
+  if (flags & MRBO_FLAG_HOST_POINTERS) {
+    HIP_TRY(hipMemcpy(ll, dll_, sizeof(double) * P, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(dll, ddll, sizeof(double) * P, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(status, dst, sizeof(int32_t) * P, hipMemcpyDeviceToHost));
+    if (L_out) HIP_TRY(hipMemcpy(L_out, dL, sizeof(double) * NN * P, hipMemcpyDeviceToHost));
+    if (c_out) HIP_TRY(hipMemcpy(c_out, dc, sizeof(double) * N * P, hipMemcpyDeviceToHost));
+  }
+  return MRBO_OK;
+}
+
 double mrbo_last_kernel_ms(mrbo_plan_t* P) {
   if (!P || !P->timed) return -1.0;
   float ms = -1.f;

@@ -28,4 +28,20 @@ MRBO_DECLARE_D(1) MRBO_DECLARE_D(2) MRBO_DECLARE_D(3) MRBO_DECLARE_D(4)
 MRBO_DECLARE_D(5) MRBO_DECLARE_D(6) MRBO_DECLARE_D(7) MRBO_DECLARE_D(8)
 #undef MRBO_DECLARE_D
 
+// base-GP fit + marginal likelihood for P lengthscales (mrbo_gpfit.hip)
+struct GpFitParams {
+  int d, N, kernel;
+  double sn2;
+  const double* X;     // d×N
+  const double* y;     // N
+  const double* ells;  // P
+  double* ll;          // P
+  double* dll;         // P
+  int* status;         // P: 0, or 1 = PosDefException
+  double* L_out;       // optional N×N×P
+  double* c_out;       // optional N×P
+  double* work;        // 3·N²·P
+};
+void launch_gpfit(int P, hipStream_t st, const GpFitParams& q);
+
 }  // namespace mrbo

@@ -7,10 +7,12 @@ Reference API surface kept (DarianNwankwo/Rollout-Bayesian-Optimization):
   trajectories       Trajectory, TrajectoryParameters, ExpectedTrajectoryOutput  trajectory.jl
   rollout            simulate_trajectory_mc                    rollout.jl:279-340
   outer ascent       StandardSGA, Adam, eswavs, stochastic_solve  optimizers.jl, utils.jl
+  surrogate upkeep   log_likelihood, ∇log_likelihood, optimize!  radial_basis_surrogates.jl:770-829
 Compute runs in libmrbo.so (hand-written HIP for gfx950); see include/mrbo.h.
 """
 from .decision_rules import EI, LCB, POI, DecisionRule, RandomAcquisition, get_name
 from .kernels import Matern12, Matern32, Matern52, SquaredExponential, eval_KxX, eval_KXX
+from .mle import grad_log_likelihood, gp_fit_batch, log_likelihood, optimize
 from .optimizers import Adam, StandardSGA, update
 from .rollout import (simulate_trajectory_ghq, simulate_trajectory_ghq_batch, simulate_trajectory_mc,
                       simulate_trajectory_mc_batch)

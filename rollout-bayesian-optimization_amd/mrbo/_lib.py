@@ -31,7 +31,7 @@ STATUS_BITS = {
 EXPORTS = [
     "mrbo_version", "mrbo_last_error", "mrbo_device_count", "mrbo_plan_create", "mrbo_plan_destroy",
     "mrbo_simulate_mc", "mrbo_simulate_ghq", "mrbo_eto_reduce", "mrbo_partial_sums", "mrbo_eval_base", "mrbo_rnstream",
-    "mrbo_initial_guesses", "mrbo_dual_uniform", "mrbo_last_kernel_ms",
+    "mrbo_initial_guesses", "mrbo_dual_uniform", "mrbo_last_kernel_ms", "mrbo_gp_fit",
 ]
 
 
@@ -80,6 +80,8 @@ def load():
     L.mrbo_initial_guesses.argtypes = [ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp]
     L.mrbo_dual_uniform.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]
     L.mrbo_dual_uniform.restype = ctypes.c_double
+    L.mrbo_gp_fit.argtypes = [ctypes.POINTER(SurrogateDesc), ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp,
+                              ctypes.c_uint32, _vp]
     L.mrbo_last_kernel_ms.argtypes = [_vp]
     L.mrbo_last_kernel_ms.restype = ctypes.c_double
     _lib = L

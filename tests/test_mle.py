@@ -1,0 +1,165 @@
+"""Between-step surrogate maintenance: log_likelihood, ∇log_likelihood and
+optimize! (radial_basis_surrogates.jl:770-829).
+
+CPU: the oracle's restatement against an independent NumPy/SciPy one and central finite
+differences (the reference's FD methodology, runtests.jl:11-20), and the host minimiser driven
+by the oracle.  GPU (marked): mrbo_gp_fit against the oracle, and optimize! on the device
+against the same minimiser driven by the oracle.  Parity of the optimum with Optim.jl's
+Fminbox(LBFGS()) is unpinned (Optim.jl absent); both target the same box-constrained
+stationary point, which the tests check through its KKT conditions.
+"""
+import numpy as np
+import pytest
+from scipy.linalg import cho_factor, cho_solve
+
+KERNELS = ["matern52", "matern32", "matern12", "se"]
+
+
+def _psi(kernel, ell, rho):
+    if kernel == "matern52":
+        s = np.sqrt(5.0) / ell * rho
+        return (1 + s + s * s / 3) * np.exp(-s)
+    if kernel == "matern32":
+        s = np.sqrt(3.0) / ell * rho
+        return (1 + s) * np.exp(-s)
+    if kernel == "matern12":
+        return np.exp(-rho / ell)
+    return np.exp(-rho * rho / (2 * ell * ell))
+
+
+def _numpy_ll(X, y, kernel, ell, sn2, h=1e-5):
+    """Independent restatement: K via SciPy's Cholesky; dll via the trace formula with δK from a
+    central difference of ψ in ℓ."""
+    rho = np.sqrt(((X[:, :, None] - X[:, None, :]) ** 2).sum(0))
+    K = _psi(kernel, ell, rho) + sn2 * np.eye(len(y))
+    cf = cho_factor(K, lower=True)
+    c = cho_solve(cf, y)
+    ll = -y @ c / 2 - np.log(np.diag(cf[0])).sum() - len(y) * np.log(2 * np.pi) / 2
+    dK = (_psi(kernel, ell + h, rho) - _psi(kernel, ell - h, rho)) / (2 * h)
+    np.fill_diagonal(dK, 0.0)
+    dll = (c @ dK @ c - np.trace(cho_solve(cf, dK))) / 2
+    return ll, dll
+
+
+def _data(d, N, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.random((d, N))
+    y = np.sin(3 * X.sum(0)) + 0.1 * rng.standard_normal(N)
+    return X, y
+
+
+# SE's K is numerically singular on 30 points in [0,1]³ beyond ℓ ≈ 1: keep its cases conditioned
+@pytest.mark.parametrize("kernel,ell", [(k, e) for k in KERNELS[:3] for e in (0.3, 1.0, 2.5)] +
+                         [("se", 0.1), ("se", 0.3), ("se", 0.6)])
+def test_oracle_loglik_vs_numpy_and_fd(oracle, kernel, ell):
+    X, y = _data(3, 30)
+    ll, dll = oracle.log_likelihood(X, y, kernel, ell, 1e-6)
+    ll_np, dll_np = _numpy_ll(X, y, kernel, ell, 1e-6)
+    assert ll == pytest.approx(ll_np, rel=1e-9)
+    assert dll == pytest.approx(dll_np, rel=1e-6, abs=1e-6)
+    h = 1e-6 * ell
+    fd = (oracle.log_likelihood(X, y, kernel, ell + h, 1e-6)[0] - oracle.log_likelihood(X, y, kernel, ell - h, 1e-6)[0]) / (2 * h)
+    assert dll == pytest.approx(fd, rel=1e-6, abs=1e-6)
+
+
+def test_oracle_loglik_posdef_failure(oracle):
+    X, y = _data(2, 10)
+    # σn2 = −1 zeroes the diagonal (ψ(0) = 1): the first pivot is 0 → PosDefException.  (A
+    # duplicated point with σn2 = 0 leaves a pivot of ±rounding, passing or failing by order.)
+    ll, dll = oracle.log_likelihood(X, y, "se", 0.5, -1.0)
+    assert np.isnan(ll) and np.isnan(dll)
+
+
+def _oracle_fg(oracle, X, y, kernel, sn2):
+    def fg(T):
+        r = [oracle.log_likelihood(X, y, kernel, float(t), sn2) for t in T[:, 0]]
+        return np.array([-a for a, _ in r]), np.array([[-b] for _, b in r])
+    return fg
+
+
+def _assert_kkt(theta, g, lo, hi, tol):
+    if theta <= lo:
+        assert g >= -tol
+    elif theta >= hi:
+        assert g <= tol
+    else:
+        assert abs(g) <= tol
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_projected_lbfgs_reaches_box_stationary_point(oracle, kernel):
+    """optimize!'s objective −log_likelihood over ℓ ∈ [0.1, 5] (experiments/nonmyopic_bayesopt.jl:230)."""
+    from mrbo.mle import projected_lbfgs
+    X, y = _data(2, 25, seed=3)
+    fg = _oracle_fg(oracle, X, y, kernel, 1e-6)
+    θ, f, g, it = projected_lbfgs(fg, np.array([1.0]), [0.1], [5.0], iterations=60)
+    _assert_kkt(θ[0], g[0], 0.1, 5.0, 1e-5 * max(1.0, abs(f)))
+    # no better point on a dense grid around the optimum's basin
+    grid = np.linspace(max(0.1, θ[0] * 0.8), min(5.0, θ[0] * 1.2), 41)
+    fgrid, _ = fg(grid[:, None])
+    assert f <= np.nanmin(fgrid) + 1e-9 * abs(f)
+
+
+def test_projected_lbfgs_respects_bounds(oracle):
+    from mrbo.mle import projected_lbfgs
+    X, y = _data(2, 25, seed=3)
+    fg = _oracle_fg(oracle, X, y, "matern52", 1e-6)
+    θ, f, g, it = projected_lbfgs(fg, np.array([0.5]), [0.1], [0.2], iterations=30)
+    assert 0.1 <= θ[0] <= 0.2
+    _assert_kkt(θ[0], g[0], 0.1, 0.2, 1e-6 * max(1.0, abs(f)))
+
+
+# ---------------------------------------------------------------------------------- GPU
+def _surrogate(X, y, kernel, ell, sn2=1e-6):
+    from mrbo import kernels
+    from mrbo.surrogates import Surrogate
+    k = {"matern52": kernels.Matern52, "matern32": kernels.Matern32, "matern12": kernels.Matern12,
+         "se": kernels.SquaredExponential}[kernel]([ell])
+    return Surrogate(k, X, y, capacity=len(y), σn2=sn2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("d,N", [(1, 8), (3, 20), (6, 64), (5, 150), (8, 256)])
+def test_gp_fit_vs_oracle(gpu, oracle, kernel, d, N):
+    from mrbo.mle import gp_fit_batch
+    X, y = _data(d, N, seed=d)
+    ells = np.array([0.2, 0.5, 1.0, 2.0, 4.0]) * np.sqrt(d) * (0.15 if kernel == "se" else 1.0)
+    s = _surrogate(X, y, kernel, 1.0)
+    r = gp_fit_batch(s, ells, want_fit=True)
+    for p, ell in enumerate(ells):
+        ll, dll, L, c = oracle.log_likelihood(X, y, kernel, ell, 1e-6, want_fit=True)
+        if np.isnan(ll):
+            assert r["status"][p] == 1
+            continue
+        assert r["status"][p] == 0
+        assert r["ll"][p] == pytest.approx(ll, rel=1e-10, abs=1e-9)
+        assert r["dll"][p] == pytest.approx(dll, rel=1e-8, abs=1e-8 * (1 + abs(ll)))
+        np.testing.assert_allclose(r["L"][:, :, p], L, rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(r["c"][:, p], c, rtol=1e-8, atol=1e-8 * np.abs(c).max())
+
+
+@pytest.mark.gpu
+def test_gp_fit_posdef_failure(gpu):
+    from mrbo.mle import gp_fit_batch
+    X, y = _data(2, 10)
+    s = _surrogate(X, y, "se", 0.5)
+    s.σn2 = -1.0                   # zero diagonal: first pivot 0 (see the oracle test above)
+    r = gp_fit_batch(s, [0.5, 1.0])
+    assert (r["status"] == 1).all() and np.isnan(r["ll"]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_optimize_on_device_vs_oracle_driven(gpu, oracle, kernel):
+    """optimize!(s; lowerbounds=[0.1], upperbounds=[5.]) on the device: same minimiser as the
+    oracle-driven run (same iterates up to rounding), a KKT point, and the surrogate refit."""
+    from mrbo.mle import log_likelihood, optimize, projected_lbfgs
+    X, y = _data(2, 25, seed=3)
+    s = _surrogate(X, y, kernel, 1.0)
+    res = optimize(s, [0.1], [5.0], iterations=30)
+    θo, fo, go, _ = projected_lbfgs(_oracle_fg(oracle, X, y, kernel, 1e-6), np.array([1.0]), [0.1], [5.0], 30)
+    assert res["theta"][0] == pytest.approx(θo[0], rel=1e-7)
+    assert s.ψ.lengthscale == pytest.approx(θo[0], rel=1e-7)
+    assert log_likelihood(s) == pytest.approx(-fo, rel=1e-10)
+    _assert_kkt(res["theta"][0], res["gradient"][0], 0.1, 5.0, 1e-5 * max(1.0, abs(fo)))
