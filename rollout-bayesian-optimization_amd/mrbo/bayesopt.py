@@ -1,0 +1,172 @@
+"""Non-myopic Bayesian-optimisation loop on the rollout acquisition.
+
+Mirrors experiments/nonmyopic_bayesopt.jl -- its CLI, its experiment layout and its CSV outputs
+(create_csv / write_to_csv, utils.jl:155-172) -- with the acquisition step routed through the
+rollout path as the survey prescribes: the reference's main loop calls the myopic
+multistart_base_solve! (:245-253) and its adaptive driver names a rollout_solver that is
+defined nowhere (experiments/adaptive_bayesopt.jl:490), so the solver here is build-defined:
+
+  batch = generate_batch(batch_size)             utils.jl:97-106 (Sobol + two near-bound points)
+  x_r  ← stochastic_solve from every batch point  utils.jl:235-265 (StandardSGA, eswavs stop),
+         all restarts in one rollout launch per SGA iteration (stochastic_solve_batch)
+  xnext = the restart with the largest final ETO mean, clamped to the box
+
+Per budget step the metrics are recorded as in the reference (:268-289): time of the solve,
+gap and simple regret of the observations BEFORE conditioning on xnext, then condition!,
+optionally optimize! (lengthscale MLE on the device, bounds [0.1, 5]), then the minimum
+observation.  `allocations` is the reference's @timed byte count; the build records the
+device workspace is preallocated and writes 0.
+
+Parity with the reference's BO trajectories is unpinned: Julia's MersenneTwister initial
+designs, Optim.jl's inner solves and the undefined rollout solver cannot be reproduced.
+"""
+import argparse
+import os
+import time
+
+import numpy as np
+
+from . import testfns as T
+from .decision_rules import EI, LCB, POI
+from .kernels import Matern52
+from .optimizers import StandardSGA
+from .rollout import simulate_trajectory_mc_batch
+from .surrogates import FantasySurrogate, Surrogate
+from .trajectory import Trajectory, TrajectoryParameters
+from .utils import ExperimentSetup, gap, generate_batch, simple_regret, stochastic_solve_batch
+
+INITIAL_OBSERVATIONS = 5            # nonmyopic_bayesopt.jl:131
+METRICS = ["times", "gaps", "allocations", "simple_regret", "minimum_observations"]   # :191
+KERNEL_LBS, KERNEL_UBS = [0.1], [5.0]   # :230
+
+TESTFNS = {
+    "gramacylee": T.TestGramacyLee,
+    "braninhoo": T.TestBraninHoo,
+    "hartmann6d": T.TestHartmann6D,
+    "rosenbrock": T.TestRosenbrock,
+    **{f"ackley{d}d": (lambda d=d: T.TestAckley(d)) for d in (1, 2, 3, 4, 5, 8)},
+    **{f"rastrigin{d}d": (lambda d=d: T.TestRastrigin(d)) for d in (1, 4)},
+}
+
+
+# ---- CSV outputs (utils.jl:155-172) --------------------------------------------------------
+def _fmt(v):
+    v = float(v)
+    return repr(v) if np.isfinite(v) else ("NaN" if np.isnan(v) else ("Inf" if v > 0 else "-Inf"))
+
+
+def create_csv(filename, budget):
+    """create_csv: header [trial; 1..budget] and one placeholder row of −1.0."""
+    with open(filename + ".csv", "w") as f:
+        f.write(",".join(["trial"] + [str(b) for b in range(1, budget + 1)]) + "\n")
+        f.write(",".join(["-1.0"] * (budget + 1)) + "\n")
+
+
+def write_to_csv(filename, data):
+    """write_to_csv: append `data` as one row (CSV.write(Tables.table(data'), append=true) writes
+    the budget values only, without a trial column)."""
+    with open(filename + ".csv", "a") as f:
+        f.write(",".join(_fmt(v) for v in np.asarray(data, dtype=np.float64).ravel()) + "\n")
+
+
+def write_metadata(directory, budget, trials, starts):
+    """write_metadata_to_file (:102-118)."""
+    with open(os.path.join(directory, "metadata.txt"), "w") as f:
+        f.write(f"Budget: {budget}\nNumber of Trials: {trials}\nNumber of Starts: {starts}\n")
+
+
+# ---- one acquisition solve -------------------------------------------------------------------
+def rollout_solve(sur, lbs, ubs, horizon, mc_samples, batch_size, starts, sgd_iterations, theta, eta=0.5,
+                  device=0):
+    """xnext from the rollout acquisition: SGA restarts from a Sobol batch, best final ETO mean."""
+    lbs, ubs = np.asarray(lbs, float), np.asarray(ubs, float)
+    batch = generate_batch(batch_size, lbs, ubs)
+    tp = TrajectoryParameters(start=batch[:, 0], hypers=[theta], horizon=horizon, mc_iterations=mc_samples,
+                              use_low_discrepancy_sequence=True, spatial_lowerbounds=lbs, spatial_upperbounds=ubs)
+    es = ExperimentSetup(tp, number_of_starts=starts)
+    traj = Trajectory(sur, FantasySurrogate(sur, horizon), start=batch[:, 0], hypers=[theta], horizon=horizon)
+    opts = [StandardSGA(η=eta) for _ in range(batch.shape[1])]
+    x, _ = stochastic_solve_batch(opts, sur, tp, es, batch, T=traj, iterations=sgd_iterations, device=device)
+    x = np.clip(x, lbs[:, None], ubs[:, None])
+    etos = simulate_trajectory_mc_batch(traj, tp, x, es.get_starts(), with_gradient=False, device=device).etos(
+        with_gradient=False)
+    means = np.array([e.mean() for e in etos])
+    means = np.where(np.isfinite(means), means, -np.inf)
+    k = int(np.argmax(means))
+    return x[:, k].copy(), float(means[k])
+
+
+# ---- the experiment loop (nonmyopic_bayesopt.jl:120-300) -------------------------------------
+def run(function_name, output_dir, budget=15, trials=60, starts=16, horizon=0, mc_samples=200, batch_size=8,
+        sgd_iterations=50, optimize=False, seed=1906, device=0, log=print):
+    testfn = TESTFNS[function_name]()
+    lbs, ubs = testfn.get_bounds()
+    directory = os.path.join(output_dir, function_name)
+    os.makedirs(directory, exist_ok=True)
+    acquisitions = [f"rollout_{horizon}_ei", f"rollout_{horizon}_poi", f"rollout_{horizon}_lcb"]
+    dr_hypers = [0.0, 0.0, 2.0]
+    rules = [EI(), POI(), LCB()]
+    for metric in METRICS:
+        for acq in acquisitions:
+            create_csv(os.path.join(directory, f"{acq}_{metric}"), budget)
+    write_metadata(directory, budget, trials, starts)
+    rng = np.random.default_rng(seed)
+    initial_samples = [lbs[:, None] + (ubs - lbs)[:, None] * rng.random((testfn.dim, INITIAL_OBSERVATIONS))
+                       for _ in range(trials)]
+    true_minimum = float(testfn.f(np.asarray(testfn.xopt[0], dtype=np.float64)))
+    results = {}
+    for acq, rule, theta in zip(acquisitions, rules, dr_hypers):
+        log(f"Conducting experiments with acquisition = {acq}")
+        for trial in range(trials):
+            Xinit = initial_samples[trial]
+            yinit = testfn(Xinit)
+            sur = Surrogate(Matern52(), Xinit, yinit, capacity=budget + INITIAL_OBSERVATIONS, decision_rule=rule,
+                            σn2=1e-6)
+            initial_best = float(np.min(yinit))
+            times, gaps, allocs, regrets, minobs = (np.zeros(budget) for _ in range(5))
+            for b in range(budget):
+                t0 = time.perf_counter()
+                xnext, _ = rollout_solve(sur, lbs, ubs, horizon, mc_samples, batch_size, starts, sgd_iterations,
+                                         theta, device=device)
+                times[b] = time.perf_counter() - t0
+                observed_best = float(np.min(sur.get_active_observations()))
+                regrets[b] = simple_regret(true_minimum, observed_best)
+                gaps[b] = gap(initial_best, observed_best, true_minimum)
+                sur.condition(xnext, float(testfn.f(xnext)))
+                if optimize:
+                    from .mle import optimize as mle_optimize
+                    mle_optimize(sur, KERNEL_LBS, KERNEL_UBS)
+                minobs[b] = float(np.min(sur.get_active_observations()))
+            for metric, data in zip(METRICS, (times, gaps, allocs, regrets, minobs)):
+                write_to_csv(os.path.join(directory, f"{acq}_{metric}"), data)
+            results[(acq, trial)] = dict(times=times, gaps=gaps, simple_regret=regrets, minimum_observations=minobs,
+                                         X=sur.get_active_covariates().copy(), y=sur.get_active_observations().copy())
+    return results
+
+
+def parse(argv=None):
+    """parse_command_line (nonmyopic_bayesopt.jl:4-75)."""
+    ap = argparse.ArgumentParser("Non-myopic Bayesian optimisation on the MI355X rollout acquisition")
+    ap.add_argument("--seed", type=int, default=1906)
+    ap.add_argument("--optimize", action="store_true", help="optimize the surrogate's lengthscale (MLE)")
+    ap.add_argument("--starts", type=int, default=16)
+    ap.add_argument("--trials", type=int, default=60)
+    ap.add_argument("--budget", type=int, default=15)
+    ap.add_argument("--output-dir", required=True)
+    ap.add_argument("--mc-samples", type=int, default=200)
+    ap.add_argument("--horizon", type=int, default=0)
+    ap.add_argument("--batch-size", type=int, default=8)
+    ap.add_argument("--function-name", required=True, choices=sorted(TESTFNS))
+    ap.add_argument("--sgd-iterations", type=int, default=50)
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    a = parse(argv)
+    run(a.function_name, a.output_dir, budget=a.budget, trials=a.trials, starts=a.starts, horizon=a.horizon,
+        mc_samples=a.mc_samples, batch_size=a.batch_size, sgd_iterations=a.sgd_iterations, optimize=a.optimize,
+        seed=a.seed)
+
+
+if __name__ == "__main__":
+    main()
