@@ -49,7 +49,8 @@ typedef enum {
   MRBO_KERNEL_MATERN52 = 0, /* radial_basis_functions.jl:60-68  */
   MRBO_KERNEL_MATERN32 = 1, /* :70-78 */
   MRBO_KERNEL_MATERN12 = 2, /* :80-88 */
-  MRBO_KERNEL_SE = 3        /* :90-96 */
+  MRBO_KERNEL_SE = 3,       /* :90-96 */
+  MRBO_KERNEL_PERIODIC = 4  /* :98-103  exp(−2 sin²(πρ/p)/ℓ²), p = mrbo_surrogate_t.period */
 } mrbo_kernel_t;
 
 typedef enum {
@@ -86,6 +87,7 @@ typedef struct {
   int32_t ldL;
   const double* c;      /* N coefficients L'\(L\y)                                */
   const double* y;      /* N observations                                        */
+  double period;        /* ψ.θ[2] of the Periodic kernel (unused otherwise)      */
 } mrbo_surrogate_t;
 
 /* TrajectoryParameters (trajectory.jl:43-94) + inner-solve options (rbf_optim.jl:24-30). */

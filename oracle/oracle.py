@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "librbo_oracle.so")
 _lib = None
 
-KERNELS = {"matern52": 0, "matern32": 1, "matern12": 2, "se": 3}
+KERNELS = {"matern52": 0, "matern32": 1, "matern12": 2, "se": 3, "periodic": 4}
 TESTFNS = {"gramacylee": 0, "braninhoo": 1, "hartmann6d": 2, "ackley": 3, "rosenbrock": 4, "rastrigin": 5}
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -25,7 +25,7 @@ _lp = ctypes.POINTER(ctypes.c_int64)
 class Surrogate(ctypes.Structure):
     _fields_ = [("d", ctypes.c_int32), ("N", ctypes.c_int32), ("kernel", ctypes.c_int32),
                 ("ell", ctypes.c_double), ("sigma_n2", ctypes.c_double), ("fmini", ctypes.c_double),
-                ("X", _dp), ("L", _dp), ("c", _dp), ("y", _dp)]
+                ("X", _dp), ("L", _dp), ("c", _dp), ("y", _dp), ("period", ctypes.c_double)]
 
 
 class Params(ctypes.Structure):
@@ -114,11 +114,12 @@ def testfn(name, x):
 class OracleSurrogate:
     """Holds the base-surrogate arrays alive for the C struct."""
 
-    def __init__(self, X, L, c, y, kernel="matern52", ell=1.0, sigma_n2=1e-6, fmini=None):
+    def __init__(self, X, L, c, y, kernel="matern52", ell=1.0, sigma_n2=1e-6, fmini=None, period=1.0):
         self.X, self.L, self.c, self.y = _f64(X), _f64(L), _f64(c), _f64(y)
         d, N = self.X.shape
         fm = float(np.min(self.y)) if fmini is None else float(fmini)
-        self.s = Surrogate(d, N, KERNELS[kernel], ell, sigma_n2, fm, _p(self.X), _p(self.L), _p(self.c), _p(self.y))
+        self.s = Surrogate(d, N, KERNELS[kernel], ell, sigma_n2, fm, _p(self.X), _p(self.L), _p(self.c), _p(self.y),
+                           float(period))
 
 
 RULES = {"EI": 0, "POI": 1, "LCB": 2}
@@ -131,8 +132,10 @@ def log_likelihood(X, y, kernel="matern52", ell=1.0, sigma_n2=1e-6, want_fit=Fal
     ll, dll = ctypes.c_double(), ctypes.c_double()
     L = np.zeros((N, N), order="F")
     c = np.zeros(N)
-    lib().rbo_log_likelihood(d, N, KERNELS[kernel], float(ell), float(sigma_n2), _p(X), _p(y), ctypes.byref(ll),
-                             ctypes.byref(dll), _p(L), _p(c))
+    rc = lib().rbo_log_likelihood(d, N, KERNELS[kernel], float(ell), float(sigma_n2), _p(X), _p(y), ctypes.byref(ll),
+                                  ctypes.byref(dll), _p(L), _p(c))
+    if rc < 0:
+        raise ValueError(f"log_likelihood: kernel {kernel} not supported")
     return (ll.value, dll.value, L, c) if want_fit else (ll.value, dll.value)
 
 

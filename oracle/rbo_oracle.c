@@ -203,13 +203,19 @@ double rbo_testfn(int32_t id, int32_t d, const double* x) {
  * Kernels: radial_basis_functions.jl:60-103 (ψ) and the ρ-derivatives that
  * compute_derivatives (:41-46) takes by ForwardDiff -- restated in closed form.
  * ---------------------------------------------------------------------------------- */
-typedef struct { int kind; double ell; } kern_t;
+typedef struct { int kind; double ell, per; } kern_t;
+
+/* Periodic (:98-103): ψ = exp(−2 sin²(πρ/p)/ℓ²).  With A = 2π/(pℓ²), B = 2π/p, t = Bρ:
+ * ψ' = −ψ A sin t,  ψ'' = ψ (A² sin²t − A B cos t). */
+#define PER_A(k) (2 * JL_PI / ((k)->per * (k)->ell * (k)->ell))
+#define PER_B(k) (2 * JL_PI / (k)->per)
 
 static double k_psi(const kern_t* k, double rho) {
   switch (k->kind) {
     case RBO_K_MATERN52: { const double c = sqrt(5.0) / k->ell, s = c * rho; return (1 + s * (1 + s / 3.0)) * exp(-s); }
     case RBO_K_MATERN32: { const double c = sqrt(3.0) / k->ell, s = c * rho; return (1 + s) * exp(-s); }
     case RBO_K_MATERN12: { const double s = rho / k->ell; return exp(-s); }
+    case RBO_K_PERIODIC: { const double sn = sin(JL_PI * rho / k->per); return exp(-2 * sn * sn / (k->ell * k->ell)); }
     default: return exp(-rho * rho / (2 * k->ell * k->ell));
   }
 }
@@ -218,6 +224,7 @@ static double k_dpsi(const kern_t* k, double rho) {
     case RBO_K_MATERN52: { const double c = sqrt(5.0) / k->ell, s = c * rho; return -c * (s / 3.0) * (1 + s) * exp(-s); }
     case RBO_K_MATERN32: { const double c = sqrt(3.0) / k->ell, s = c * rho; return -c * s * exp(-s); }
     case RBO_K_MATERN12: { const double c = 1.0 / k->ell; return -c * exp(-c * rho); }
+    case RBO_K_PERIODIC: return -k_psi(k, rho) * PER_A(k) * sin(PER_B(k) * rho);
     default: { const double l2 = k->ell * k->ell; return -(rho / l2) * exp(-rho * rho / (2 * l2)); }
   }
 }
@@ -226,6 +233,10 @@ static double k_d2psi(const kern_t* k, double rho) {
     case RBO_K_MATERN52: { const double c = sqrt(5.0) / k->ell, s = c * rho; return c * c * (s * s - s - 1) * exp(-s) / 3.0; }
     case RBO_K_MATERN32: { const double c = sqrt(3.0) / k->ell, s = c * rho; return c * c * (s - 1) * exp(-s); }
     case RBO_K_MATERN12: { const double c = 1.0 / k->ell; return c * c * exp(-c * rho); }
+    case RBO_K_PERIODIC: {
+      const double A = PER_A(k), B = PER_B(k), t = B * rho, st = sin(t);
+      return k_psi(k, rho) * (A * A * st * st - A * B * cos(t));
+    }
     default: { const double l2 = k->ell * k->ell; return (rho * rho / (l2 * l2) - 1.0 / l2) * exp(-rho * rho / (2 * l2)); }
   }
 }
@@ -397,7 +408,7 @@ typedef struct {
 
 static int fsur_alloc(fsur_t* fs, const rbo_surrogate* s, int h, int rule) {
   fs->d = s->d; fs->N = s->N; fs->h = h; fs->cap = s->N + h + 1; fs->rule = rule;
-  fs->k.kind = s->kernel; fs->k.ell = s->ell; fs->sn2 = s->sigma_n2;
+  fs->k.kind = s->kernel; fs->k.ell = s->ell; fs->k.per = s->period; fs->sn2 = s->sigma_n2;
   fs->X = (double*)calloc((size_t)fs->d * fs->cap, sizeof(double));
   fs->L = (double*)calloc((size_t)fs->cap * fs->cap, sizeof(double));
   fs->y = (double*)calloc((size_t)fs->cap, sizeof(double));
@@ -617,6 +628,7 @@ static void k_gcert(const kern_t* k, double* gmu, double* gsig) {
     }
     case RBO_K_MATERN32: *gmu = 1.01 * (sqrt(3.0) / k->ell) * exp(-1.0); break;
     case RBO_K_MATERN12: *gmu = 1.01 / k->ell; break;
+    case RBO_K_PERIODIC: *gmu = 1.01 * PER_A(k); break;   /* |ψ'| = ψ A |sin t| ≤ A */
     default: *gmu = 1.01 * (1.0 / k->ell) * exp(-0.5); break;
   }
   *gsig = (d2 < 0) ? 1.01 * sqrt(k_psi(k, 0.0) * -d2) : -1.0;
@@ -1124,7 +1136,8 @@ static double k_dpsi_dell(const kern_t* k, double rho) {
 
 int rbo_log_likelihood(int32_t d, int32_t N, int32_t kernel, double ell, double sigma_n2, const double* X,
                        const double* y, double* ll, double* dll, double* L_out, double* c_out) {
-  const kern_t k = {kernel, ell};
+  const kern_t k = {kernel, ell, 1.0};
+  if (kernel == RBO_K_PERIODIC) return -1;   /* two hyperparameters: ∂/∂ℓ alone is not ∇log_likelihood */
   const int64_t NN = (int64_t)N * N;
   double* K = (double*)calloc((size_t)NN, sizeof(double));
   double* dK = (double*)calloc((size_t)NN, sizeof(double));

@@ -10,7 +10,7 @@
  *   radial_basis_surrogates.jl   Surrogate/FantasySurrogate eval, condition!, gp_draw,
  *                                log_likelihood / ∇log_likelihood (:770-799),
  *                                Spatial/DataPerturbationSurrogate (dense δK, as written)
- *   radial_basis_functions.jl    Matern52/32/12, SquaredExponential and their ρ-derivatives
+ *   radial_basis_functions.jl    Matern52/32/12, SquaredExponential, Periodic and their ρ-derivatives
  *   decision_rules.jl:84-127     EI, POI, LCB and their partials (closed forms of the ForwardDiff partials)
  *   observables.jl:83-124        StochasticObservable (gp_draw with gradient)
  *   utils.jl:4-74,145-153        Sobol uniforms, Box–Muller(log10), rnstream reshape, inner starts
@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-enum { RBO_K_MATERN52 = 0, RBO_K_MATERN32 = 1, RBO_K_MATERN12 = 2, RBO_K_SE = 3 };
+enum { RBO_K_MATERN52 = 0, RBO_K_MATERN32 = 1, RBO_K_MATERN12 = 2, RBO_K_SE = 3, RBO_K_PERIODIC = 4 };
 
 /* per-trajectory status bits (reference: Julia exceptions, see SURVEY.md §8b "Errors") */
 enum {
@@ -53,6 +53,7 @@ typedef struct {
   const double* L;         /* N×N lower Cholesky of K, column-major, ld = N      */
   const double* c;         /* N, L'\(L\y)                                        */
   const double* y;         /* N                                                  */
+  double period;           /* Periodic kernel θ[2] (radial_basis_functions.jl:98-103) */
 } rbo_surrogate;
 
 typedef struct {

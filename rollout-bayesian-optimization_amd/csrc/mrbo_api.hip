@@ -45,7 +45,7 @@ struct mrbo_plan {
   mrbo_params_t p{};
   std::vector<double> lbs, ubs;
   int kernel = 0;
-  double ell = 1, cK = 1, psi0 = 1, d2psi0 = -1, sn2 = 1e-6;
+  double ell = 1, cK = 1, cP = 0, psi0 = 1, d2psi0 = -1, sn2 = 1e-6;
   double gcert_mu = 0, gcert_sig = -1;
   double fmin_base = 0, fmini = 0;
   // device state
@@ -214,7 +214,7 @@ static void fill_common(const mrbo_plan_t* P, KParams& kp) {
   memset(&kp, 0, sizeof kp);
   kp.d = P->d; kp.N = P->N; kp.Npad = P->Npad; kp.h = P->p.h; kp.M = P->p.M; kp.R = P->p.R;
   kp.nstarts = P->p.nstarts;
-  kp.kernel = P->kernel; kp.rule = P->p.rule; kp.ell = P->ell; kp.cK = P->cK; kp.psi0 = P->psi0; kp.d2psi0 = P->d2psi0; kp.sn2 = P->sn2;
+  kp.kernel = P->kernel; kp.rule = P->p.rule; kp.ell = P->ell; kp.cK = P->cK; kp.cP = P->cP; kp.psi0 = P->psi0; kp.d2psi0 = P->d2psi0; kp.sn2 = P->sn2;
   kp.gcert_mu = P->gcert_mu; kp.gcert_sig = P->gcert_sig;
   kp.fmin_base = P->fmin_base; kp.fmini = P->fmini; kp.theta = P->p.theta;
   kp.max_iters = P->p.max_iters; kp.max_ls = P->p.max_ls;
@@ -297,7 +297,8 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   if (p->M < 1 || p->R < 1 || p->nstarts < 1 || !p->lbs || !p->ubs) return fail(MRBO_ERR_ARG, "bad params");
   if (p->rule != MRBO_RULE_EI && p->rule != MRBO_RULE_POI && p->rule != MRBO_RULE_LCB)
     return fail(MRBO_ERR_ARG, "unknown decision rule %d", (int)p->rule);
-  if (s->kernel < 0 || s->kernel > 3) return fail(MRBO_ERR_ARG, "kernel id %d", s->kernel);
+  if (s->kernel < 0 || s->kernel > 4) return fail(MRBO_ERR_ARG, "kernel id %d", s->kernel);
+  if (s->kernel == MRBO_KERNEL_PERIODIC && !(s->period > 0.0)) return fail(MRBO_ERR_ARG, "period %g", s->period);
   const int ldL = s->ldL > 0 ? s->ldL : N;
 
   mrbo_plan* P = new mrbo_plan();
@@ -323,6 +324,7 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
     case 0: P->cK = std::sqrt(5.0) / ell; P->d2psi0 = -P->cK * P->cK / 3.0; break;
     case 1: P->cK = std::sqrt(3.0) / ell; P->d2psi0 = -P->cK * P->cK; break;
     case 2: P->cK = 1.0 / ell; P->d2psi0 = P->cK * P->cK; break;
+    case 4: P->cK = 1.0 / (ell * ell); P->cP = 2.0 * M_PI / s->period; P->d2psi0 = -P->cK * P->cP * P->cP; break;
     default: P->cK = 1.0 / (ell * ell); P->d2psi0 = -P->cK; break;
   }
   P->psi0 = 1.0;
@@ -332,6 +334,7 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
               P->gcert_mu = 1.01 * P->cK * (s / 3.0) * (1.0 + s) * std::exp(-s); break; }
     case 1: P->gcert_mu = 1.01 * P->cK * std::exp(-1.0); break;
     case 2: P->gcert_mu = 1.01 * P->cK; break;
+    case 4: P->gcert_mu = 1.01 * P->cK * P->cP; break;   // |ψ'| = ψ (2π/(pℓ²)) |sin t| ≤ 2π/(pℓ²)
     default: P->gcert_mu = 1.01 * std::sqrt(P->cK) * std::exp(-0.5); break;
   }
   P->gcert_sig = (P->d2psi0 < 0.0) ? 1.01 * std::sqrt(P->psi0 * -P->d2psi0) : -1.0;
@@ -582,7 +585,8 @@ int mrbo_gp_fit(const mrbo_surrogate_t* s, int32_t np, const double* ells, doubl
   const int d = s->d, N = s->N;
   if (d < 1 || N < 1 || !s->X || !s->y) return fail(MRBO_ERR_ARG, "bad surrogate (d=%d N=%d)", d, N);
   if (N > 256) return fail(MRBO_ERR_UNSUPPORTED, "N=%d > 256", N);
-  if (s->kernel < 0 || s->kernel > 3) return fail(MRBO_ERR_ARG, "kernel id %d", s->kernel);
+  // the Periodic kernel has two hyperparameters: ∂/∂ℓ alone is not its ∇log_likelihood
+  if (s->kernel < 0 || s->kernel > 3) return fail(MRBO_ERR_UNSUPPORTED, "gp_fit: kernel id %d", s->kernel);
   hipStream_t st = (hipStream_t)stream;
   const size_t P = (size_t)np, NN = (size_t)N * N;
   Stage sg;

@@ -38,7 +38,7 @@ struct KParams {
   int d, N, Npad, h, M, R, nstarts;
   int kernel;
   int rule;             // mrbo_rule_t: EI, POI, LCB
-  double ell, cK, psi0, d2psi0, sn2;
+  double ell, cK, cP, psi0, d2psi0, sn2;   // cP: Periodic 2π/p
   double fmin_base, fmini, theta;
   // gradient certificate (newton_grad_certified): max_ρ |ψ'(ρ)| and √(ψ(0)·(−ψ''(0))), the
   // latter ≤ 0 when the derivative process has no finite variance (Matérn-1/2: disabled)
@@ -196,7 +196,8 @@ __device__ __attribute__((noinline)) double xerfc(double x) { return erfc(x); }
 // ---- radial kernels (radial_basis_functions.jl:60-96; derivatives in closed form) -------
 struct Radial {
   int kind;
-  double cK;   // √5/ℓ, √3/ℓ, 1/ℓ  (Matérn) ; 1/ℓ² (SE)
+  double cK;   // √5/ℓ, √3/ℓ, 1/ℓ  (Matérn) ; 1/ℓ² (SE, Periodic)
+  double cP;   // Periodic: 2π/p
 };
 
 // ψ(ρ), g1 = ψ'(ρ)/ρ and g2 = (ψ''(ρ) − ψ'(ρ)/ρ)/ρ² from ρ², so that
@@ -206,6 +207,25 @@ struct Radial {
 // reference's ρ = 0 branches (∇k = 0, ∇²k = ψ''(0)·I).
 __device__ __forceinline__ void rad_eval(const Radial& k, double rho2, double& psi, double& g1, double& g2) {
   const double c = k.cK;
+  if (k.kind == 4) {
+    // Periodic (:98-103) ψ = exp(−2 sin²(πρ/p)/ℓ²).  With B = 2π/p, A = B/ℓ², t = Bρ:
+    //   g1 = ψ'/ρ = −ψ A B sinc t,   g2 = ψ B² (A² sinc²t + A B (sinc t − cos t)/t²)
+    // (sinc t − cos t)/t² = (sin t − t cos t)/t³ by its series below t = 0.1 (cancellation)
+    const double B = k.cP, A = B * c;
+    const double rho = sqrt(rho2), t = B * rho;
+    double su, cu;
+    sincos(0.5 * t, &su, &cu);
+    psi = xexp(-2.0 * su * su * c);
+    const double st = 2.0 * su * cu, ct = fma(-2.0 * su, su, 1.0);
+    const double t2 = t * t;
+    const bool small = t < 0.1;
+    const double sinc = small ? fma(t2, fma(t2, 1.0 / 120.0, -1.0 / 6.0), 1.0) : st / t;
+    const double f = small ? fma(t2, fma(t2, fma(t2, -1.0 / 45360.0, 1.0 / 840.0), -1.0 / 30.0), 1.0 / 3.0)
+                           : (st - t * ct) / (t2 * t);
+    g1 = -psi * A * B * sinc;
+    g2 = psi * B * B * A * fma(A, sinc * sinc, B * f);
+    return;
+  }
   if (k.kind == 3) {
     const double e = xexp(-0.5 * c * rho2);
     psi = e;

@@ -1151,6 +1151,7 @@ __device__ __forceinline__ void stage_start_tables(const KParams& kp, double* sm
   Radial rad;
   rad.kind = kp.kernel;
   rad.cK = kp.cK;
+  rad.cP = kp.cP;
   for (int q = threadIdx.x; q < NR * ns; q += blockDim.x) {
     const int i = q / ns, k = q - (q / ns) * ns;
     double v = 0.0;
@@ -1805,6 +1806,7 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
   W.Npad = kp.Npad;
   W.rad.kind = kp.kernel;
   W.rad.cK = kp.cK;
+  W.rad.cP = kp.cP;
 #pragma unroll
   for (int s = 0; s < RPL; ++s) {
     const int i = W.lane + WAVE * s;

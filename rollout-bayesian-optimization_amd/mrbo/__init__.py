@@ -1,8 +1,8 @@
 """mrbo -- MI355X-native rollout-acquisition evaluator (host mirror of the reference API).
 
 Reference API surface kept (DarianNwankwo/Rollout-Bayesian-Optimization):
-  kernels            Matern52/32/12, SquaredExponential        radial_basis_functions.jl
-  decision rules     EI (compiled), POI/LCB/Random (declared)  decision_rules.jl
+  kernels            Matern52/32/12, SquaredExponential, Periodic  radial_basis_functions.jl
+  decision rules     EI, POI, LCB (compiled), Random (declared)  decision_rules.jl
   surrogates         Surrogate, FantasySurrogate               radial_basis_surrogates.jl
   trajectories       Trajectory, TrajectoryParameters, ExpectedTrajectoryOutput  trajectory.jl
   rollout            simulate_trajectory_mc                    rollout.jl:279-340
@@ -11,7 +11,7 @@ Reference API surface kept (DarianNwankwo/Rollout-Bayesian-Optimization):
 Compute runs in libmrbo.so (hand-written HIP for gfx950); see include/mrbo.h.
 """
 from .decision_rules import EI, LCB, POI, DecisionRule, RandomAcquisition, get_name
-from .kernels import Matern12, Matern32, Matern52, SquaredExponential, eval_KxX, eval_KXX
+from .kernels import Matern12, Matern32, Matern52, Periodic, SquaredExponential, eval_KxX, eval_KXX
 from .mle import grad_log_likelihood, gp_fit_batch, log_likelihood, optimize
 from .optimizers import Adam, StandardSGA, update
 from .rollout import (simulate_trajectory_ghq, simulate_trajectory_ghq_batch, simulate_trajectory_mc,

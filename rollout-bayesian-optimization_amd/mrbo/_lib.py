@@ -38,7 +38,7 @@ EXPORTS = [
 class SurrogateDesc(ctypes.Structure):
     _fields_ = [("d", ctypes.c_int32), ("N", ctypes.c_int32), ("kernel", ctypes.c_int32),
                 ("lengthscale", ctypes.c_double), ("sigma_n2", ctypes.c_double), ("fmini", ctypes.c_double),
-                ("X", _dp), ("L", _dp), ("ldL", ctypes.c_int32), ("c", _dp), ("y", _dp)]
+                ("X", _dp), ("L", _dp), ("ldL", ctypes.c_int32), ("c", _dp), ("y", _dp), ("period", ctypes.c_double)]
 
 
 class ParamsDesc(ctypes.Structure):
@@ -64,6 +64,13 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise MrboError(f"libmrbo.so not built at {LIB_PATH}: run __graft_entry__.build()")
+    # torch ships its own libamdhip64.so.7 (same SONAME as /opt/rocm's): whichever loads first
+    # serves the whole process, and torch cannot initialise on the other one.  Load torch's
+    # first so that the process has one HIP runtime shared by torch and libmrbo.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     L.mrbo_version.restype = ctypes.c_char_p
     L.mrbo_last_error.restype = ctypes.c_char_p

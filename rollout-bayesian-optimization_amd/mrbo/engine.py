@@ -40,7 +40,7 @@ class RolloutPlan:
     """Device state for (surrogate, trajectory parameters)."""
 
     def __init__(self, X, L, c, y, kernel, lengthscale, sigma_n2, fmini, h, M, R, nstarts, lbs, ubs, theta,
-                 device=0, **opts):
+                 device=0, period=1.0, **opts):
         self.lib = _lib.load()
         o = dict(DEFAULTS)
         o.update(opts)
@@ -54,7 +54,7 @@ class RolloutPlan:
         dp = ctypes.POINTER(ctypes.c_double)
         sd = _lib.SurrogateDesc(self.d, self.N, int(kernel), float(lengthscale), float(sigma_n2), float(fmini),
                                 self._X.ctypes.data_as(dp), self._L.ctypes.data_as(dp), self.N,
-                                self._c.ctypes.data_as(dp), self._y.ctypes.data_as(dp))
+                                self._c.ctypes.data_as(dp), self._y.ctypes.data_as(dp), float(period))
         pd = _lib.ParamsDesc(self.h, self.M, self.R, self.nstarts, int(o.get("rule", 0)), self.theta,
                              self._lbs.ctypes.data_as(dp),
                              self._ubs.ctypes.data_as(dp), int(o["max_iters"]), int(o["max_ls"]), float(o["x_tol"]),

@@ -6,7 +6,7 @@ on the rollout path runs in libmrbo.so; the kernel id selects the same closed fo
 """
 import numpy as np
 
-MATERN52, MATERN32, MATERN12, SE = 0, 1, 2, 3
+MATERN52, MATERN32, MATERN12, SE, PERIODIC = 0, 1, 2, 3, 4
 
 
 class RadialBasisFunction:
@@ -22,13 +22,27 @@ class RadialBasisFunction:
     def lengthscale(self):
         return float(self.θ[0])
 
+    @property
+    def period(self):
+        """θ[2] of the Periodic kernel (1.0 for the one-parameter kernels)."""
+        return float(self.θ[1]) if self.kind == PERIODIC else 1.0
+
+    def _per(self):
+        # Periodic: A = 2π/(pℓ²), B = 2π/p; ψ = exp(−2 sin²(πρ/p)/ℓ²), ψ' = −ψ A sin(Bρ),
+        # ψ'' = ψ (A² sin²(Bρ) − A B cos(Bρ))
+        l, p = self.θ
+        return 2 * np.pi / (p * l * l), 2 * np.pi / p
+
     def _c(self):
         l = self.lengthscale
-        return {MATERN52: np.sqrt(5.0) / l, MATERN32: np.sqrt(3.0) / l, MATERN12: 1.0 / l, SE: 1.0 / (l * l)}[self.kind]
+        return {MATERN52: np.sqrt(5.0) / l, MATERN32: np.sqrt(3.0) / l, MATERN12: 1.0 / l, SE: 1.0 / (l * l),
+                PERIODIC: 1.0 / (l * l)}[self.kind]
 
     def __call__(self, rho):
         rho = np.asarray(rho, dtype=np.float64)
         c = self._c()
+        if self.kind == PERIODIC:
+            return np.exp(-2 * np.sin(np.pi * rho / self.θ[1]) ** 2 * c)
         if self.kind == MATERN52:
             s = c * rho
             return (1 + s * (1 + s / 3.0)) * np.exp(-s)
@@ -42,6 +56,9 @@ class RadialBasisFunction:
     def derivative(self, rho):
         rho = np.asarray(rho, dtype=np.float64)
         c = self._c()
+        if self.kind == PERIODIC:
+            A, B = self._per()
+            return -self(rho) * A * np.sin(B * rho)
         if self.kind == MATERN52:
             s = c * rho
             return -c * (s / 3.0) * (1 + s) * np.exp(-s)
@@ -55,6 +72,9 @@ class RadialBasisFunction:
     def second_derivative(self, rho):
         rho = np.asarray(rho, dtype=np.float64)
         c = self._c()
+        if self.kind == PERIODIC:
+            A, B = self._per()
+            return self(rho) * (A * A * np.sin(B * rho) ** 2 - A * B * np.cos(B * rho))
         if self.kind == MATERN52:
             s = c * rho
             return c * c * (s * s - s - 1) * np.exp(-s) / 3.0
@@ -83,6 +103,11 @@ def Matern12(θ=(1.0,)):
 
 def SquaredExponential(θ=(1.0,)):
     return RadialBasisFunction("SquaredExponential", SE, θ)
+
+
+def Periodic(θ=(1.0, 1.0)):
+    """radial_basis_functions.jl:98-103: θ = [ℓ, p]."""
+    return RadialBasisFunction("Periodic", PERIODIC, θ)
 
 
 def get_hyperparameters(k):

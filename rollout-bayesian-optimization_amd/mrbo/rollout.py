@@ -26,7 +26,7 @@ def _plan_for(s, h, M, R, nstarts, lbs, ubs, theta, device, opts):
     if p is None:
         n = s.observed
         p = RolloutPlan(s.X[:, :n], s.L[:n, :n], s.c[:n], s.y[:n], s.ψ.kind, s.ψ.lengthscale, s.σn2, s.fmini(),
-                        h, M, R, nstarts, lbs, ubs, theta, device=device, **opts)
+                        h, M, R, nstarts, lbs, ubs, theta, device=device, period=s.ψ.period, **opts)
         if len(_PLANS) > 16:
             _PLANS.clear()
         _PLANS[key] = p

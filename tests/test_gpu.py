@@ -24,7 +24,8 @@ def _plan(g, M=None, R=None, h=None, nstarts=None, kernel=0, theta=0.0, **opts):
     R = R or g["x0s"].shape[1]
     h = int(g["h"]) if h is None else h
     return RolloutPlan(g["X"], g["L"], g["c"], g["y"], kernel, float(g.get("ell", 1.0)), 1e-6, float(g["fmini"]), h, M, R,
-                       nstarts or g["xstarts"].shape[1], g["lbs"], g["ubs"], theta, **opts)
+                       nstarts or g["xstarts"].shape[1], g["lbs"], g["ubs"], theta, period=g.get("period", 1.0),
+                       **opts)
 
 
 def _run(plan, g, dual=None, replay=None, want_policy=True, with_gradient=True, rn=None, x0s=None):
@@ -53,7 +54,7 @@ def _run(plan, g, dual=None, replay=None, want_policy=True, with_gradient=True, 
 
 def _osur(oracle, g, kernel="matern52"):
     return oracle.OracleSurrogate(g["X"], g["L"], g["c"], g["y"], kernel=kernel, ell=float(g.get("ell", 1.0)),
-                                  fmini=float(g["fmini"]))
+                                  fmini=float(g["fmini"]), period=float(g.get("period", 1.0)))
 
 
 def _assert_grads_close(a, b, rtol=1e-6):
@@ -83,7 +84,7 @@ def test_replay_vs_golden(gpu, case):
 
 def _problem_arrays(name, M, R, kernel=None, testfn=None, d=None, N=None, h=None, ell=None):
     from mrbo import configs
-    from mrbo.kernels import Matern12, Matern32, Matern52, SquaredExponential
+    from mrbo.kernels import Matern12, Matern32, Matern52, Periodic, SquaredExponential
     if testfn is not None:
         cfg = configs.Config(f"T{testfn}{d}", testfn, d, h, M, R, N, 1)
         pb = configs.Problem(cfg)
@@ -91,13 +92,16 @@ def _problem_arrays(name, M, R, kernel=None, testfn=None, d=None, N=None, h=None
         pb = configs.problem(name, M=M, R=R)
     s = pb.surrogate
     if kernel is not None:
-        s.set_kernel({"matern32": Matern32(), "matern12": Matern12(), "se": SquaredExponential()}[kernel])
+        # Periodic: a period beyond twice the box diagonal (Branin: 21) and an effective
+        # lengthscale ℓp/2π ≈ 1 below the design spacing keep K well conditioned
+        s.set_kernel({"matern32": Matern32(), "matern12": Matern12(), "se": SquaredExponential(),
+                      "periodic": Periodic([0.125, 50.0])}[kernel])
     if ell is not None:
         s.set_kernel(Matern52([ell]))
     n = s.observed
     return dict(X=s.X[:, :n], L=s.L[:n, :n], c=s.c[:n], y=s.y[:n], fmini=s.fmini(), lbs=pb.lbs, ubs=pb.ubs,
                 x0s=pb.x0s, rnstream=pb.tp.rnstream_sequence, xstarts=pb.es.get_starts(), h=pb.cfg.h,
-                ell=1.0 if ell is None else ell)
+                ell=s.ψ.lengthscale, period=s.ψ.period)
 
 
 @pytest.mark.parametrize("name,M,R,ell", [("C1", 32, 4, None), ("C2", 32, 4, None), ("C3", 32, 4, None),
@@ -191,10 +195,14 @@ def test_ghq_vs_oracle(gpu, oracle):
     _assert_grads_close(r["grad_x"][:, ok], o2["grad_x"][:, ok], rtol=1e-5)
 
 
-@pytest.mark.parametrize("kernel,kid", [("matern32", 1), ("matern12", 2), ("se", 3)])
+@pytest.mark.parametrize("kernel,kid", [("matern32", 1), ("matern12", 2), ("se", 3), ("periodic", 4)])
 def test_other_kernels_replay_vs_oracle(gpu, oracle, kernel, kid):
     g = _problem_arrays("C2", 16, 2, kernel=kernel)
-    r = _run(_plan(g, kernel=kid), g)
+    p = _plan(g, kernel=kid)
+    pts = np.asfortranarray(g["xstarts"][:, :8] * 0.9 + 0.05 * g["x0s"][:, :1])
+    np.testing.assert_allclose(p.eval_base(pts), oracle.eval_base(_osur(oracle, g, kernel), pts), rtol=1e-9,
+                               atol=1e-12)
+    r = _run(p, g)
     rp = np.asfortranarray(r["policy_x"][:, 1:])
     o = oracle.simulate_mc(_osur(oracle, g, kernel), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"],
                            int(g["h"]), replay_x=rp, nthreads=8)

@@ -210,3 +210,33 @@ def test_generate_indices_order():
     from mrbo.utils import generate_indices
     ix = generate_indices(3, 2)
     assert ix[:4] == [(0, 0), (1, 0), (2, 0), (0, 1)] and len(ix) == 9
+
+
+@pytest.mark.parametrize("name", ["Matern52", "Matern32", "Matern12", "SquaredExponential", "Periodic"])
+def test_host_kernel_derivatives_fd(name):
+    """ψ', ψ'' of every kernel (radial_basis_functions.jl:60-103; ForwardDiff there) by central FD."""
+    from mrbo import kernels
+    k = getattr(kernels, name)([0.7, 1.3] if name == "Periodic" else [0.7])
+    rho = np.array([0.05, 0.3, 0.9, 1.7, 2.6])
+    h = 1e-5
+    np.testing.assert_allclose(k.derivative(rho), (k(rho + h) - k(rho - h)) / (2 * h), rtol=1e-7, atol=1e-10)
+    np.testing.assert_allclose(k.second_derivative(rho), (k.derivative(rho + h) - k.derivative(rho - h)) / (2 * h),
+                               rtol=1e-6, atol=1e-9)
+
+
+def test_eval_base_periodic_fd(oracle):
+    """Posterior μ, σ and ∇α of a Periodic-kernel surrogate (oracle) against FD."""
+    from mrbo.kernels import Periodic
+    from mrbo.surrogates import Surrogate
+    rng = np.random.default_rng(5)
+    X = rng.random((2, 12)) * 3
+    y = np.sin(X.sum(0))
+    s = Surrogate(Periodic([1.2, 4.0]), X, y, capacity=12)
+    os_ = oracle.OracleSurrogate(X, s.L, s.c, y, kernel="periodic", ell=1.2, period=4.0)
+    col = lambda xx: oracle.eval_base(os_, xx.reshape(-1, 1))[:, 0]
+    x = np.array([1.1, 1.7])
+    o = col(x)
+    d = 2
+    np.testing.assert_allclose(o[3:3 + d], _fd(lambda xx: col(xx)[0], x), rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(o[3 + d:3 + 2 * d], _fd(lambda xx: col(xx)[1], x), rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(o[3 + 2 * d:3 + 3 * d], _fd(lambda xx: col(xx)[2], x), rtol=1e-6, atol=1e-10)
