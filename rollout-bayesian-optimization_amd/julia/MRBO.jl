@@ -9,7 +9,7 @@
 # Python ctypes harness (rollout-bayesian-optimization_amd/mrbo/_lib.py) and tests/test_gpu.py.
 module MRBO
 
-export MrboBackend, MrboPlan, mrbo_simulate!
+export MrboBackend, MrboPlan, mrbo_simulate!, mrbo_log_likelihood
 
 const libmrbo = joinpath(@__DIR__, "..", "mrbo", "libmrbo.so")
 const MRBO_FLAG_HOST_POINTERS = UInt32(1)
@@ -28,6 +28,7 @@ struct MrboSurrogateC
     ldL::Int32
     c::Ptr{Float64}
     y::Ptr{Float64}
+    period::Float64      # Periodic θ[2]
 end
 
 # mirrors mrbo_params_t
@@ -67,7 +68,8 @@ end
 
 kernel_id(ψ) = ψ.constructor === Matern52 ? 0 : ψ.constructor === Matern32 ? 1 :
                ψ.constructor === Matern12 ? 2 : ψ.constructor === SquaredExponential ? 3 :
-               error("kernel not compiled into libmrbo")
+               ψ.constructor === Periodic ? 4 : error("kernel not compiled into libmrbo")
+kernel_period(ψ) = ψ.constructor === Periodic ? ψ.θ[2] : 1.0
 
 function check(rc)
     rc == 0 && return
@@ -89,7 +91,7 @@ function MrboPlan(s::Surrogate, tp::TrajectoryParameters, θ::Vector{Float64}, n
     lbs, ubs = get_spatial_bounds(tp)
     GC.@preserve X L c y lbs ubs begin
         sd = MrboSurrogateC(size(X, 1), N, kernel_id(get_kernel(s)), get_kernel(s).θ[1], s.σn2, fmini,
-                            pointer(X), pointer(L), N, pointer(c), pointer(y))
+                            pointer(X), pointer(L), N, pointer(c), pointer(y), kernel_period(get_kernel(s)))
         pd = MrboParamsC(tp.horizon, M, 1, nstarts, rule_id(get_decision_rule(s)), θ[1], pointer(lbs), pointer(ubs),
                          max_iters, max_ls, 1e-3, 1e-3, 1e-8, 1e-4, 1e-8, seed, 0, 0)
         h = Ref{Ptr{Cvoid}}(C_NULL)
@@ -170,6 +172,29 @@ function simulate_trajectory_ghq(T::Trajectory, tp::TrajectoryParameters, backen
     ∇μθ = vec(Distributions.mean(hyperparameter_gradients_container, dims=2))
     σ_∇μθ = vec(Distributions.std(hyperparameter_gradients_container, dims=2, mean=∇μθ))
     return ExpectedTrajectoryOutput(μxθ=μxθ, σ_μxθ=σ_μxθ, ∇μx=∇μx, σ_∇μx=σ_∇μx, ∇μθ=∇μθ, σ_∇μθ=σ_∇μθ)
+end
+
+
+# log_likelihood / ∇log_likelihood (radial_basis_surrogates.jl:770-799) of `s` refit at each
+# lengthscale in `ells` on the GPU (mrbo_gp_fit; host arrays, staged by the library).  Returns
+# (ll, dll, status) vectors; status 1 marks a PosDefException.  An `optimize!` method can call it
+# from its fg! closure (one launch evaluates every trial lengthscale of a line search).
+function mrbo_log_likelihood(s::Surrogate, ells::Vector{Float64})
+    N = get_observed(s)
+    X = Matrix(get_active_covariates(s))
+    y = Vector(get_active_observations(s))
+    P = length(ells)
+    ll, dll, st = zeros(P), zeros(P), zeros(Int32, P)
+    GC.@preserve X y ells ll dll st begin
+        sd = MrboSurrogateC(size(X, 1), N, kernel_id(get_kernel(s)), get_kernel(s).θ[1], s.σn2,
+                            minimum(get_observations(s)), pointer(X), C_NULL, N, C_NULL, pointer(y),
+                            kernel_period(get_kernel(s)))
+        check(ccall((:mrbo_gp_fit, libmrbo), Cint,
+                    (Ref{MrboSurrogateC}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32},
+                     Ptr{Float64}, Ptr{Float64}, UInt32, Ptr{Cvoid}),
+                    sd, P, ells, ll, dll, st, C_NULL, C_NULL, MRBO_FLAG_HOST_POINTERS, C_NULL))
+    end
+    return ll, dll, st
 end
 
 end # module
