@@ -72,8 +72,9 @@ namespace {
 
 // ---- kernel dispatch: one translation unit per input dimension (mrbo_kernels.hip) -------
 bool get_kset(int d, int rpl, KernelSet& ks) {
-#define CASE(DD) \
+#define CASE_(DD) \
   case DD: return kset_d##DD(rpl, ks);
+#define CASE(DD) CASE_(DD)
   switch (d) {
 #ifdef MRBO_ONLY_D
     CASE(MRBO_ONLY_D)
@@ -83,27 +84,32 @@ bool get_kset(int d, int rpl, KernelSet& ks) {
     default: return false;
   }
 #undef CASE
+#undef CASE_
 }
 
 void launch_rollout(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
-#define CASE(DD) \
+#define CASE_(DD) \
   case DD: launch_rollout_d##DD(rpl, g, b, sm, st, kp); break;
+#define CASE(DD) CASE_(DD)
 #ifdef MRBO_ONLY_D
   switch (d) { CASE(MRBO_ONLY_D) }
 #else
   switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) }
 #endif
 #undef CASE
+#undef CASE_
 }
 void launch_evalb(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
-#define CASE(DD) \
+#define CASE_(DD) \
   case DD: launch_evalb_d##DD(rpl, g, b, sm, st, kp); break;
+#define CASE(DD) CASE_(DD)
 #ifdef MRBO_ONLY_D
   switch (d) { CASE(MRBO_ONLY_D) }
 #else
   switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) }
 #endif
 #undef CASE
+#undef CASE_
 }
 
 // choose waves per workgroup maximising resident waves per CU (LDS + register limits)

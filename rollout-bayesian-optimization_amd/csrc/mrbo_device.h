@@ -185,9 +185,52 @@ __device__ __forceinline__ void wave_reduce(double (&v)[K], double* red, int lan
 // The fp64 exp/erfc expansions carry tens of 64-bit polynomial constants; inlined into the
 // Newton/horizon loops, LICM hoists their materialisation out of the loops and the kernel
 // spills them.  As leaf calls the constants stay local to the callee.
+// 64-bit constant materialised in an SGPR pair at its point of use: the volatile moves cannot be
+// hoisted out of loops, so polynomial coefficients never occupy registers across the Newton /
+// horizon loops (two SALU moves per use, issued beside the VALU stream)
+template <unsigned LO, unsigned HI>
+__device__ __forceinline__ double sconst() {
+  int lo, hi;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "i"(LO));
+  asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "i"(HI));
+  return djoin(lo, hi);
+}
+
+// exp(x), inlined: the device library's algorithm and coefficients in the same operation order
+// (Cody–Waite reduction by ln2, degree-11 polynomial, 2^k by v_ldexp_f64, overflow / underflow
+// selects), so results are bit-identical to exp() -- without a call's prologue (scratch save of
+// a VGPR and a full s_waitcnt on entry) or VALU moves for the coefficients.
+__device__ __forceinline__ double fexp(double x) {
+  const double k = __builtin_rint(x * sconst<0x652b82feu, 0x3ff71547u>());            // x·log2(e)
+  double r = fma(sconst<0xfefa39efu, 0xbfe62e42u>(), k, x);                          // − k·ln2_hi
+  r = fma(sconst<0x3b39803fu, 0xbc7abc9eu>(), k, r);                                 // − k·ln2_lo
+  double c10 = sconst<0xfca7ab0cu, 0x3e928af3u>();
+  asm volatile("" : "+v"(c10));   // one of the first step's two constants must live in VGPRs
+  double p = fma(sconst<0x6a5dcb37u, 0x3e5ade15u>(), r, c10);
+  p = fma(r, p, sconst<0x623fde64u, 0x3ec71deeu>());
+  p = fma(r, p, sconst<0x7c89e6b0u, 0x3efa0199u>());
+  p = fma(r, p, sconst<0x14761f6eu, 0x3f2a01a0u>());
+  p = fma(r, p, sconst<0x1852b7b0u, 0x3f56c16cu>());
+  p = fma(r, p, sconst<0x11122322u, 0x3f811111u>());
+  p = fma(r, p, sconst<0x555502a1u, 0x3fa55555u>());
+  p = fma(r, p, sconst<0x55555511u, 0x3fc55555u>());
+  p = fma(r, p, sconst<0x0000000bu, 0x3fe00000u>());
+  p = fma(r, p, 1.0);
+  p = fma(r, p, 1.0);
+  double e = __builtin_ldexp(p, (int)k);
+  e = (x > sconst<0u, 0x40900000u>()) ? __builtin_inf() : e;   // x > 1024
+  e = (x < sconst<0u, 0xc090cc00u>()) ? 0.0 : e;               // x < −1075
+  return e;
+}
+
+// Default: leaf calls.  MRBO_FEXP inlines fexp instead (A/B on C3: no gain -- the calls' latency
+// is hidden by the second wave, and inlining raised VGPR spills 66 → 93).
 #ifdef MRBO_INLINE_TRANSCENDENTALS
 __device__ __forceinline__ double xexp(double x) { return exp(x); }
 __device__ __forceinline__ double xerfc(double x) { return erfc(x); }
+#elif defined(MRBO_FEXP)
+__device__ __forceinline__ double xexp(double x) { return fexp(x); }
+__device__ __attribute__((noinline)) double xerfc(double x) { return erfc(x); }
 #else
 __device__ __attribute__((noinline)) double xexp(double x) { return exp(x); }
 __device__ __attribute__((noinline)) double xerfc(double x) { return erfc(x); }
