@@ -270,11 +270,27 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   if (mode != EV_BACK) {
   // ---- 1. kernel rows B[i] = [k(x,X_i), ∇k(x - X_i)]  (eval_KxX :180-191, eval_∇KxX :193-208)
   double Bown[RPL][D1];
+  // GRADC follows the VALUE evaluation at the same x: its g1 (G12), fantasy rows (B) and
+  // fantasy Hessian terms (U_HF) are still in LDS, so no radial function is re-evaluated
+  const bool rows_kept = (mode == EV_GRADC);
 #pragma unroll
   for (int s = 0; s < RPL; ++s) {
     double r[D], rho2 = 0.0;
 #pragma unroll
     for (int a = 0; a < D; ++a) { r[a] = x[a] - W.X0[s][a]; rho2 = fma(r[a], r[a], rho2); }
+    if (rows_kept) {
+      const double g1 = W.G12[3 * (lane + WAVE * s)];
+      const bool v = W.valid[s];
+      Bown[s][0] = 0.0;   // column 0 comes from the VALUE pass
+#pragma unroll
+      for (int a = 0; a < D; ++a) Bown[s][1 + a] = v ? g1 * r[a] : 0.0;
+      if constexpr (!Ly::SQ) {
+        double* row = B + (lane + WAVE * s) * BS;
+#pragma unroll
+        for (int a = 0; a < D; ++a) row[1 + a] = Bown[s][1 + a];
+      }
+      continue;
+    }
     double psi, g1, g2;
     rad_eval(W.rad, rho2, psi, g1, g2);
     const bool v = W.valid[s];
@@ -293,7 +309,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       }
     }
   }
-  if (lane < nf) {  // fantasy rows B[N + r]; [x − X_r, g1, g2] kept for the Hessian
+  if (lane < nf && !rows_kept) {  // fantasy rows B[N + r]; [x − X_r, g1, g2] kept for the Hessian
     double r[D], rho2 = 0.0;
 #pragma unroll
     for (int a = 0; a < D; ++a) { r[a] = x[a] - U[Ly::U_XF + lane * D + a]; rho2 = fma(r[a], r[a], rho2); }
