@@ -270,6 +270,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   if (mode != EV_BACK) {
   // ---- 1. kernel rows B[i] = [k(x,X_i), ∇k(x - X_i)]  (eval_KxX :180-191, eval_∇KxX :193-208)
   double Bown[RPL][D1];
+  double rf[D], psif = 0.0, g1f = 0.0, g2f = 0.0;   // fantasy row of this lane (paired radial evaluation)
   // GRADC follows the VALUE evaluation at the same x: its g1 (G12), fantasy rows (B) and
   // fantasy Hessian terms (U_HF) are still in LDS, so no radial function is re-evaluated
   const bool rows_kept = (mode == EV_GRADC);
@@ -292,6 +293,16 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       continue;
     }
     double psi, g1, g2;
+#ifndef MRBO_NO_PAIRED_RAD
+    if constexpr (RPL == 1) {
+      // this lane's fantasy row (lanes < nf) shares the radial evaluation of its base row
+      const int fl = lane < nf ? lane : 0;
+      double rho2f = 0.0;
+#pragma unroll
+      for (int a = 0; a < D; ++a) { rf[a] = x[a] - U[Ly::U_XF + fl * D + a]; rho2f = fma(rf[a], rf[a], rho2f); }
+      rad_eval2(W.rad, rho2, rho2f, psi, g1, g2, psif, g1f, g2f);
+    } else
+#endif
     rad_eval(W.rad, rho2, psi, g1, g2);
     const bool v = W.valid[s];
     Bown[s][0] = v ? psi : 0.0;
@@ -310,11 +321,22 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     }
   }
   if (lane < nf && !rows_kept) {  // fantasy rows B[N + r]; [x − X_r, g1, g2] kept for the Hessian
-    double r[D], rho2 = 0.0;
+    double r[D], psi, g1, g2;
+#ifndef MRBO_NO_PAIRED_RAD
+    if constexpr (RPL == 1) {
 #pragma unroll
-    for (int a = 0; a < D; ++a) { r[a] = x[a] - U[Ly::U_XF + lane * D + a]; rho2 = fma(r[a], r[a], rho2); }
-    double psi, g1, g2;
-    rad_eval(W.rad, rho2, psi, g1, g2);
+      for (int a = 0; a < D; ++a) r[a] = rf[a];
+      psi = psif;
+      g1 = g1f;
+      g2 = g2f;
+    } else
+#endif
+    {
+      double rho2 = 0.0;
+#pragma unroll
+      for (int a = 0; a < D; ++a) { r[a] = x[a] - U[Ly::U_XF + lane * D + a]; rho2 = fma(r[a], r[a], rho2); }
+      rad_eval(W.rad, rho2, psi, g1, g2);
+    }
     double* row = B + (Ly::FR0 + lane) * BS;
     row[0] = psi;
 #pragma unroll
@@ -829,6 +851,11 @@ __device__ __forceinline__ int draw(WaveCtx<D, RPL>& W, const KParams& kp, const
   using Ly = Lay<D, RPL>;
   constexpr int D1 = Ly::D1;
   const double* U = W.U;
+#ifdef MRBO_EXP_STUB_DRAW
+  yv = U[Ly::U_SC + SC_MU] + z[0];
+  for (int a = 0; a < D; ++a) gy[a] = U[Ly::U_GMU + a] + z[1 + a];
+  return 0;
+#endif
   double Lc[D1 * (D1 + 1) / 2];
 #define TRI(i, j) ((i) * ((i) + 1) / 2 + (j))
 #pragma unroll
@@ -1245,8 +1272,19 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   const double* U = W.U;
   const int lane = W.ln();
   const int ns = kp.nstarts, nf = S + 1;
+#ifndef MRBO_NO_BATCH_SPLIT
+  // ns ≤ 32: both half-waves take every start (lane k and k + 32); the lower half sums the
+  // even data rows, the upper half the odd ones, one permlane32 swap per value adds the halves,
+  // and each half evaluates every other fantasy radial function.  Both halves then hold the
+  // same per-start values; the ballots below read the lower half.
+  const bool split = ns <= 32;
+#else
+  const bool split = false;
+#endif
+  const int kl = split ? (lane & 31) : lane;
+  const int hf = split ? (lane >> 5) : 0;
   const bool act = lane < ns;
-  const int k = act ? lane : 0;
+  const int k = kl < ns ? kl : 0;
   double x[D];
 #pragma unroll
   for (int a = 0; a < D; ++a) x[a] = clampd(W.XS[k * D + a], U[Ly::U_LB + a], U[Ly::U_UB + a]);
@@ -1255,24 +1293,63 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   for (int r = 0; r < FMAX; ++r) ae[r] = 0.0;
   const double* cS = W.C + (long long)(S + 1) * NR;
   // all FMAX rows unconditionally (rows ≥ nf hold finite stale values, masked below): a load
-  // under a condition would become a branch with a full LDS round trip per row
+  // under a condition would become a branch with a full LDS round trip per row.  Rows N..NR-1
+  // of the tables are zero.
+  if (split) {
 #pragma unroll 8
-  for (int i = 0; i < W.N; ++i) {
-    const double kv = W.KXB[i * ns + k];
-    amu = fma(cS[i], kv, amu);
+    for (int j = 0; j < NR / 2; ++j) {
+      const int i = 2 * j + hf;
+      const double kv = W.KXB[i * ns + k];
+      amu = fma(cS[i], kv, amu);
 #pragma unroll
-    for (int r = 0; r < FMAX; ++r) ae[r] = fma(W.E[(long long)r * NR + i], kv, ae[r]);
+      for (int r = 0; r < FMAX; ++r) ae[r] = fma(W.E[(long long)r * NR + i], kv, ae[r]);
+    }
+    amu = swap_fold<32>(amu, amu);
+#pragma unroll
+    for (int r = 0; r < FMAX; ++r) ae[r] = swap_fold<32>(ae[r], ae[r]);
+  } else {
+#pragma unroll 8
+    for (int i = 0; i < W.N; ++i) {
+      const double kv = W.KXB[i * ns + k];
+      amu = fma(cS[i], kv, amu);
+#pragma unroll
+      for (int r = 0; r < FMAX; ++r) ae[r] = fma(W.E[(long long)r * NR + i], kv, ae[r]);
+    }
   }
   double pf[FMAX];
+  if (split) {
+    // half h evaluates fantasy points q = 2e + h; one swap hands each half the other's values
 #pragma unroll
-  for (int q = 0; q < FMAX; ++q) {
-    pf[q] = 0.0;
-    if (q < nf) {
-      double rho2 = 0.0;
+    for (int e = 0; e < FMAX / 2; ++e) {
+      const int q = 2 * e + hf;
+      double v = 0.0;
+      if (2 * e < nf) {
+        double rho2 = 0.0;
 #pragma unroll
-      for (int a = 0; a < D; ++a) { const double r = x[a] - U[Ly::U_XF + q * D + a]; rho2 = fma(r, r, rho2); }
-      double g1, g2;
-      rad_eval(W.rad, rho2, pf[q], g1, g2);
+        for (int a = 0; a < D; ++a) { const double r = x[a] - U[Ly::U_XF + q * D + a]; rho2 = fma(r, r, rho2); }
+        double g1, g2;
+        rad_eval(W.rad, rho2, v, g1, g2);
+      }
+      int lo, hi;
+      dsplit(v, lo, hi);
+      const auto l2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+      const auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+      pf[2 * e] = djoin(l2[0], h2[0]);       // lower half's value (q = 2e)
+      pf[2 * e + 1] = djoin(l2[1], h2[1]);   // upper half's value (q = 2e + 1)
+    }
+#pragma unroll
+    for (int q = 0; q < FMAX; ++q) pf[q] = (q < nf) ? pf[q] : 0.0;
+  } else {
+#pragma unroll
+    for (int q = 0; q < FMAX; ++q) {
+      pf[q] = 0.0;
+      if (q < nf) {
+        double rho2 = 0.0;
+#pragma unroll
+        for (int a = 0; a < D; ++a) { const double r = x[a] - U[Ly::U_XF + q * D + a]; rho2 = fma(r, r, rho2); }
+        double g1, g2;
+        rad_eval(W.rad, rho2, pf[q], g1, g2);
+      }
     }
   }
   double g00 = W.GTAB[k * Ly::NG], mu = amu;
