@@ -197,7 +197,7 @@ def main():
                    "N": cfg.N, "d": d, "parallelism": f"mc-shard x{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": f"rollout_kernel<{d},{1 if cfg.N <= 64 else 2 if cfg.N <= 128 else 4}>", "kernel_ms": kms, "flops_per_launch": fl,
+                     "kernel": f"rollout_kernel<{d},{1 if cfg.N <= 64 else 2 if cfg.N <= 128 else 4},1>", "kernel_ms": kms, "flops_per_launch": fl,
                      "note": "compute-bound fp64: peak = the dense fp64 matrix peak, equal to the fp64 vector "
                              "peak on MI355X; the kernel issues VALU v_fma_f64 (matrix-vector work, not "
                              "GEMM-shaped); algorithmic FLOP model in DESIGN.md §5; HBM algorithmic "

@@ -60,6 +60,7 @@ struct mrbo_plan {
   int* dqueue = nullptr;
   int wpg = 4, blocks = 0;
   size_t smem = 0;
+  int spec = 0;             // 1: rollout_kernel<D, RPL, 1> (Matérn-5/2 + EI fixed)
   int xs_lds = 0;           // rollout launches stage xstarts in LDS (≤ 8 KB)
   int batch = 0;            // batched start-point values (start tables in LDS)
   int ewpg = 4, eblocks = 0;
@@ -87,9 +88,9 @@ bool get_kset(int d, int rpl, KernelSet& ks) {
 #undef CASE_
 }
 
-void launch_rollout(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
+void launch_rollout(int d, int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
 #define CASE_(DD) \
-  case DD: launch_rollout_d##DD(rpl, g, b, sm, st, kp); break;
+  case DD: launch_rollout_d##DD(rpl, spec, g, b, sm, st, kp); break;
 #define CASE(DD) CASE_(DD)
 #ifdef MRBO_ONLY_D
   switch (d) { CASE(MRBO_ONLY_D) }
@@ -388,13 +389,18 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   int wpg0 = 0, blocks0 = 0;
   size_t smem0 = 0;
   const int maxw = ks.max_threads / WAVE;
+  // Matérn-5/2 + EI: the compile-time specialised rollout kernel
+  // (MRBO_GENERIC_KERNEL=1 forces the generic instantiation, for A/B runs and tests)
+  const char* gen = getenv("MRBO_GENERIC_KERNEL");
+  P->spec = (P->kernel == MRBO_KERNEL_MATERN52 && P->p.rule == MRBO_RULE_EI && !(gen && gen[0] == '1')) ? 1 : 0;
+  const void* rk = P->spec ? ks.rollout_spec : ks.rollout;
   const int waves0 =
-      pick_grid(ks.rollout, fixed, ks.wave_bytes, prop.multiProcessorCount, wpg0, blocks0, smem0, 0, maxw);
+      pick_grid(rk, fixed, ks.wave_bytes, prop.multiProcessorCount, wpg0, blocks0, smem0, 0, maxw);
   P->batch = 0;
   if (ks.square && P->xs_lds && ns <= 64) {
     int wpg1 = 0, blocks1 = 0;
     size_t smem1 = 0;
-    const int waves1 = pick_grid(ks.rollout, fixed + kxb_bytes, ks.wave_bytes, prop.multiProcessorCount, wpg1, blocks1,
+    const int waves1 = pick_grid(rk, fixed + kxb_bytes, ks.wave_bytes, prop.multiProcessorCount, wpg1, blocks1,
                                  smem1);
     if (waves1 >= waves0 && waves1 > 0) { P->batch = 1; P->wpg = wpg1; P->blocks = blocks1; P->smem = smem1; }
   }
@@ -491,7 +497,7 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
   HIP_TRY(hipEventRecord(P->ev0, st));
   kp.xs_lds = P->xs_lds;
   kp.batch = P->batch;
-  launch_rollout(d, P->RPL, dim3(P->blocks), dim3(P->wpg * WAVE), P->smem, st, kp);
+  launch_rollout(d, P->RPL, P->spec, dim3(P->blocks), dim3(P->wpg * WAVE), P->smem, st, kp);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(P->ev1, st));
   P->timed = true;

@@ -237,6 +237,8 @@ __device__ __attribute__((noinline)) double xerfc(double x) { return erfc(x); }
 #endif
 
 // ---- radial kernels (radial_basis_functions.jl:60-96; derivatives in closed form) -------
+// kind ids = mrbo_kernel_t (include/mrbo.h)
+enum { KERNEL_MATERN52 = 0, KERNEL_MATERN32 = 1, KERNEL_MATERN12 = 2, KERNEL_SE = 3, KERNEL_PERIODIC = 4 };
 struct Radial {
   int kind;
   double cK;   // √5/ℓ, √3/ℓ, 1/ℓ  (Matérn) ; 1/ℓ² (SE, Periodic)

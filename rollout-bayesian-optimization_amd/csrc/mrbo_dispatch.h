@@ -9,7 +9,8 @@ namespace mrbo {
 
 // launch geometry and L0⁻¹ image of one rollout_kernel<D, RPL> / eval_base_kernel<D, RPL> pair
 struct KernelSet {
-  const void* rollout;
+  const void* rollout;      // generic: kernel function and decision rule from KParams
+  const void* rollout_spec; // Matérn-5/2 + EI fixed at compile time (rollout_kernel SPEC = 1)
   const void* evalb;
   size_t wave_bytes;        // per-wave LDS
   bool square;              // L0⁻¹ layout: dense square (ld) or packed triangle
@@ -22,7 +23,7 @@ struct KernelSet {
 
 #define MRBO_DECLARE_D(DD)                                                                      \
   bool kset_d##DD(int rpl, KernelSet& ks);                                                      \
-  void launch_rollout_d##DD(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp); \
+  void launch_rollout_d##DD(int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp); \
   void launch_evalb_d##DD(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp);
 MRBO_DECLARE_D(1) MRBO_DECLARE_D(2) MRBO_DECLARE_D(3) MRBO_DECLARE_D(4)
 MRBO_DECLARE_D(5) MRBO_DECLARE_D(6) MRBO_DECLARE_D(7) MRBO_DECLARE_D(8)

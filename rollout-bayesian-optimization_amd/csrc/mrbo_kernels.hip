@@ -15,7 +15,8 @@ namespace mrbo {
 template <int D, int RPL>
 static KernelSet kset() {
   using Ly = Lay<D, RPL>;
-  return KernelSet{(const void*)&rollout_kernel<D, RPL>, (const void*)&eval_base_kernel<D, RPL>,
+  return KernelSet{(const void*)&rollout_kernel<D, RPL, 0>, (const void*)&rollout_kernel<D, RPL, 1>,
+                   (const void*)&eval_base_kernel<D, RPL>,
                    sizeof(double) * Ly::WAVE_LDS, Ly::SQ, Ly::LD, Ly::LINV_DOUBLES, Ly::GL, Ly::LINV_GLOBAL,
                    KBounds<RPL>::threads};
 }
@@ -28,10 +29,17 @@ bool MRBO_CAT(kset_d, MRBO_D)(int rpl, KernelSet& ks) {
   return true;
 }
 
-void MRBO_CAT(launch_rollout_d, MRBO_D)(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
-  if (rpl == 1) hipLaunchKernelGGL((rollout_kernel<MRBO_D, 1>), g, b, sm, st, kp);
-  else if (rpl == 2) hipLaunchKernelGGL((rollout_kernel<MRBO_D, 2>), g, b, sm, st, kp);
-  else hipLaunchKernelGGL((rollout_kernel<MRBO_D, 4>), g, b, sm, st, kp);
+template <int SPEC>
+static void launch_rollout_spec(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
+  if (rpl == 1) hipLaunchKernelGGL((rollout_kernel<MRBO_D, 1, SPEC>), g, b, sm, st, kp);
+  else if (rpl == 2) hipLaunchKernelGGL((rollout_kernel<MRBO_D, 2, SPEC>), g, b, sm, st, kp);
+  else hipLaunchKernelGGL((rollout_kernel<MRBO_D, 4, SPEC>), g, b, sm, st, kp);
+}
+
+void MRBO_CAT(launch_rollout_d, MRBO_D)(int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st,
+                                       const KParams& kp) {
+  if (spec) launch_rollout_spec<1>(rpl, g, b, sm, st, kp);
+  else launch_rollout_spec<0>(rpl, g, b, sm, st, kp);
 }
 
 void MRBO_CAT(launch_evalb_d, MRBO_D)(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {

@@ -322,3 +322,21 @@ def test_reference_signature_and_outer_ascent(gpu):
     np.testing.assert_allclose(eto.gradient(), es.spatial_gradients_container.mean(axis=1), rtol=1e-10)
     x = stochastic_solve(StandardSGA(η=0.5), pb.surrogate, pb.tp, es, pb.x0s[:, 0], T=pb.T, iterations=3)
     assert x.shape == (2,) and np.all(np.isfinite(x))
+
+
+@pytest.mark.parametrize("name,M,R", [("C2", 32, 4), ("C3", 32, 4), ("C4", 8, 2)])
+def test_specialised_kernel_equals_generic(gpu, monkeypatch, name, M, R):
+    """Matérn-5/2 + EI runs rollout_kernel<D, RPL, 1> (kernel and rule fixed at compile time);
+    MRBO_GENERIC_KERNEL=1 forces the generic instantiation.  Same source and operation order; the
+    compiler schedules the two differently (measured: a few results differ by 1 ulp), so the
+    comparison is to rtol 1e-12, with identical policy paths and identical Newton work."""
+    g = _problem_arrays(name, M, R)
+    r_spec = _run(_plan(g), g)
+    monkeypatch.setenv("MRBO_GENERIC_KERNEL", "1")
+    r_gen = _run(_plan(g), g)
+    assert (r_spec["status"] == 0).all() and (r_gen["status"] == 0).all()
+    np.testing.assert_array_equal(r_spec["evals"], r_gen["evals"])
+    for k in ("values", "obs", "policy_x"):
+        np.testing.assert_allclose(r_spec[k], r_gen[k], rtol=1e-12, atol=1e-15, err_msg=k)
+    for k in ("grad_x", "grad_theta"):
+        _assert_grads_close(r_spec[k], r_gen[k], rtol=1e-10)
