@@ -169,7 +169,8 @@ def main():
 
     st = out["status"].cpu().numpy()
     ev = evals_acc.cpu().numpy().reshape((flops.NCOUNTERS, hi - lo, R), order="F") / max(args.steps, 1)
-    fl = flops.launch_flops(ev, cfg.N, d, h)
+    info = plan.info()
+    fl = flops.launch_flops(ev, cfg.N, d, h, info=info, nstarts=pb.es.get_starts().shape[1])
     kms = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
     achieved = fl / (kms * 1e-3) / 1e12
     traffic = None
@@ -197,7 +198,8 @@ def main():
                    "N": cfg.N, "d": d, "parallelism": f"mc-shard x{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": f"rollout_kernel<{d},{1 if cfg.N <= 64 else 2 if cfg.N <= 128 else 4},1>", "kernel_ms": kms, "flops_per_launch": fl,
+                     "kernel": f"rollout_kernel<{d},{info['rpl']},{info['spec']}>", "kernel_ms": kms, "flops_per_launch": fl,
+                     "launch": info,
                      "note": "compute-bound fp64: peak = the dense fp64 matrix peak, equal to the fp64 vector "
                              "peak on MI355X; the kernel issues VALU v_fma_f64 (matrix-vector work, not "
                              "GEMM-shaped); algorithmic FLOP model in DESIGN.md §5; HBM algorithmic "

@@ -193,6 +193,11 @@ double mrbo_dual_uniform(uint64_t seed, int64_t traj, int32_t j, int32_t k);
 /* Timing of the last mrbo_simulate_mc kernel on its stream (HIP events), milliseconds. */
 double mrbo_last_kernel_ms(mrbo_plan_t* plan);
 
+/* Launch geometry of a plan (no reference counterpart; measurement and FLOP accounting):
+ * info[0..5] = rows per lane (1/2/4), workgroups, waves per workgroup, batched start values
+ * (0/1), compile-time specialised kernel (0/1), LDS bytes per workgroup.  Writes min(n, 6). */
+int mrbo_plan_info(const mrbo_plan_t* plan, int32_t* info, int32_t n);
+
 #ifdef __cplusplus
 }
 #endif

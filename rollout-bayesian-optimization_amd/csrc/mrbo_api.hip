@@ -55,7 +55,9 @@ struct mrbo_plan {
   double* dlbs = nullptr;
   double* dubs = nullptr;
   double* dwork = nullptr;
-  double* dytab = nullptr;  // batched starts: per-workgroup Y0(x_start) slices
+  double* dytab = nullptr;  // batched starts: per-workgroup Y0(x_start) slices (square layout)
+  double* dkxb = nullptr;   // batched starts, packed layouts: global start tables (start_tables_kernel)
+  double* dgtab = nullptr;
   long long work_stride = 0;
   int* dqueue = nullptr;
   int wpg = 4, blocks = 0;
@@ -84,6 +86,20 @@ bool get_kset(int d, int rpl, KernelSet& ks) {
 #endif
     default: return false;
   }
+#undef CASE
+#undef CASE_
+}
+
+// start tables of the packed layouts (rpl 2 / 4), before a rollout launch with kp.batch
+void launch_tables(int d, int rpl, int nstarts, hipStream_t st, const KParams& kp) {
+#define CASE_(DD) \
+  case DD: launch_tables_d##DD(rpl, nstarts, st, kp); break;
+#define CASE(DD) CASE_(DD)
+#ifdef MRBO_ONLY_D
+  switch (d) { CASE(MRBO_ONLY_D) }
+#else
+  switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) }
+#endif
 #undef CASE
 #undef CASE_
 }
@@ -405,6 +421,8 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
     if (waves1 >= waves0 && waves1 > 0) { P->batch = 1; P->wpg = wpg1; P->blocks = blocks1; P->smem = smem1; }
   }
   if (!P->batch) { P->wpg = wpg0; P->blocks = blocks0; P->smem = smem0; }
+  // packed layouts: the start tables live in global memory (no LDS, no occupancy cost)
+  if (!ks.square && P->xs_lds && ns <= 64) P->batch = 1;
   if (!waves0 ||
       !pick_grid(ks.evalb, linv_bytes, ks.wave_bytes, prop.multiProcessorCount, P->ewpg, P->eblocks, P->esmem, 0,
                  maxw)) {
@@ -419,7 +437,11 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
             hipMalloc(&P->dlbs, sizeof(double) * d) == hipSuccess &&
             hipMalloc(&P->dubs, sizeof(double) * d) == hipSuccess &&
             hipMalloc(&P->dwork, sizeof(double) * (size_t)slots * P->work_stride) == hipSuccess &&
-            (!P->batch || hipMalloc(&P->dytab, sizeof(double) * (size_t)P->blocks * ns * P->NR) == hipSuccess) &&
+            (!P->batch || !ks.square ||
+             hipMalloc(&P->dytab, sizeof(double) * (size_t)P->blocks * ns * P->NR) == hipSuccess) &&
+            (!P->batch || ks.square ||
+             (hipMalloc(&P->dkxb, sizeof(double) * (size_t)P->NR * ns) == hipSuccess &&
+              hipMalloc(&P->dgtab, sizeof(double) * (size_t)ns * ng) == hipSuccess)) &&
             hipMalloc(&P->dqueue, sizeof(int) * 4) == hipSuccess;
   ok = ok && hipMemcpy(P->dX0, X0.data(), sizeof(double) * X0.size(), hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(P->dc0, c0.data(), sizeof(double) * c0.size(), hipMemcpyHostToDevice) == hipSuccess &&
@@ -439,7 +461,7 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
 int mrbo_plan_destroy(mrbo_plan_t* P) {
   if (!P) return MRBO_OK;
   for (void* b : {(void*)P->dX0, (void*)P->dc0, (void*)P->dLinv, (void*)P->dlbs, (void*)P->dubs, (void*)P->dwork, (void*)P->dytab,
-                  (void*)P->dqueue})
+                  (void*)P->dkxb, (void*)P->dgtab, (void*)P->dqueue})
     if (b) (void)hipFree(b);
   if (P->ev0) (void)hipEventDestroy(P->ev0);
   if (P->ev1) (void)hipEventDestroy(P->ev1);
@@ -497,6 +519,12 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
   HIP_TRY(hipEventRecord(P->ev0, st));
   kp.xs_lds = P->xs_lds;
   kp.batch = P->batch;
+  if (P->batch && P->RPL > 1) {   // packed layouts: global start tables for this launch's xstarts
+    kp.kxb_g = P->dkxb;
+    kp.gtab_g = P->dgtab;
+    launch_tables(d, P->RPL, P->p.nstarts, st, kp);
+    HIP_TRY(hipGetLastError());
+  }
   launch_rollout(d, P->RPL, P->spec, dim3(P->blocks), dim3(P->wpg * WAVE), P->smem, st, kp);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(P->ev1, st));
@@ -627,6 +655,13 @@ int mrbo_gp_fit(const mrbo_surrogate_t* s, int32_t np, const double* ells, doubl
     if (L_out) HIP_TRY(hipMemcpy(L_out, dL, sizeof(double) * NN * P, hipMemcpyDeviceToHost));
     if (c_out) HIP_TRY(hipMemcpy(c_out, dc, sizeof(double) * N * P, hipMemcpyDeviceToHost));
   }
+  return MRBO_OK;
+}
+
+int mrbo_plan_info(const mrbo_plan_t* P, int32_t* info, int32_t n) {
+  if (!P || !info || n < 0) return fail(MRBO_ERR_ARG, "bad arguments");
+  const int32_t v[6] = {P->RPL, P->blocks, P->wpg, P->batch, P->spec, (int32_t)P->smem};
+  for (int i = 0; i < n && i < 6; ++i) info[i] = v[i];
   return MRBO_OK;
 }
 

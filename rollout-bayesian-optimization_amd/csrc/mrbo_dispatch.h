@@ -24,7 +24,8 @@ struct KernelSet {
 #define MRBO_DECLARE_D(DD)                                                                      \
   bool kset_d##DD(int rpl, KernelSet& ks);                                                      \
   void launch_rollout_d##DD(int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp); \
-  void launch_evalb_d##DD(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp);
+  void launch_evalb_d##DD(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp); \
+  void launch_tables_d##DD(int rpl, int nstarts, hipStream_t st, const KParams& kp);
 MRBO_DECLARE_D(1) MRBO_DECLARE_D(2) MRBO_DECLARE_D(3) MRBO_DECLARE_D(4)
 MRBO_DECLARE_D(5) MRBO_DECLARE_D(6) MRBO_DECLARE_D(7) MRBO_DECLARE_D(8)
 #undef MRBO_DECLARE_D

@@ -42,6 +42,11 @@ void MRBO_CAT(launch_rollout_d, MRBO_D)(int rpl, int spec, dim3 g, dim3 b, size_
   else launch_rollout_spec<0>(rpl, g, b, sm, st, kp);
 }
 
+void MRBO_CAT(launch_tables_d, MRBO_D)(int rpl, int nstarts, hipStream_t st, const KParams& kp) {
+  if (rpl == 2) hipLaunchKernelGGL((start_tables_kernel<MRBO_D, 2>), dim3(nstarts), dim3(WAVE), 0, st, kp);
+  else if (rpl == 4) hipLaunchKernelGGL((start_tables_kernel<MRBO_D, 4>), dim3(nstarts), dim3(WAVE), 0, st, kp);
+}
+
 void MRBO_CAT(launch_evalb_d, MRBO_D)(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
   if (rpl == 1) hipLaunchKernelGGL((eval_base_kernel<MRBO_D, 1>), g, b, sm, st, kp);
   else if (rpl == 2) hipLaunchKernelGGL((eval_base_kernel<MRBO_D, 2>), g, b, sm, st, kp);

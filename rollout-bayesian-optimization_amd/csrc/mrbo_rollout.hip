@@ -111,9 +111,10 @@ struct WgTables {
     xs = Ly::LINV_DOUBLES;
     const long long nxs = kp.xs_lds ? (((long long)kp.nstarts * D + 1) & ~1LL) : 0;
     kxb = xs + nxs;
-    const long long nk = kp.batch ? (((long long)Ly::NR * kp.nstarts + 1) & ~1LL) : 0;
+    const bool lt = Ly::SQ && kp.batch;   // packed layouts keep the start tables in global memory
+    const long long nk = lt ? (((long long)Ly::NR * kp.nstarts + 1) & ~1LL) : 0;
     gtab = kxb + nk;
-    end = gtab + (kp.batch ? (((long long)kp.nstarts * Ly::NG + 1) & ~1LL) : 0);
+    end = gtab + (lt ? (((long long)kp.nstarts * Ly::NG + 1) & ~1LL) : 0);
   }
 };
 
@@ -127,8 +128,8 @@ struct WaveCtx {
   const double* Linv;   // L0⁻¹: LDS (Lay::SQ square or packed columns) or global packed columns (GL)
   const double* LinvT;  // GL: global L0⁻¹ packed by rows (row k: entries 0..k)
   const double* XS;     // inner-solve start points: LDS copy (kp.xs_lds) or kp.xstarts
-  const double* KXB;    // LDS [NR][nstarts]: ψ(|clamp(x_k) − X_i|) (kp.batch)
-  const double* GTAB;   // LDS [nstarts][NG]: base Gram of the start points (kp.batch)
+  const double* KXB;    // [NR][nstarts]: ψ(|clamp(x_k) − X_i|) (kp.batch; LDS, global for packed layouts)
+  const double* GTAB;   // [nstarts][NG]: base Gram of the start points (kp.batch; LDS, global for packed)
   const double* YTAB;   // global [nstarts][NR]: this workgroup's Y0(x_k) = L0⁻¹kx(x_k) (kp.batch)
   double* G12;          // LDS: per-lane [g1, g2, Y0] of the base rows (GRAD / FULL / RICH)
   double* E;            // LDS (SQ) or global: FMAX × NR  inverse-factor fantasy rows (base columns)
@@ -1108,7 +1109,9 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
   wave_sync();
   // have_f0: the start's value (and certificate) came from batch_start_values and did not
   // stop the iteration, so it begins with the gradient at x_start
-  int phase = have_f0 ? P_GRAD : P_VAL, mode = have_f0 ? EV_GSTART : EV_VALUE, it = 0, ls = 0;
+  // (GSTART takes the base forward product from the square layout's per-workgroup tables; the
+  // packed layouts evaluate the gradient at the start point in full)
+  int phase = have_f0 ? P_GRAD : P_VAL, mode = have_f0 ? (Ly::SQ ? EV_GSTART : EV_GRAD) : EV_VALUE, it = 0, ls = 0;
   double f = have_f0 ? f0 : 0.0, ft = 0.0, t = 1.0, dec = 0.0;
   for (;;) {
     evaluate<D, RPL>(W, kp, S, mode, lr, k);
@@ -1882,8 +1885,8 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
   const WgTables<D, RPL> tb(kp);
   double* wbase = smem + tb.end + (long long)wave_in_block * Ly::WAVE_LDS;
   W.XS = kp.xs_lds ? smem + tb.xs : kp.xstarts;
-  W.KXB = smem + tb.kxb;
-  W.GTAB = smem + tb.gtab;
+  W.KXB = Ly::SQ ? smem + tb.kxb : kp.kxb_g;
+  W.GTAB = Ly::SQ ? smem + tb.gtab : kp.gtab_g;
   W.YTAB = kp.ytab + (long long)blockIdx.x * kp.nstarts * Ly::NR;
   W.B = wbase;
   W.red = wbase + Ly::BROWS * Ly::BS;
@@ -1950,6 +1953,80 @@ __global__ void __launch_bounds__(KBounds<RPL>::threads, KBounds<RPL>::waves_per
     for (int k = 0; k < 20; ++k)
       atomicAdd(kp.stamps + k, reinterpret_cast<unsigned long long*>(W.U + Lay<D, RPL>::U_STAMP)[k]);
 #endif
+}
+
+// Start tables of the packed layouts (N > 64, kp.batch), one wave per start point k, written to
+// global memory before the rollout launch (every workgroup reads the same copy through L2):
+//   kxb_g[i][k] = ψ(|clamp(x_k) − X_i|) (0 on padded rows),
+//   gtab_g[k]   = base Gram YᵀY of Y = L0⁻¹[kx, ∇kx](x_k), upper triangle row-major (entry 0 is
+//                 |L0⁻¹kx|², the only entry batch_start_values reads).
+// The forward product walks the packed-by-columns image of L0⁻¹ (column j: rows j..Npad-1).
+template <int D, int RPL>
+__global__ void __launch_bounds__(WAVE) start_tables_kernel(KParams kp) {
+  using Ly = Lay<D, RPL>;
+  constexpr int NR = Ly::NR, D1 = Ly::D1;
+  __shared__ double Bs[NR * D1];
+  __shared__ double red[16 * ((Ly::NG + 15) / 16)];
+  const int lane = threadIdx.x, k = blockIdx.x, ns = kp.nstarts;
+  Radial rad;
+  rad.kind = kp.kernel;
+  rad.cK = kp.cK;
+  rad.cP = kp.cP;
+  double xk[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) xk[a] = clampd(kp.xstarts[(long long)k * D + a], kp.lbs[a], kp.ubs[a]);
+#pragma unroll
+  for (int s = 0; s < RPL; ++s) {
+    const int i = lane + WAVE * s;
+    double r[D], rho2 = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) { r[a] = xk[a] - kp.X0[(long long)a * NR + i]; rho2 = fma(r[a], r[a], rho2); }
+    double psi, g1, g2;
+    rad_eval(rad, rho2, psi, g1, g2);
+    const bool v = i < kp.N;
+    Bs[i * D1] = v ? psi : 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) Bs[i * D1 + 1 + a] = v ? g1 * r[a] : 0.0;
+    kp.kxb_g[(long long)i * ns + k] = v ? psi : 0.0;
+  }
+  __syncthreads();
+  double acc[RPL][D1];
+#pragma unroll
+  for (int s = 0; s < RPL; ++s)
+#pragma unroll
+    for (int c = 0; c < D1; ++c) acc[s][c] = 0.0;
+  for (int j = 0; j < kp.N; ++j) {
+    double bj[D1];
+#pragma unroll
+    for (int c = 0; c < D1; ++c) bj[c] = Bs[j * D1 + c];
+#pragma unroll
+    for (int s = 0; s < RPL; ++s) {
+      const int i = lane + WAVE * s;
+      const double l = (i >= j && i < kp.N) ? kp.Linv[linv_colstart(j, kp.Npad) - j + i] : 0.0;
+#pragma unroll
+      for (int c = 0; c < D1; ++c) acc[s][c] = fma(l, bj[c], acc[s][c]);
+    }
+  }
+#pragma unroll
+  for (int ch = 0; ch < (Ly::NG + 15) / 16; ++ch) {
+    double gv[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int t = 16 * ch + q;
+      double s_ = 0.0;
+      if (t < Ly::NG) {
+        int a = 0, rem = t;
+#pragma unroll
+        for (int aa = 0; aa < D1; ++aa) if (a == aa && rem >= D1 - aa) { rem -= D1 - aa; a = aa + 1; }
+#pragma unroll
+        for (int s = 0; s < RPL; ++s) s_ = fma(acc[s][a], acc[s][a + rem], s_);
+      }
+      gv[q] = s_;
+    }
+    wave_reduce<16>(gv, red + 16 * ch, lane);
+  }
+  __syncthreads();
+  if (lane < Ly::NG) kp.gtab_g[(long long)k * Ly::NG + lane] = red[lane];
 }
 
 // eval(s, x, θ) on the base surrogate for P points (fixture / primitive parity path)

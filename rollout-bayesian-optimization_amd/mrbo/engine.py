@@ -155,6 +155,14 @@ class RolloutPlan:
     def last_kernel_ms(self):
         return self.lib.mrbo_last_kernel_ms(self.handle)
 
+    def info(self):
+        """Launch geometry: rows per lane, workgroups, waves per workgroup, batched start values,
+        specialised kernel, LDS bytes per workgroup."""
+        v = (ctypes.c_int32 * 6)()
+        _lib.check(self.lib.mrbo_plan_info(self.handle, v, 6))
+        keys = ("rpl", "blocks", "waves_per_group", "batch", "spec", "lds_bytes")
+        return dict(zip(keys, (int(x) for x in v)))
+
 
 def rnstream(M, d, H):
     """gen_low_discrepancy_sequence (utils.jl:65-74) via the library's host Sobol."""

@@ -63,6 +63,20 @@ def f_pair(N, nf, d):
     return N * (5 * d + 12 + 2 * (d * d + 2 * d)) + nf * (5 * d + 12 + 2 * (d * d + 2 * d)) + (d + 1) * (6 * d * d + 40 * d)
 
 
+def f_batch_start(N, nf, d):
+    """One start point of the batched start-value pass (batch_start_values): the base part of μ
+    and of the fantasy rows from the launch's kernel-row table (c·kxb, E_r·kxb over N rows), the
+    fantasy radial functions, Dinv·pf, σ² from the tabled |L0⁻¹kx|², EI and the certificate."""
+    return 2 * N * (1 + nf) + nf * (3 * d + 10) + nf * (nf + 1) + 4 * nf + 40
+
+
+def f_start_table(N, d):
+    """Launch constants of one start point (stage_start_tables / start_tables_kernel): base kernel
+    rows and gradients, Y = L0⁻¹[kx, ∇kx], the base Gram YᵀY."""
+    D1 = d + 1
+    return _rows(N, d) + D1 * N * (N + 1) + N * D1 * (D1 + 1)
+
+
 NCOUNTERS = 5   # mrbo_simulate_mc evals: grad, value, hess, rich, pairs
 
 
@@ -75,10 +89,23 @@ def trajectory_flops(counts, N, d, h):
             + rich * f_rich(N, nf_solve, d) + pairs * f_pair(N, nf_solve, d))
 
 
-def launch_flops(evals, N, d, h):
-    """evals: (NCOUNTERS, M, R) counters of one launch → total algorithmic flops of the launch."""
+def launch_flops(evals, N, d, h, info=None, nstarts=0):
+    """evals: (NCOUNTERS, M, R) counters of one launch → total algorithmic flops of the launch.
+
+    info: RolloutPlan.info() of the launch.  With batched start values the counters still count
+    every start point as a value evaluation (as the oracle does); those h·nstarts evaluations per
+    trajectory are charged at the batched pass's cost instead, plus the start tables (staged once
+    per workgroup for the square layout, once per launch for the packed ones)."""
     import numpy as np
     e = np.asarray(evals, dtype=np.float64).reshape(NCOUNTERS, -1)
     ntraj = e.shape[1]
     draws = sum(f_draw(N, k, d) for k in range(h + 1))
-    return float(trajectory_flops(e.sum(axis=1), N, d, h) + ntraj * draws)
+    tot = e.sum(axis=1)
+    extra = 0.0
+    if info is not None and info.get("batch") and nstarts:
+        nb = min(float(h * nstarts * ntraj), float(tot[1]))   # batched start values of the launch
+        tot[1] -= nb
+        nf_solve = (1 + h) / 2.0
+        tables = info["blocks"] if info.get("rpl", 1) == 1 else 1
+        extra = nb * f_batch_start(N, nf_solve, d) + tables * nstarts * f_start_table(N, d)
+    return float(trajectory_flops(tot, N, d, h) + ntraj * draws + extra)
