@@ -70,7 +70,7 @@ struct KParams {
   double* work;         // per wave-slot global scratch
   long long work_stride;
   double* ytab;         // kp.batch, square layout: per-workgroup slices [blockIdx][nstarts][NR] of Y0(x_start)
-  double* kxb_g;        // kp.batch, packed layouts (N > 64): global start tables [NR][nstarts] and
+  double* kxb_g;        // kp.batch, packed layouts (N > 64): global start tables [nstarts][NR] and
   double* gtab_g;       //   [nstarts][NG] written by start_tables_kernel before the rollout launch
   const double* ghq_nodes;  // Gauss–Hermite estimator: M×(h+1) nodes and weights per sample (else null)
   const double* ghq_w;

@@ -128,7 +128,7 @@ struct WaveCtx {
   const double* Linv;   // L0⁻¹: LDS (Lay::SQ square or packed columns) or global packed columns (GL)
   const double* LinvT;  // GL: global L0⁻¹ packed by rows (row k: entries 0..k)
   const double* XS;     // inner-solve start points: LDS copy (kp.xs_lds) or kp.xstarts
-  const double* KXB;    // [NR][nstarts]: ψ(|clamp(x_k) − X_i|) (kp.batch; LDS, global for packed layouts)
+  const double* KXB;    // ψ(|clamp(x_k) − X_i|) (kp.batch): LDS [NR][nstarts]; packed layouts: global [nstarts][NR]
   const double* GTAB;   // [nstarts][NG]: base Gram of the start points (kp.batch; LDS, global for packed)
   const double* YTAB;   // global [nstarts][NR]: this workgroup's Y0(x_k) = L0⁻¹kx(x_k) (kp.batch)
   double* G12;          // LDS: per-lane [g1, g2, Y0] of the base rows (GRAD / FULL / RICH)
@@ -1298,7 +1298,50 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   // all FMAX rows unconditionally (rows ≥ nf hold finite stale values, masked below): a load
   // under a condition would become a branch with a full LDS round trip per row.  Rows N..NR-1
   // of the tables are zero.
-  if (split) {
+  if constexpr (!Ly::SQ) {
+    // packed layouts (E, c and the kernel-row table in global memory): lanes own data rows and
+    // the starts run in a loop, so every load is a coalesced row walk (a lane-per-start loop over
+    // rows would chain NR dependent global round trips).  Per start the 1 + FMAX base products
+    // [c_S·kxb_k, E_r·kxb_k] are transpose-reduced (two starts per 16-value reduction) into B
+    // (scratch between evaluations), then lane k reads its start's sums.
+    double cv[RPL], ev[RPL][FMAX];
+#pragma unroll
+    for (int s2 = 0; s2 < RPL; ++s2) {
+      const int i = lane + WAVE * s2;
+      cv[s2] = cS[i];
+#pragma unroll
+      for (int r = 0; r < FMAX; ++r) ev[s2][r] = W.E[(long long)r * NR + i];
+    }
+    double* sums = W.B;   // [ns][8]
+    for (int kc = 0; kc < ns; kc += 2) {
+      double v[16];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int kq = (kc + kk < ns) ? kc + kk : kc;
+        double kx[RPL];
+#pragma unroll
+        for (int s2 = 0; s2 < RPL; ++s2) kx[s2] = W.KXB[(long long)kq * NR + lane + WAVE * s2];
+        double a0 = 0.0;
+#pragma unroll
+        for (int s2 = 0; s2 < RPL; ++s2) a0 = fma(cv[s2], kx[s2], a0);
+        v[8 * kk] = a0;
+#pragma unroll
+        for (int r = 0; r < FMAX; ++r) {
+          double a = 0.0;
+#pragma unroll
+          for (int s2 = 0; s2 < RPL; ++s2) a = fma(ev[s2][r], kx[s2], a);
+          v[8 * kk + 1 + r] = a;
+        }
+        v[8 * kk + 7] = 0.0;
+      }
+      wave_reduce<16>(v, sums + 8 * kc, lane);
+    }
+    wave_sync();
+    amu = sums[8 * k];
+#pragma unroll
+    for (int r = 0; r < FMAX; ++r) ae[r] = sums[8 * k + 1 + r];
+    wave_sync();   // sums read before B is reused
+  } else if (split) {
 #pragma unroll 8
     for (int j = 0; j < NR / 2; ++j) {
       const int i = 2 * j + hf;
@@ -1957,7 +2000,7 @@ __global__ void __launch_bounds__(KBounds<RPL>::threads, KBounds<RPL>::waves_per
 
 // Start tables of the packed layouts (N > 64, kp.batch), one wave per start point k, written to
 // global memory before the rollout launch (every workgroup reads the same copy through L2):
-//   kxb_g[i][k] = ψ(|clamp(x_k) − X_i|) (0 on padded rows),
+//   kxb_g[k][i] = ψ(|clamp(x_k) − X_i|) (0 on padded rows; start-major, unlike the LDS table),
 //   gtab_g[k]   = base Gram YᵀY of Y = L0⁻¹[kx, ∇kx](x_k), upper triangle row-major (entry 0 is
 //                 |L0⁻¹kx|², the only entry batch_start_values reads).
 // The forward product walks the packed-by-columns image of L0⁻¹ (column j: rows j..Npad-1).
@@ -1987,7 +2030,7 @@ __global__ void __launch_bounds__(WAVE) start_tables_kernel(KParams kp) {
     Bs[i * D1] = v ? psi : 0.0;
 #pragma unroll
     for (int a = 0; a < D; ++a) Bs[i * D1 + 1 + a] = v ? g1 * r[a] : 0.0;
-    kp.kxb_g[(long long)i * ns + k] = v ? psi : 0.0;
+    kp.kxb_g[(long long)k * NR + i] = v ? psi : 0.0;
   }
   __syncthreads();
   double acc[RPL][D1];
