@@ -388,7 +388,12 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   std::vector<double> packed((size_t)ks.linv_dev, 0.0);
   for (int j = 0; j < N; ++j)
     for (int i = j; i < N; ++i) {
-      packed[ks.square ? (size_t)j * ks.ld + i : (size_t)linv_colstart(j, Npad) + (i - j)] = Li[i + (size_t)N * j];
+      size_t at;
+      if (ks.blocks)   // block (s,t) = (i/64, j/64) at (s(s+1)/2 + t)·64·ld, column-major inside
+        at = ((size_t)(i / 64) * (i / 64 + 1) / 2 + j / 64) * 64 * ks.ld + (size_t)(j % 64) * ks.ld + i % 64;
+      else
+        at = ks.square ? (size_t)j * ks.ld + i : (size_t)linv_colstart(j, Npad) + (i - j);
+      packed[at] = Li[i + (size_t)N * j];
       if (ks.gl) packed[(size_t)linv_size(Npad) + (size_t)i * (i + 1) / 2 + j] = Li[i + (size_t)N * j];
     }
   hipDeviceProp_t prop;
@@ -430,7 +435,9 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
     return fail(MRBO_ERR_UNSUPPORTED, "no feasible launch configuration");
   }
   const int slots = std::max(P->blocks * P->wpg, P->eblocks * P->ewpg);
-  P->work_stride = (long long)(2 * FMAX + 1) * P->NR;
+  // per wave slot: E (FMAX × NR) and C ((FMAX+1) × NR), then the batched start pass's per-start
+  // sums (64 × 8) for the packed layouts
+  P->work_stride = (long long)(2 * FMAX + 1) * P->NR + 64 * 8;
   bool ok = hipMalloc(&P->dX0, sizeof(double) * X0.size()) == hipSuccess &&
             hipMalloc(&P->dc0, sizeof(double) * c0.size()) == hipSuccess &&
             hipMalloc(&P->dLinv, sizeof(double) * packed.size()) == hipSuccess &&

@@ -14,6 +14,7 @@ struct KernelSet {
   const void* evalb;
   size_t wave_bytes;        // per-wave LDS
   bool square;              // L0⁻¹ layout: dense square (ld) or packed triangle
+  bool blocks;              // L0⁻¹ layout: the three 64×64 blocks (0,0), (1,0), (1,1), each ld-square
   int ld;
   long long linv_doubles;   // LDS-resident L0⁻¹ (0 when it stays in global memory)
   bool gl;                  // L0⁻¹ in global memory: packed by columns, then packed by rows

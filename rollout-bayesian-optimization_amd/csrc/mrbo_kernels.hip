@@ -17,7 +17,7 @@ static KernelSet kset() {
   using Ly = Lay<D, RPL>;
   return KernelSet{(const void*)&rollout_kernel<D, RPL, 0>, (const void*)&rollout_kernel<D, RPL, 1>,
                    (const void*)&eval_base_kernel<D, RPL>,
-                   sizeof(double) * Ly::WAVE_LDS, Ly::SQ, Ly::LD, Ly::LINV_DOUBLES, Ly::GL, Ly::LINV_GLOBAL,
+                   sizeof(double) * Ly::WAVE_LDS, Ly::SQ, Ly::BC && !Ly::SQ, Ly::LD, Ly::LINV_DOUBLES, Ly::GL, Ly::LINV_GLOBAL,
                    KBounds<RPL>::threads};
 }
 

@@ -26,10 +26,13 @@ struct Lay {
   static constexpr int D1 = D + 1;
   static constexpr int BS = (D1 + 1) & ~1;         // B row stride in doubles (16-B aligned rows)
   static constexpr int NR = RPL * WAVE;            // base-row capacity of the wave
-  // L0⁻¹ layout (see LINV_DOUBLES below); the square layout also moves the base kernel rows
-  // out of LDS (register broadcast) and the per-wave E / C rows into LDS
+  // L0⁻¹ layout (see LINV_DOUBLES below).  BC: register-broadcast triangular products over
+  // square 64×64 blocks of L0⁻¹ in LDS (RPL = 1: one block; RPL = 2: the three blocks of the
+  // lower block triangle), which also moves the base kernel rows out of LDS.  SQ (RPL = 1)
+  // additionally keeps the per-wave E / C rows and the start tables in LDS.
   static constexpr bool SQ = (RPL == 1);
-  static constexpr int FR0 = SQ ? 0 : NR;          // first fantasy row in B
+  static constexpr bool BC = (RPL <= 2);
+  static constexpr int FR0 = BC ? 0 : NR;          // first fantasy row in B
   static constexpr int BROWS = FR0 + FMAX;         // [base rows +] fantasy rows
   static constexpr int NG = D1 * (D1 + 1) / 2;     // Gram entries (a ≤ b)
   static constexpr int NH = D * (D + 1) / 2;       // Hessian entries (a ≤ b)
@@ -81,18 +84,22 @@ struct Lay {
   static constexpr int G12 = 3 * NR;                     // per-lane [g1, g2, Y0] of the base rows
   static constexpr int EC = SQ ? (2 * FMAX + 1) * NR : 0;  // E (FMAX×NR) + C ((FMAX+1)×NR) in LDS
   static constexpr int WAVE_LDS = BROWS * BS + REDN + U_SIZE + G12 + EC;
-  // L0⁻¹ in LDS, shared by the waves of a workgroup.  RPL == 1: dense zero-padded square,
-  // column-major with odd leading dimension LD = NR + 1, so the column walk (forward product,
+  // L0⁻¹ in LDS, shared by the waves of a workgroup.  BC: dense zero-padded 64×64 blocks,
+  // column-major with odd leading dimension LD = 65, so the column walk (forward product,
   // lane i reads [i][j]) and the row walk (backward product, lane i reads [k][i]) are both
-  // bank-conflict free and neither needs a triangle mask.  RPL > 1: packed triangle (the
-  // square would not fit next to the per-wave areas).
-  static constexpr int LD = NR + 1;
+  // bank-conflict free and neither needs a triangle mask.  RPL = 2 stores the blocks (0,0),
+  // (1,0), (1,1) of the block triangle (block (s,t) holds rows 64s.., columns 64t..; the
+  // all-zero block (0,1) is skipped), 99.8 KB.
+  static constexpr int LD = WAVE + 1;
+  static constexpr int NBLK = RPL * (RPL + 1) / 2;
+  static constexpr int BLK = WAVE * LD;            // doubles per block
+  __host__ __device__ static constexpr int blk(int s, int t) { return s * (s + 1) / 2 + t; }   // t ≤ s
   // RPL > 2 (N ≤ 256): L0⁻¹ does not fit in LDS next to the wave areas (263 KB packed); it stays
   // in global memory (L2-resident, shared by every wave of the XCD) as two packed copies --
   // by columns for the forward product, by rows for the backward one -- so that both row walks
   // are coalesced 512-byte loads
   static constexpr bool GL = (RPL > 2);
-  static constexpr long long LINV_DOUBLES = GL ? 0 : (((SQ ? (long long)NR * LD : linv_size(NR)) + 1) & ~1LL);
+  static constexpr long long LINV_DOUBLES = GL ? 0 : (((BC ? (long long)NBLK * BLK : linv_size(NR)) + 1) & ~1LL);
   static constexpr long long LINV_GLOBAL = GL ? 2 * linv_size(NR) : LINV_DOUBLES;  // device image
 };
 // scalar slots in U_SC
@@ -134,6 +141,7 @@ struct WaveCtx {
   double* G12;          // LDS: per-lane [g1, g2, Y0] of the base rows (GRAD / FULL / RICH)
   double* E;            // LDS (SQ) or global: FMAX × NR  inverse-factor fantasy rows (base columns)
   double* C;            // LDS (SQ) or global: (FMAX+1) × NR  base part of c for surfaces -1..h
+  double* SUMS;         // packed layouts: global [64][8] per-start sums of the batched start pass
   double X0[RPL][D];    // own base rows
   bool valid[RPL];
   int N, Npad;
@@ -286,7 +294,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       Bown[s][0] = 0.0;   // column 0 comes from the VALUE pass
 #pragma unroll
       for (int a = 0; a < D; ++a) Bown[s][1 + a] = v ? g1 * r[a] : 0.0;
-      if constexpr (!Ly::SQ) {
+      if constexpr (!Ly::BC) {
         double* row = B + (lane + WAVE * s) * BS;
 #pragma unroll
         for (int a = 0; a < D; ++a) row[1 + a] = Bown[s][1 + a];
@@ -311,7 +319,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     for (int a = 0; a < D; ++a) Bown[s][1 + a] = v ? g1 * r[a] : 0.0;
     W.G12[3 * (lane + WAVE * s)] = g1;       // kept for a Hessian (phase 6, maybe deferred)
     W.G12[3 * (lane + WAVE * s) + 1] = g2;
-    if constexpr (!Ly::SQ) {   // the LDS row-broadcast path reads the base rows from B
+    if constexpr (!Ly::BC) {   // the LDS row-broadcast path reads the base rows from B
       double* row = B + (lane + WAVE * s) * BS;
       if (all_cols) {
 #pragma unroll
@@ -358,24 +366,46 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   for (int s = 0; s < RPL; ++s)
 #pragma unroll
     for (int c = 0; c < D1; ++c) acc[s][c] = 0.0;
-  if constexpr (Ly::SQ) {
-    // lane i reads L0⁻¹[i][j] at j·LD + i
+  if constexpr (Ly::BC) {
+    // lane i reads L0⁻¹[64s+i][64t+j] at blk(s,t)·BLK + j·LD + i; rows j of block column t are
+    // broadcast from register slot t.  Row slot s sums block columns t = 0..s in order.
+    auto nrows = [&](int t) { const int n = N - WAVE * t; return n < WAVE ? n : WAVE; };
     if (mode == EV_VALUE) {
-      double a1[1] = {0.0}, v1[1] = {Bown[0][0]};
-      bcast_product<1, Ly::LD>(a1, v1, W.Linv + lane, N);
-      acc[0][0] = a1[0];
+#pragma unroll
+      for (int s = 0; s < RPL; ++s) {
+        double a1[1] = {0.0};
+#pragma unroll
+        for (int t = 0; t <= s; ++t) {
+          const double v1[1] = {Bown[t][0]};
+          bcast_product<1, Ly::LD>(a1, v1, W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
+        }
+        acc[s][0] = a1[0];
+      }
     } else if (mode == EV_GSTART) {  // base forward product of start kst from the launch tables
-      acc[0][0] = W.YTAB[(long long)kst * NR + lane];
+      if constexpr (Ly::SQ) acc[0][0] = W.YTAB[(long long)kst * NR + lane];
     } else if (mode == EV_GRADC) {   // columns 1..d; column 0 from the VALUE pass
-      double ag[D], vg[D];
 #pragma unroll
-      for (int a = 0; a < D; ++a) { ag[a] = 0.0; vg[a] = Bown[0][1 + a]; }
-      bcast_product<D, Ly::LD>(ag, vg, W.Linv + lane, N);
+      for (int s = 0; s < RPL; ++s) {
+        double ag[D];
 #pragma unroll
-      for (int a = 0; a < D; ++a) acc[0][1 + a] = ag[a];
-      acc[0][0] = W.G12[3 * lane + 2];
+        for (int a = 0; a < D; ++a) ag[a] = 0.0;
+#pragma unroll
+        for (int t = 0; t <= s; ++t) {
+          double vg[D];
+#pragma unroll
+          for (int a = 0; a < D; ++a) vg[a] = Bown[t][1 + a];
+          bcast_product<D, Ly::LD>(ag, vg, W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
+        }
+#pragma unroll
+        for (int a = 0; a < D; ++a) acc[s][1 + a] = ag[a];
+        acc[s][0] = W.G12[3 * (lane + WAVE * s) + 2];
+      }
     } else {
-      bcast_product<D1, Ly::LD>(acc[0], Bown[0], W.Linv + lane, N);
+#pragma unroll
+      for (int s = 0; s < RPL; ++s)
+#pragma unroll
+        for (int t = 0; t <= s; ++t)
+          bcast_product<D1, Ly::LD>(acc[s], Bown[t], W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
     }
   } else {
   // L0⁻¹[i][j] for this lane's row i = lane + 64s.  Row block s needs columns j < 64(s+1) only
@@ -619,7 +649,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   // ---- 5. backward product w = L⁻ᵀ v (and P = L⁻ᵀ V for the adjoint)
   // stash Y rows (base) into B, then lane i walks column i of L0⁻¹
   const bool rich = (mode == EV_RICH);
-  if constexpr (!Ly::SQ) {
+  if constexpr (!Ly::BC) {
 #pragma unroll
     for (int s = 0; s < RPL; ++s) {
       double* row = B + (lane + WAVE * s) * BS;
@@ -639,20 +669,31 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
 #pragma unroll
       for (int a = 0; a < D; ++a) pv[s][a] = 0.0;
     }
-    if constexpr (Ly::SQ) {
-      // lane i reads L0⁻¹[k][i] at i·LD + k; Y rows broadcast from registers
-      if (rich) {
-        double a7[D1];
+    if constexpr (Ly::BC) {
+      // lane i (row slot s) reads L0⁻¹[64t+k][64s+i] at blk(t,s)·BLK + i·LD + k for block rows
+      // t = s..RPL-1; rows k of Y are broadcast from register slot t
+      auto nrows = [&](int t) { const int n = N - WAVE * t; return n < WAVE ? n : WAVE; };
 #pragma unroll
-        for (int c = 0; c < D1; ++c) a7[c] = 0.0;
-        bcast_product<D1, 1>(a7, acc[0], W.Linv + lane * Ly::LD, N);
-        wv[0] = a7[0];
+      for (int s = 0; s < RPL; ++s) {
+        if (rich) {
+          double a7[D1];
 #pragma unroll
-        for (int a = 0; a < D; ++a) pv[0][a] = a7[1 + a];
-      } else {
-        double a1[1] = {0.0}, v1[1] = {acc[0][0]};
-        bcast_product<1, 1>(a1, v1, W.Linv + lane * Ly::LD, N);
-        wv[0] = a1[0];
+          for (int c = 0; c < D1; ++c) a7[c] = 0.0;
+#pragma unroll
+          for (int t = s; t < RPL; ++t)
+            bcast_product<D1, 1>(a7, acc[t], W.Linv + Ly::blk(t, s) * Ly::BLK + lane * Ly::LD, nrows(t));
+          wv[s] = a7[0];
+#pragma unroll
+          for (int a = 0; a < D; ++a) pv[s][a] = a7[1 + a];
+        } else {
+          double a1[1] = {0.0};
+#pragma unroll
+          for (int t = s; t < RPL; ++t) {
+            const double v1[1] = {acc[t][0]};
+            bcast_product<1, 1>(a1, v1, W.Linv + Ly::blk(t, s) * Ly::BLK + lane * Ly::LD, nrows(t));
+          }
+          wv[s] = a1[0];
+        }
       }
     } else {
     // lane i walks column i of L0⁻¹ (= row i of L0⁻ᵀ) in a wave-uniform k loop; Y[k] is an
@@ -1302,8 +1343,8 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
     // packed layouts (E, c and the kernel-row table in global memory): lanes own data rows and
     // the starts run in a loop, so every load is a coalesced row walk (a lane-per-start loop over
     // rows would chain NR dependent global round trips).  Per start the 1 + FMAX base products
-    // [c_S·kxb_k, E_r·kxb_k] are transpose-reduced (two starts per 16-value reduction) into B
-    // (scratch between evaluations), then lane k reads its start's sums.
+    // [c_S·kxb_k, E_r·kxb_k] are transpose-reduced (two starts per 16-value reduction) into the
+    // wave's global scratch (after E / C in its work slot), then lane k reads its start's sums.
     double cv[RPL], ev[RPL][FMAX];
 #pragma unroll
     for (int s2 = 0; s2 < RPL; ++s2) {
@@ -1312,7 +1353,7 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
 #pragma unroll
       for (int r = 0; r < FMAX; ++r) ev[s2][r] = W.E[(long long)r * NR + i];
     }
-    double* sums = W.B;   // [ns][8]
+    double* sums = W.SUMS;   // [ns][8]
     for (int kc = 0; kc < ns; kc += 2) {
       double v[16];
 #pragma unroll
@@ -1340,7 +1381,7 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
     amu = sums[8 * k];
 #pragma unroll
     for (int r = 0; r < FMAX; ++r) ae[r] = sums[8 * k + 1 + r];
-    wave_sync();   // sums read before B is reused
+    wave_sync();   // sums read before the scratch is reused
   } else if (split) {
 #pragma unroll 8
     for (int j = 0; j < NR / 2; ++j) {
@@ -1941,6 +1982,7 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
   if constexpr (Ly::SQ) W.E = W.G12 + Ly::G12;
   else W.E = kp.work + slot * kp.work_stride;
   W.C = W.E + (long long)FMAX * Ly::NR;
+  W.SUMS = W.E + (long long)(2 * FMAX + 1) * Ly::NR;   // packed layouts only (work_stride covers it)
   W.N = kp.N;
   W.Npad = kp.Npad;
   W.rad.kind = kp.kernel;
@@ -2045,7 +2087,10 @@ __global__ void __launch_bounds__(WAVE) start_tables_kernel(KParams kp) {
 #pragma unroll
     for (int s = 0; s < RPL; ++s) {
       const int i = lane + WAVE * s;
-      const double l = (i >= j && i < kp.N) ? kp.Linv[linv_colstart(j, kp.Npad) - j + i] : 0.0;
+      long long li;
+      if constexpr (Ly::BC) li = (long long)Ly::blk(s, j / WAVE) * Ly::BLK + (j % WAVE) * Ly::LD + lane;
+      else li = linv_colstart(j, kp.Npad) - j + i;
+      const double l = (i >= j && i < kp.N) ? kp.Linv[li] : 0.0;
 #pragma unroll
       for (int c = 0; c < D1; ++c) acc[s][c] = fma(l, bj[c], acc[s][c]);
     }

@@ -218,7 +218,8 @@ def test_other_kernels_replay_vs_oracle(gpu, oracle, kernel, kid):
                                    (6, 128, 4), (3, 150, 2), (5, 200, 5), (8, 256, 3)])
 def test_dimensions_and_sizes_replay_vs_oracle(gpu, oracle, d, N, h):
     """d = 1..8 and N up to 256 on Ackley(d): one data row per lane (N ≤ 64, L0⁻¹ square in
-    LDS), two (N ≤ 128, packed in LDS), four (N ≤ 256, L0⁻¹ in global memory); ragged N.  The
+    LDS), two (N ≤ 128, three square 64×64 blocks in LDS), four (N ≤ 256, L0⁻¹ in global memory);
+    ragged N.  The
     lengthscale tracks the design spacing (0.6 · width · N^(-1/d)) so that K is dense: with ℓ = 1
     on Ackley's 65-wide box K ≈ I and the triangular products would multiply zeros."""
     ell = 0.6 * 65.536 * N ** (-1.0 / d)
