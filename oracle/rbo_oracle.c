@@ -636,15 +636,29 @@ static void k_gcert(const kern_t* k, double* gmu, double* gsig) {
 
 /* Gradient certificate from a value-only evaluation: ‖∇α‖∞ ≤ g_tol guaranteed:
  * |∂μ| ≤ Σ|c| max|ψ'|, |∂σ| ≤ √(ψ(0)(−ψ''(0)))/σ, factor 4 for rounding; gμ = gσ = 0 makes
- * ∇α zero or NaN, which stops the iteration as well. */
-static int grad_certified(const solve_ctx* cx, const sx_t* sx) {
+ * ∇α zero or NaN, which stops the iteration as well.  When that cheap bound fails, the tight
+ * one at the point itself: |∂_a μ| ≤ Σ_j |c_j| |ψ'(ρ_j)| over the surface's data rows, and
+ * |∂_a σ| = |∂_a kxᵀK⁻¹kx|/σ ≤ √(−ψ''(0)) √(kxᵀK⁻¹kx)/σ with kxᵀK⁻¹kx = ψ(0) − σ². */
+static int grad_certified(const solve_ctx* cx, const sx_t* sx, const double* x) {
   const double gm = sx->e.gmu, gs = sx->e.gsig;
   if (gm == 0.0 && gs == 0.0) return 1;
   double cmu, csig;
   k_gcert(&cx->fs->k, &cmu, &csig);
   if (!(csig > 0.0)) return 0;
   const double bound = fabs(gm) * cmu * cx->cabs + fabs(gs) * csig / sx->sigma;
-  return bound <= 0.25 * cx->p->g_tol;
+  if (bound <= 0.25 * cx->p->g_tol) return 1;
+  const fsur_t* fs = cx->fs;
+  const int d = fs->d, n = fs->N + cx->fi + 1;
+  const double* c = fs->cs + (int64_t)(cx->fi + 1) * fs->cap;
+  double bmu = 0, r[16];
+  for (int j = 0; j < n; ++j) {
+    for (int a = 0; a < d; ++a) r[a] = x[a] - fs->X[(int64_t)d * j + a];
+    bmu += fabs(c[j]) * fabs(k_dpsi(&fs->k, vnorm(r, d)));
+  }
+  const double psi0 = k_psi(&fs->k, 0.0), d2 = k_d2psi(&fs->k, 0.0);
+  const double q = fmax(psi0 - sx->sigma * sx->sigma, 0.0);
+  const double tight = fabs(gm) * bmu + fabs(gs) * 1.01 * sqrt(-d2) * sqrt(q) / sx->sigma;
+  return tight <= 0.25 * cx->p->g_tol;
 }
 
 static double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -673,7 +687,7 @@ static void newton_solve(solve_ctx* cx, const double* xs, double* xout, double* 
     /* decision point at x; sx holds its value-only evaluation */
     if (it >= p->max_iters) break;
     if (isnan(f)) break;
-    if (grad_certified(cx, &sx)) break;
+    if (grad_certified(cx, &sx, x)) break;
     fsur_eval(fs, x, p->theta, p->sigma_tol, cx->fi, 0, &sx, cx->sc);
     cx->n_grad++;
     for (int a = 0; a < d; ++a) g[a] = -sx.galpha[a];

@@ -239,6 +239,7 @@ static void fill_common(const mrbo_plan_t* P, KParams& kp) {
   kp.nstarts = P->p.nstarts;
   kp.kernel = P->kernel; kp.rule = P->p.rule; kp.ell = P->ell; kp.cK = P->cK; kp.cP = P->cP; kp.psi0 = P->psi0; kp.d2psi0 = P->d2psi0; kp.sn2 = P->sn2;
   kp.gcert_mu = P->gcert_mu; kp.gcert_sig = P->gcert_sig;
+  kp.gcert_d2 = (P->d2psi0 < 0.0) ? 1.01 * std::sqrt(-P->d2psi0) : -1.0;
   kp.fmin_base = P->fmin_base; kp.fmini = P->fmini; kp.theta = P->p.theta;
   kp.max_iters = P->p.max_iters; kp.max_ls = P->p.max_ls;
   kp.x_tol = P->p.x_tol; kp.f_tol = P->p.f_tol; kp.g_tol = P->p.g_tol; kp.htol = P->p.htol;

@@ -43,6 +43,7 @@ struct KParams {
   // gradient certificate (newton_grad_certified): max_ρ |ψ'(ρ)| and √(ψ(0)·(−ψ''(0))), the
   // latter ≤ 0 when the derivative process has no finite variance (Matérn-1/2: disabled)
   double gcert_mu, gcert_sig;
+  double gcert_d2;      // tight certificate: 1.01·√(−ψ''(0)) (used when gcert_sig > 0)
   int max_iters, max_ls;
   double x_tol, f_tol, g_tol, htol, sigma_tol;
   unsigned long long seed;

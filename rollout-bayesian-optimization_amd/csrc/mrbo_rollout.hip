@@ -1128,6 +1128,59 @@ __device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const K
   return ((gm == 0.0) & (gs == 0.0)) | ((kp.gcert_sig > 0.0) & (bound <= 0.25 * kp.g_tol));
 }
 
+// Tight certificate at x = U[U_X] on surface S, where grad_certified's cheap bound failed
+// (gμ, gσ, σ of the value evaluation at x).  At the point itself:
+//   |∂_a μ| = |Σ_j c_j g1_j (x − X_j)_a| ≤ Σ_j |c_j| |ψ'(ρ_j)|  over base and fantasy rows,
+//   |∂_a σ| ≤ √(−ψ''(0)) √(kxᵀK⁻¹kx) / σ  with kxᵀK⁻¹kx = ψ(0) − σ²,
+// i.e. the cheap bound with max|ψ'| replaced by the actual |ψ'(ρ_j)| and ψ(0) by the explained
+// variance; far from the data both vanish.  One radial evaluation per row and one reduction --
+// instead of the gradient columns (O(N²d)).  Factor 4 for rounding, as above; the oracle
+// (rbo_oracle.c grad_certified) applies the same test.
+template <int D, int RPL>
+__device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParams& kp, int S, double gm, double gs,
+                                                double sig) {
+  using Ly = Lay<D, RPL>;
+  constexpr int NR = Ly::NR;
+  const double* U = W.U;
+  const int lane = W.ln();
+  const int nf = S + 1;
+  // the σ part needs no rows: if it alone exceeds the threshold the test fails, and with the
+  // cheap μ part (Σ|c|·max|ψ'| ≥ the row sum) it may already pass -- same decisions as the
+  // full test, without the row pass
+  const double q = fmax(kp.psi0 - sig * sig, 0.0);
+  const double bsig = fabs(gs) * kp.gcert_d2 * sqrt(q) / sig, thr = 0.25 * kp.g_tol;
+  if (!(bsig <= thr)) return false;
+  if (fabs(gm) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + bsig <= thr) return true;
+  double x[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) x[a] = U[Ly::U_X + a];
+  double v[1] = {0.0};
+#pragma unroll
+  for (int s = 0; s < RPL; ++s) {
+    double rho2 = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) { const double r = x[a] - W.X0[s][a]; rho2 = fma(r, r, rho2); }
+    double psi, g1, g2;
+    rad_eval(W.rad, rho2, psi, g1, g2);
+    const double cb = W.C[(long long)(S + 1) * NR + lane + WAVE * s];
+    v[0] += W.valid[s] ? fabs(cb) * fabs(g1) * sqrt(rho2) : 0.0;
+  }
+  if (lane < nf) {
+    double rho2 = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) { const double r = x[a] - U[Ly::U_XF + lane * D + a]; rho2 = fma(r, r, rho2); }
+    double psi, g1, g2;
+    rad_eval(W.rad, rho2, psi, g1, g2);
+    v[0] += fabs(U[Ly::U_CF + (S + 1) * FMAX + lane]) * fabs(g1) * sqrt(rho2);
+  }
+  wave_sync();
+  wave_reduce<1>(v, W.red, lane);
+  wave_sync();
+  const double bmu = W.red[0];
+  wave_sync();
+  return fabs(gm) * bmu + bsig <= thr;
+}
+
 // Deterministic projected Newton on f = -α over the box, from start k.
 // A state machine around ONE evaluate() call site.  Work is lazy, decisions are not: every
 // point gets a value-only evaluation; the gradient columns are completed (GRADC) only where
@@ -1137,7 +1190,8 @@ __device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const K
 // counts equal the oracle's (rbo_oracle.c newton_solve).  Result: x in U_NX, f returned.
 template <int D, int RPL>
 __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, int S, int k, Counters& nevals,
-                                         int& st, LaneRes<D, RPL>& lr, double f0, bool have_f0) {
+                                         int& st, LaneRes<D, RPL>& lr, double f0, bool have_f0, double gm0 = 0.0,
+                                         double gs0 = 0.0, double sig0 = 0.0) {
   using Ly = Lay<D, RPL>;
   double* U = W.U;
   const int lane = W.ln();
@@ -1148,6 +1202,12 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
     U[Ly::U_X + lane] = xa;
   }
   wave_sync();
+  // a batched start whose cheap certificate failed: the tight one at x_start (gμ, gσ, σ of the
+  // batched value) before any gradient work
+  if (have_f0 && kp.gcert_sig > 0.0 && tight_certified<D, RPL>(W, kp, S, gm0, gs0, sig0)) {
+    wave_sync();
+    return f0;
+  }
   // have_f0: the start's value (and certificate) came from batch_start_values and did not
   // stop the iteration, so it begins with the gradient at x_start
   // (GSTART takes the base forward product from the square layout's per-workgroup tables; the
@@ -1214,6 +1274,9 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
     if (it >= kp.max_iters) break;
     if (f != f) break;
     if (grad_certified<D, RPL>(W, kp)) break;     // ‖∇α‖ ≤ g_tol guaranteed: stationary
+    if (kp.gcert_sig > 0.0 &&
+        tight_certified<D, RPL>(W, kp, S, U[Ly::U_SC + SC_GMU], U[Ly::U_SC + SC_GSIG], U[Ly::U_SC + SC_SIG]))
+      break;
     STAMP(W, 12);
     phase = P_GRAD;
     mode = EV_GRADC;
@@ -1309,6 +1372,7 @@ __device__ __forceinline__ void stage_start_tables(const KParams& kp, double* sm
 // Replaces nstarts value evaluations (and their wave-redundant EI) by one pass.
 template <int D, int RPL>
 __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KParams& kp, int S, double& f_lane,
+                                                   double& gm_lane, double& gs_lane, double& sig_lane,
                                                    unsigned long long& stopmask, unsigned long long& xnanmask,
                                                    bool& varneg) {
   using Ly = Lay<D, RPL>;
@@ -1457,6 +1521,9 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   if (!cert && kp.gcert_sig > 0.0)
     cert = fabs(e.gmu) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + fabs(e.gsig) * kp.gcert_sig / sig <= 0.25 * kp.g_tol;
   f_lane = -e.g;
+  gm_lane = e.gmu;
+  gs_lane = e.gsig;
+  sig_lane = sig;
   // the iteration stops at the start point: certified, f NaN, or no iterations allowed
   const bool stop = cert || (f_lane != f_lane) || kp.max_iters <= 0;
   bool xn = false;
@@ -1490,12 +1557,12 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
     if (lane == 0) U[Ly::U_SC + SC_CABS] = cabs;
     wave_sync();
   }
-  double f_lane = 0.0;
+  double f_lane = 0.0, gm_lane = 0.0, gs_lane = 0.0, sig_lane = 0.0;
   unsigned long long stopmask = 0, xnanmask = 0;
   if (kp.batch) {
     bool varneg = false;
     STAMP(W, 16);
-    batch_start_values<D, RPL>(W, kp, S, f_lane, stopmask, xnanmask, varneg);
+    batch_start_values<D, RPL>(W, kp, S, f_lane, gm_lane, gs_lane, sig_lane, stopmask, xnanmask, varneg);
     STAMP(W, 15);
     nevals.value += kp.nstarts;
     if (varneg) st |= 1;
@@ -1504,7 +1571,8 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
   // starts that need a Newton iteration, in index order (all of them without kp.batch)
   for (int k = 0; k < kp.nstarts; ++k) {
     if ((stopmask >> k) & 1ull) continue;
-    const double fo = kp.batch ? newton<D, RPL>(W, kp, S, k, nevals, st, lr, readlane_d(f_lane, k), true)
+    const double fo = kp.batch ? newton<D, RPL>(W, kp, S, k, nevals, st, lr, readlane_d(f_lane, k), true,
+                                                readlane_d(gm_lane, k), readlane_d(gs_lane, k), readlane_d(sig_lane, k))
                                : newton<D, RPL>(W, kp, S, k, nevals, st, lr, 0.0, false);
     bool xnan = false;
 #pragma unroll
