@@ -240,3 +240,37 @@ def test_eval_base_periodic_fd(oracle):
     np.testing.assert_allclose(o[3:3 + d], _fd(lambda xx: col(xx)[0], x), rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(o[3 + d:3 + 2 * d], _fd(lambda xx: col(xx)[1], x), rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(o[3 + 2 * d:3 + 3 * d], _fd(lambda xx: col(xx)[2], x), rtol=1e-6, atol=1e-10)
+
+
+@pytest.mark.parametrize("case", ["c2", "c2near"])
+def test_tight_gradient_certificate_bounds_the_gradient(oracle, case):
+    """The tight certificate (rbo_oracle.c grad_certified, mrbo_rollout.hip tight_certified) stops
+    the Newton iteration without computing ∇α; it is rigorous only if, at every x,
+      ‖∇α‖∞ ≤ |gμ| Σ_j |c_j| |ψ'(ρ_j)| + |gσ| √(−ψ''(0)) √(ψ(0) − σ²) / σ.
+    Checked here against the oracle's own ∇α at points spread over the box and next to the data."""
+    from mrbo.kernels import Matern52
+    from scipy.special import erfc
+    g = load_golden(case)
+    s = _osur(oracle, g)
+    X, c = g["X"], g["c"]
+    d, N = X.shape
+    ell = float(g.get("ell", 1.0))
+    k = Matern52([ell])
+    rng = np.random.default_rng(7)
+    lbs, ubs = g["lbs"], g["ubs"]
+    far = lbs[:, None] + (ubs - lbs)[:, None] * rng.random((d, 200))
+    near = X[:, rng.integers(0, N, 200)] + 1e-2 * (ubs - lbs)[:, None] * rng.standard_normal((d, 200))
+    pts = np.asfortranarray(np.clip(np.hstack([far, near]), lbs[:, None], ubs[:, None]))
+    o = oracle.eval_base(s, pts)
+    mu, sig, galpha = o[0], o[1], o[3 + 2 * d:3 + 3 * d]
+    fmin = float(np.min(g["y"]))
+    z = (fmin - mu) / sig
+    gm = -0.5 * erfc(-z / np.sqrt(2.0))
+    gs = np.exp(-0.5 * z * z) / np.sqrt(2 * np.pi)
+    rho = np.sqrt(((pts[:, None, :] - X[:, :, None]) ** 2).sum(axis=0))     # N × P
+    bmu = (np.abs(c)[:, None] * np.abs(k.derivative(rho))).sum(axis=0)
+    d2 = -5.0 / (3.0 * ell * ell)
+    bsig = np.sqrt(-d2) * np.sqrt(np.maximum(1.0 - sig * sig, 0.0)) / sig
+    bound = np.abs(gm) * bmu + np.abs(gs) * bsig
+    assert np.all(np.abs(galpha).max(axis=0) <= bound * (1 + 1e-9) + 1e-300)
+    assert np.median(bound / np.maximum(np.abs(galpha).max(axis=0), 1e-300)) < 1e6   # not vacuous
