@@ -1,6 +1,6 @@
 #!/bin/bash
-# Build A/B variants of libmrbo.so (d=6 only) into mrbo/variants/ for timing on the GPU box.
-# usage: tools/build_variants.sh name:"-DFLAG ..." [name:"..."] ...   (default: base + stamps)
+# Build A/B variants of libmrbo.so (one input dimension, default d=6) into mrbo/variants/ for timing
+# on the GPU box.  usage: [MRBO_VARIANT_DIMS=8] tools/build_variants.sh name:"-DFLAG ..." [name:"..."] ...   (default: base + stamps)
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p rollout-bayesian-optimization_amd/mrbo/variants
@@ -11,7 +11,9 @@ for spec in "$@"; do
 import shlex, sys
 import __graft_entry__ as g
 name, flags = sys.argv[1], sys.argv[2]
-g.compile_lib(f"{g.PKG}/mrbo/variants/libmrbo_{name}.so", extra=shlex.split(flags), dims=[6], jobs=2)
+import os
+dims = [int(x) for x in os.environ.get("MRBO_VARIANT_DIMS", "6").split(",")]
+g.compile_lib(f"{g.PKG}/mrbo/variants/libmrbo_{name}.so", extra=shlex.split(flags), dims=dims, jobs=2)
 PY
 done
 wait
