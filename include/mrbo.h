@@ -193,6 +193,10 @@ double mrbo_dual_uniform(uint64_t seed, int64_t traj, int32_t j, int32_t k);
 /* Timing of the last mrbo_simulate_mc kernel on its stream (HIP events), milliseconds. */
 double mrbo_last_kernel_ms(mrbo_plan_t* plan);
 
+/* Kernel time of the last mrbo_gp_fit launch (HIP events around it), milliseconds; -1 before
+ * the first call.  Process-wide (the last call on any stream). */
+double mrbo_last_gp_fit_ms(void);
+
 /* Launch geometry of a plan (no reference counterpart; measurement and FLOP accounting):
  * info[0..5] = rows per lane (1/2/4), workgroups, waves per workgroup, batched start values
  * (0/1), compile-time specialised kernel (0/1), LDS bytes per workgroup.  Writes min(n, 6). */

@@ -73,6 +73,8 @@ struct mrbo_plan {
 
 namespace {
 
+double g_gpfit_ms = -1.0;   // kernel time of the last mrbo_gp_fit (HIP events around the launch)
+
 // ---- kernel dispatch: one translation unit per input dimension (mrbo_kernels.hip) -------
 bool get_kset(int d, int rpl, KernelSet& ks) {
 #define CASE_(DD) \
@@ -648,14 +650,27 @@ int mrbo_gp_fit(const mrbo_surrogate_t* s, int32_t np, const double* ells, doubl
   }
   const double *dX = nullptr, *dy = nullptr;
   if (sg.in(s->X, (size_t)d * N, &dX) || sg.in(s->y, (size_t)N, &dy)) return fail(MRBO_ERR_NOMEM, "staging X, y");
-  double* work = nullptr;
-  if (hipMalloc(&work, sizeof(double) * 3 * NN * P) != hipSuccess) return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
-  sg.bufs.push_back(work);
+  double* work = nullptr;   // N ≤ 64 runs in LDS (gpfit_wave_kernel): no workspace
+  if (!gpfit_in_lds(N, d)) {
+    if (hipMalloc(&work, sizeof(double) * 3 * NN * P) != hipSuccess) return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
+    sg.bufs.push_back(work);
+  }
   GpFitParams q{d, N, s->kernel, s->sigma_n2, dX, dy, dells, dll_, ddll, (int*)dst, dL, dc, work};
+  static hipEvent_t gev[2] = {nullptr, nullptr};
+  if (!gev[0]) {
+    HIP_TRY(hipEventCreate(&gev[0]));
+    HIP_TRY(hipEventCreate(&gev[1]));
+  }
+  HIP_TRY(hipEventRecord(gev[0], st));
   launch_gpfit(np, st, q);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(gev[1], st));
   // the staging buffers and the workspace are freed on return: finish the launch first
   HIP_TRY(hipStreamSynchronize(st));
+  {
+    float ms = -1.f;
+    if (hipEventElapsedTime(&ms, gev[0], gev[1]) == hipSuccess) g_gpfit_ms = ms;
+  }
   if (flags & MRBO_FLAG_HOST_POINTERS) {
     HIP_TRY(hipMemcpy(ll, dll_, sizeof(double) * P, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(dll, ddll, sizeof(double) * P, hipMemcpyDeviceToHost));
@@ -665,6 +680,8 @@ int mrbo_gp_fit(const mrbo_surrogate_t* s, int32_t np, const double* ells, doubl
   }
   return MRBO_OK;
 }
+
+double mrbo_last_gp_fit_ms(void) { return g_gpfit_ms; }
 
 int mrbo_plan_info(const mrbo_plan_t* P, int32_t* info, int32_t n) {
   if (!P || !info || n < 0) return fail(MRBO_ERR_ARG, "bad arguments");

@@ -46,5 +46,7 @@ struct GpFitParams {
   double* work;        // 3·N²·P
 };
 void launch_gpfit(int P, hipStream_t st, const GpFitParams& q);
+// N ≤ 64 (and d ≤ 8): the one-wave-per-candidate kernel with the matrices in LDS (no workspace)
+inline bool gpfit_in_lds(int N, int d) { return N <= 64 && d <= 8; }
 
 }  // namespace mrbo
