@@ -130,3 +130,25 @@ def test_eswavs_and_optimizers():
     a, x = Adam(η=0.1), np.zeros(2)
     a.update(x, np.array([1.0, -1.0]))
     np.testing.assert_allclose(x, [0.1, -0.1], rtol=1e-6)
+
+
+def test_flop_model_batched_starts():
+    """flops.launch_flops: the h·nstarts batched start values per trajectory are charged at the
+    batched pass's cost plus the start tables (once per workgroup for the square layout, once per
+    launch for the packed ones), not as full value evaluations."""
+    from mrbo import flops
+    N, d, h, ns, M = 64, 6, 3, 18, 10
+    ev = np.zeros((flops.NCOUNTERS, M))
+    ev[1] = h * ns + 5          # 54 batched + 5 line-search values per trajectory
+    ev[0], ev[2] = 4, 4
+    plain = flops.launch_flops(ev, N, d, h)
+    nf = (1 + h) / 2.0
+    sq = dict(rpl=1, blocks=256, batch=1)
+    got = flops.launch_flops(ev, N, d, h, info=sq, nstarts=ns)
+    nb = h * ns * M
+    want = plain - nb * flops.f_value(N, nf, d) + nb * flops.f_batch_start(N, nf, d) + 256 * ns * flops.f_start_table(N, d)
+    assert got == pytest.approx(want, rel=1e-12)
+    packed = flops.launch_flops(ev, N, d, h, info=dict(rpl=2, blocks=256, batch=1), nstarts=ns)
+    assert packed == pytest.approx(want - 255 * ns * flops.f_start_table(N, d), rel=1e-12)
+    assert flops.launch_flops(ev, N, d, h, info=dict(rpl=1, blocks=256, batch=0), nstarts=ns) == plain
+    assert flops.f_batch_start(N, nf, d) < flops.f_value(N, nf, d) / 5
