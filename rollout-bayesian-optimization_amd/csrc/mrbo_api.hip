@@ -391,13 +391,19 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   std::vector<double> packed((size_t)ks.linv_dev, 0.0);
   for (int j = 0; j < N; ++j)
     for (int i = j; i < N; ++i) {
+      const size_t blk = (size_t)(i / 64) * (i / 64 + 1) / 2 + j / 64;   // block (i/64, j/64), j/64 ≤ i/64
       size_t at;
-      if (ks.blocks)   // block (s,t) = (i/64, j/64) at (s(s+1)/2 + t)·64·ld, column-major inside
-        at = ((size_t)(i / 64) * (i / 64 + 1) / 2 + j / 64) * 64 * ks.ld + (size_t)(j % 64) * ks.ld + i % 64;
+      if (ks.blocks)   // LDS blocks, column-major inside with leading dimension ld
+        at = blk * 64 * ks.ld + (size_t)(j % 64) * ks.ld + i % 64;
+      else if (ks.gl)  // L2 blocks, forward copy: (i, j) at j·64 + i
+        at = blk * 64 * 64 + (size_t)(j % 64) * 64 + i % 64;
       else
-        at = ks.square ? (size_t)j * ks.ld + i : (size_t)linv_colstart(j, Npad) + (i - j);
+        at = (size_t)j * ks.ld + i;
       packed[at] = Li[i + (size_t)N * j];
-      if (ks.gl) packed[(size_t)linv_size(Npad) + (size_t)i * (i + 1) / 2 + j] = Li[i + (size_t)N * j];
+      if (ks.gl) {     // backward copy (after all forward blocks): (i, j) at i·64 + j
+        const size_t nblk = (size_t)P->RPL * (P->RPL + 1) / 2;
+        packed[(nblk + blk) * 64 * 64 + (size_t)(i % 64) * 64 + j % 64] = Li[i + (size_t)N * j];
+      }
     }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete P; return fail(MRBO_ERR_HIP, "device props"); }

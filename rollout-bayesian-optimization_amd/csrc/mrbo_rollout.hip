@@ -32,7 +32,7 @@ struct Lay {
   // additionally keeps the per-wave E / C rows and the start tables in LDS.
   static constexpr bool SQ = (RPL == 1);
   static constexpr bool BC = (RPL <= 2);
-  static constexpr int FR0 = BC ? 0 : NR;          // first fantasy row in B
+  static constexpr int FR0 = 0;                    // first fantasy row in B (base rows stay in registers)
   static constexpr int BROWS = FR0 + FMAX;         // [base rows +] fantasy rows
   static constexpr int NG = D1 * (D1 + 1) / 2;     // Gram entries (a ≤ b)
   static constexpr int NH = D * (D + 1) / 2;       // Hessian entries (a ≤ b)
@@ -100,7 +100,9 @@ struct Lay {
   // are coalesced 512-byte loads
   static constexpr bool GL = (RPL > 2);
   static constexpr long long LINV_DOUBLES = GL ? 0 : (((BC ? (long long)NBLK * BLK : linv_size(NR)) + 1) & ~1LL);
-  static constexpr long long LINV_GLOBAL = GL ? 2 * linv_size(NR) : LINV_DOUBLES;  // device image
+  // device image; GL: the NBLK blocks twice, 64×64 each with the lane index fastest -- forward
+  // copy (i, j) at j·64 + i, backward copy (k, i) at k·64 + i -- zero-padded
+  static constexpr long long LINV_GLOBAL = GL ? 2LL * NBLK * WAVE * WAVE : LINV_DOUBLES;
 };
 // scalar slots in U_SC
 enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, SC_GSIG = 6, SC_GMUMU = 7,
@@ -133,8 +135,8 @@ struct WaveCtx {
   double* B;            // LDS: BROWS × BS
   double* red;          // LDS: REDN
   double* U;            // LDS: U_SIZE
-  const double* Linv;   // L0⁻¹: LDS (Lay::SQ square or packed columns) or global packed columns (GL)
-  const double* LinvT;  // GL: global L0⁻¹ packed by rows (row k: entries 0..k)
+  const double* Linv;   // L0⁻¹: LDS blocks (BC) or the forward copy of the global blocks (GL)
+  const double* LinvT;  // GL: the backward copy of the global L0⁻¹ blocks
   const double* XS;     // inner-solve start points: LDS copy (kp.xs_lds) or kp.xstarts
   const double* KXB;    // ψ(|clamp(x_k) − X_i|) (kp.batch): LDS [NR][nstarts]; packed layouts: global [nstarts][NR]
   const double* GTAB;   // [nstarts][NG]: base Gram of the start points (kp.batch; LDS, global for packed)
@@ -238,6 +240,37 @@ __device__ __forceinline__ void bcast_product(double (&acc)[K], const double (&v
   }
 }
 
+// The same product with this lane's L entries from global memory (L2-resident image):
+// step n of the block at lb[n·64].  All 64 steps of both row blocks of a pass are loaded into
+// registers before their FMAs (the image is zero-padded, so the loads need no bounds).
+template <int K>
+__device__ __forceinline__ void gl_bcast_product(double (&acc)[K], const double (&v)[K], const double* lb, int nrows) {
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    if (16 * p >= nrows) break;
+    double l[4][8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      l[0][u] = lb[(16 * p + u) * WAVE];
+      l[1][u] = lb[(16 * p + 8 + u) * WAVE];
+      l[2][u] = lb[(16 * (p + 2) + u) * WAVE];
+      l[3][u] = lb[(16 * (p + 2) + 8 + u) * WAVE];
+    }
+    double bp[K], bp2[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      if (p == 0) row_blocks<0>(v[c], bp[c], bp2[c]);
+      else row_blocks<1>(v[c], bp[c], bp2[c]);
+    }
+    BcastRegAsm<K, 0>::run(acc, bp, l[0]);
+    BcastRegAsm<K, 8>::run(acc, bp, l[1]);
+    if (16 * (p + 2) < nrows) {
+      BcastRegAsm<K, 0>::run(acc, bp2, l[2]);
+      BcastRegAsm<K, 8>::run(acc, bp2, l[3]);
+    }
+  }
+}
+
 // ================================================================================
 // eval(fs, x, θ; fantasy_index = S)  -- radial_basis_surrogates.jl:482-581
 //   x is read from U[U_X].  Results land in U (lane-uniform) and `lr` (per lane).
@@ -296,11 +329,6 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       Bown[s][0] = 0.0;   // column 0 comes from the VALUE pass
 #pragma unroll
       for (int a = 0; a < D; ++a) Bown[s][1 + a] = v ? g1 * r[a] : 0.0;
-      if constexpr (!Ly::BC) {
-        double* row = B + (lane + WAVE * s) * BS;
-#pragma unroll
-        for (int a = 0; a < D; ++a) row[1 + a] = Bown[s][1 + a];
-      }
       continue;
     }
     double psi, g1, g2;
@@ -321,15 +349,6 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     for (int a = 0; a < D; ++a) Bown[s][1 + a] = v ? g1 * r[a] : 0.0;
     W.G12[3 * (lane + WAVE * s)] = g1;       // kept for a Hessian (phase 6, maybe deferred)
     W.G12[3 * (lane + WAVE * s) + 1] = g2;
-    if constexpr (!Ly::BC) {   // the LDS row-broadcast path reads the base rows from B
-      double* row = B + (lane + WAVE * s) * BS;
-      if (all_cols) {
-#pragma unroll
-        for (int c = 0; c < D1; ++c) row[c] = Bown[s][c];
-      } else {
-        row[0] = Bown[s][0];
-      }
-    }
   }
   if (lane < nf && !rows_kept) {  // fantasy rows B[N + r]; [x − X_r, g1, g2] kept for the Hessian
     double r[D], psi, g1, g2;
@@ -410,45 +429,45 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
           bcast_product<D1, Ly::LD>(acc[s], Bown[t], W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
     }
   } else {
-  // L0⁻¹[i][j] for this lane's row i = lane + 64s.  Row block s needs columns j < 64(s+1) only
-  // (j-blocks jb ≤ s); inside the diagonal block the entries above the diagonal read as zero.
-  // Skipping the all-zero blocks leaves every accumulation order unchanged.
-  auto lfwd = [&](int s, int jb, int j) -> double {
-    const int i = lane + WAVE * s;
-    if (s > jb) return W.Linv[linv_colstart(j, W.Npad) - j + i];
-    const double l = W.Linv[linv_colstart(j, W.Npad) - j + (i > j ? i : j)];
-    return (i >= j) ? l : 0.0;
-  };
-  if (all_cols) {
+    // GL (N ≤ 256): the same register broadcast with L0⁻¹ from L2: lane i reads (i, j) of block
+    // (s,t) at blk(s,t)·4096 + j·64 + i, 16 steps' entries loaded ahead into registers
+    auto nrows = [&](int t) { const int n = N - WAVE * t; return n < WAVE ? n : WAVE; };
+    const double* L0 = W.Linv + lane;
+    if (mode == EV_VALUE) {
 #pragma unroll
-    for (int jb = 0; jb < RPL; ++jb) {
-      const int j1 = (N < WAVE * (jb + 1)) ? N : WAVE * (jb + 1);
-#pragma unroll 4
-      for (int j = WAVE * jb; j < j1; ++j) {
-        const double* bj = B + j * BS;
-        double bv[D1];
+      for (int s = 0; s < RPL; ++s) {
+        double a1[1] = {0.0};
 #pragma unroll
-        for (int c = 0; c < D1; ++c) bv[c] = bj[c];
-#pragma unroll
-        for (int s = jb; s < RPL; ++s) {
-          const double l = lfwd(s, jb, j);
-#pragma unroll
-          for (int c = 0; c < D1; ++c) acc[s][c] = fma(l, bv[c], acc[s][c]);
+        for (int t = 0; t <= s; ++t) {
+          const double v1[1] = {Bown[t][0]};
+          gl_bcast_product<1>(a1, v1, L0 + Ly::blk(s, t) * WAVE * WAVE, nrows(t));
         }
+        acc[s][0] = a1[0];
       }
-    }
-  } else {
+    } else if (mode == EV_GRADC) {
 #pragma unroll
-    for (int jb = 0; jb < RPL; ++jb) {
-      const int j1 = (N < WAVE * (jb + 1)) ? N : WAVE * (jb + 1);
-#pragma unroll 8
-      for (int j = WAVE * jb; j < j1; ++j) {
-        const double b0 = B[j * BS];
+      for (int s = 0; s < RPL; ++s) {
+        double ag[D];
 #pragma unroll
-        for (int s = jb; s < RPL; ++s) acc[s][0] = fma(lfwd(s, jb, j), b0, acc[s][0]);
+        for (int a = 0; a < D; ++a) ag[a] = 0.0;
+#pragma unroll
+        for (int t = 0; t <= s; ++t) {
+          double vg[D];
+#pragma unroll
+          for (int a = 0; a < D; ++a) vg[a] = Bown[t][1 + a];
+          gl_bcast_product<D>(ag, vg, L0 + Ly::blk(s, t) * WAVE * WAVE, nrows(t));
+        }
+#pragma unroll
+        for (int a = 0; a < D; ++a) acc[s][1 + a] = ag[a];
+        acc[s][0] = W.G12[3 * (lane + WAVE * s) + 2];
       }
+    } else {
+#pragma unroll
+      for (int s = 0; s < RPL; ++s)
+#pragma unroll
+        for (int t = 0; t <= s; ++t)
+          gl_bcast_product<D1>(acc[s], Bown[t], L0 + Ly::blk(s, t) * WAVE * WAVE, nrows(t));
     }
-  }
   }
 
   if (do_val) {   // Y0 kept for a deferred GRADC / BACK evaluation
@@ -649,20 +668,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
 
   STAMP(W, 4);
   // ---- 5. backward product w = L⁻ᵀ v (and P = L⁻ᵀ V for the adjoint)
-  // stash Y rows (base) into B, then lane i walks column i of L0⁻¹
   const bool rich = (mode == EV_RICH);
-  if constexpr (!Ly::BC) {
-#pragma unroll
-    for (int s = 0; s < RPL; ++s) {
-      double* row = B + (lane + WAVE * s) * BS;
-      row[0] = acc[s][0];
-      if (rich) {
-#pragma unroll
-        for (int a = 0; a < D; ++a) row[1 + a] = acc[s][1 + a];
-      }
-    }
-    wave_sync();
-  }
   {
     double wv[RPL], pv[RPL][D];
 #pragma unroll
@@ -698,53 +704,31 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
         }
       }
     } else {
-    // lane i walks column i of L0⁻¹ (= row i of L0⁻ᵀ) in a wave-uniform k loop; Y[k] is an
-    // LDS broadcast.  Row block s needs k ≥ 64s only (k-blocks kb ≥ s); L0⁻¹[k][i] is zero for
-    // k < i and on padded rows.  GL reads the row-packed global copy (coalesced in i).
-    auto lbwd = [&](int s, int kb, int k) -> double {
-      const int i = lane + WAVE * s;
-      if constexpr (Ly::GL) {
-        const long long rs = (long long)k * (k + 1) / 2;
-        if (s < kb) return W.LinvT[rs + i];
-        const double l = W.LinvT[rs + (i < k ? i : k)];
-        return (k >= i) ? l : 0.0;
-      } else {
-        if (s < kb) return W.Linv[linv_colstart(i, W.Npad) - i + k];
-        const double l = W.Linv[linv_colstart(i, W.Npad) - i + (k > i ? k : i)];
-        return (k >= i) ? l : 0.0;
-      }
-    };
-    if (rich) {
+      // GL: lane i (row slot s) reads (k, i) of block (t,s) from the backward copy at
+      // blk(t,s)·4096 + k·64 + i; rows k of Y from register slot t
+      auto nrows = [&](int t) { const int n = N - WAVE * t; return n < WAVE ? n : WAVE; };
+      const double* LT = W.LinvT + lane;
 #pragma unroll
-      for (int kb = 0; kb < RPL; ++kb) {
-        const int k1 = (N < WAVE * (kb + 1)) ? N : WAVE * (kb + 1);
-#pragma unroll 2
-        for (int k = WAVE * kb; k < k1; ++k) {
-          const double* yk = B + k * BS;
-          double yv[D1];
+      for (int s = 0; s < RPL; ++s) {
+        if (rich) {
+          double a7[D1];
 #pragma unroll
-          for (int c = 0; c < D1; ++c) yv[c] = yk[c];
+          for (int c = 0; c < D1; ++c) a7[c] = 0.0;
 #pragma unroll
-          for (int s = 0; s <= kb; ++s) {
-            const double l = lbwd(s, kb, k);
-            wv[s] = fma(l, yv[0], wv[s]);
+          for (int t = s; t < RPL; ++t) gl_bcast_product<D1>(a7, acc[t], LT + Ly::blk(t, s) * WAVE * WAVE, nrows(t));
+          wv[s] = a7[0];
 #pragma unroll
-            for (int a = 0; a < D; ++a) pv[s][a] = fma(l, yv[1 + a], pv[s][a]);
+          for (int a = 0; a < D; ++a) pv[s][a] = a7[1 + a];
+        } else {
+          double a1[1] = {0.0};
+#pragma unroll
+          for (int t = s; t < RPL; ++t) {
+            const double v1[1] = {acc[t][0]};
+            gl_bcast_product<1>(a1, v1, LT + Ly::blk(t, s) * WAVE * WAVE, nrows(t));
           }
+          wv[s] = a1[0];
         }
       }
-    } else {
-#pragma unroll
-      for (int kb = 0; kb < RPL; ++kb) {
-        const int k1 = (N < WAVE * (kb + 1)) ? N : WAVE * (kb + 1);
-#pragma unroll 8
-        for (int k = WAVE * kb; k < k1; ++k) {
-          const double y0 = B[k * BS];
-#pragma unroll
-          for (int s = 0; s <= kb; ++s) wv[s] = fma(lbwd(s, kb, k), y0, wv[s]);
-        }
-      }
-    }
     }
     // fantasy part: + Σ_r E[r][i] Yf[r]
 #pragma unroll
@@ -2063,7 +2047,7 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
   W.U = W.red + Ly::REDN;
   W.G12 = W.U + Ly::U_SIZE;
   W.Linv = Ly::GL ? kp.Linv : smem;
-  W.LinvT = kp.Linv + linv_size(Ly::NR);
+  W.LinvT = kp.Linv + (long long)Ly::NBLK * WAVE * WAVE;   // GL: backward copy
   const long long slot = (long long)blockIdx.x * (blockDim.x / WAVE) + wave_in_block;
   if constexpr (Ly::SQ) W.E = W.G12 + Ly::G12;
   else W.E = kp.work + slot * kp.work_stride;
@@ -2176,7 +2160,7 @@ __global__ void __launch_bounds__(WAVE) start_tables_kernel(KParams kp) {
       const int i = lane + WAVE * s;
       long long li;
       if constexpr (Ly::BC) li = (long long)Ly::blk(s, j / WAVE) * Ly::BLK + (j % WAVE) * Ly::LD + lane;
-      else li = linv_colstart(j, kp.Npad) - j + i;
+      else li = (long long)Ly::blk(s, j / WAVE) * WAVE * WAVE + (j % WAVE) * WAVE + lane;
       const double l = (i >= j && i < kp.N) ? kp.Linv[li] : 0.0;
 #pragma unroll
       for (int c = 0; c < D1; ++c) acc[s][c] = fma(l, bj[c], acc[s][c]);
