@@ -107,7 +107,6 @@ struct Lay {
 // scalar slots in U_SC
 enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, SC_GSIG = 6, SC_GMUMU = 7,
        SC_GSIGSIG = 8, SC_GMUTH = 9, SC_GSIGTH = 10, SC_FMIN = 11, SC_ST = 12, SC_CABS = 13 };
-constexpr int NBST = 9;   // per-start batched values kept for GSTART: σ, σ², g, gμ, gσ, gμμ, gσσ, gμθ, gσθ
 
 // Per-workgroup LDS after L0⁻¹: [xstarts (d×nstarts)] [kxb (NR×nstarts)] [gtab (nstarts×NG)],
 // each rounded to an even number of doubles; then the per-wave areas.  gtab[k] is the base
@@ -145,7 +144,6 @@ struct WaveCtx {
   double* E;            // LDS (SQ) or global: FMAX × NR  inverse-factor fantasy rows (base columns)
   double* C;            // LDS (SQ) or global: (FMAX+1) × NR  base part of c for surfaces -1..h
   double* SUMS;         // packed layouts: global [64][8] per-start sums of the batched start pass
-  double* BST;          // global [NBST][64]: per-start σ, σ², EI and partials of the batched pass (GSTART)
   double X0[RPL][D];    // own base rows
   bool valid[RPL];
   int N, Npad;
@@ -614,7 +612,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   // ---- σ, EI partials (all lanes, wave-uniform values)
   double sig_f;
   EIp e_f;
-  if (do_val && mode != EV_GSTART) {
+  if (do_val) {
   const double mu = mu_v;
   const double var = kp.psi0 - g00_v;
   const double sig = sqrt(var);
@@ -635,7 +633,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   if (mode == EV_VALUE) { wave_sync(); STAMP(W, 4); return; }
   sig_f = sig;
   e_f = e;
-  } else {   // GRADC: σ and the EI partials of the VALUE pass at this point; GSTART: of the batch
+  } else {   // GRADC: σ and the EI partials of the VALUE pass at this point
     sig_f = U[Ly::U_SC + SC_SIG];
     e_f.gmu = U[Ly::U_SC + SC_GMU];
     e_f.gsig = U[Ly::U_SC + SC_GSIG];
@@ -1194,17 +1192,6 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
     wave_sync();
     return f0;
   }
-  if (have_f0) {   // σ, EI and its partials at x_start from the batched pass: GSTART skips them
-    static_assert(SC_GSIG == SC_GMU + 1 && SC_GMUMU == SC_GMU + 2 && SC_GSIGSIG == SC_GMU + 3 &&
-                  SC_GMUTH == SC_GMU + 4 && SC_GSIGTH == SC_GMU + 5, "U_SC partials order");
-    if (lane < NBST) {
-      const double v = W.BST[lane * WAVE + k];
-      // BST order: σ, σ², g, gμ, gσ, gμμ, gσσ, gμθ, gσθ
-      const int slot = (lane == 0) ? SC_SIG : (lane == 1) ? SC_VAR : (lane == 2) ? SC_ALPHA : SC_GMU + (lane - 3);
-      U[Ly::U_SC + slot] = v;
-    }
-    wave_sync();
-  }
   // have_f0: the start's value (and certificate) came from batch_start_values and did not
   // stop the iteration, so it begins with the gradient at x_start
   // (GSTART takes the base forward product from the square layout's per-workgroup tables; the
@@ -1521,11 +1508,6 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   gm_lane = e.gmu;
   gs_lane = e.gsig;
   sig_lane = sig;
-  if (act && kl == lane) {   // per-start value state for a GSTART evaluation (lower half in split mode)
-    const double bst[NBST] = {sig, var, e.g, e.gmu, e.gsig, e.gmumu, e.gsigsig, e.gmuth, e.gsigth};
-#pragma unroll
-    for (int q = 0; q < NBST; ++q) W.BST[q * WAVE + k] = bst[q];
-  }
   // the iteration stops at the start point: certified, f NaN, or no iterations allowed
   const bool stop = cert || (f_lane != f_lane) || kp.max_iters <= 0;
   bool xn = false;
@@ -2053,7 +2035,6 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
   else W.E = kp.work + slot * kp.work_stride;
   W.C = W.E + (long long)FMAX * Ly::NR;
   W.SUMS = W.E + (long long)(2 * FMAX + 1) * Ly::NR;   // packed layouts only (work_stride covers it)
-  W.BST = kp.work + slot * kp.work_stride + (long long)(2 * FMAX + 1) * Ly::NR + 64 * 8;   // every layout
   W.N = kp.N;
   W.Npad = kp.Npad;
   W.rad.kind = kp.kernel;
