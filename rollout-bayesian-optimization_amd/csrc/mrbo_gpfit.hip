@@ -178,7 +178,10 @@ __global__ void __launch_bounds__(GPFIT_THREADS) gpfit_kernel(GpFitParams q) {
 }
 
 // ---- N ≤ 64: one wave per candidate ---------------------------------------------------
-constexpr int GW_N = 64, GW_LD = GW_N + 1, GW_WAVES = 2;
+#ifndef MRBO_GW_WAVES
+#define MRBO_GW_WAVES 1   // A/B at P = 256, N = 64: 1 wave per group 0.287 ms, 2 waves 0.292 ms
+#endif
+constexpr int GW_N = 64, GW_LD = GW_N + 1, GW_WAVES = MRBO_GW_WAVES;   // waves (candidates) per workgroup
 constexpr int GW_WAVE_DOUBLES = 2 * GW_N * GW_LD + GW_N;   // A, V, c
 
 __device__ __forceinline__ double gw_sum(double v) {
