@@ -89,9 +89,8 @@ def main():
     import torch.distributed as dist
     from mrbo import configs, flops, parallel
     from mrbo.engine import to_device
-    from mrbo.optimizers import StandardSGA
     from mrbo.rollout import _plan_for
-    from mrbo.utils import eswavs
+    from mrbo.utils import sga_step_batch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -122,7 +121,6 @@ def main():
     dx0 = to_device(x0, dev)
     out = plan.alloc_outputs(with_gradient=True)
     evals_acc = torch.zeros_like(out["evals"])
-    opts = [StandardSGA(η=args.eta) for _ in range(R)]
     active = np.ones(R, dtype=bool)
     W = 2 + 2 * d + 2
     kernel_ms = []
@@ -135,15 +133,8 @@ def main():
         parallel.allreduce_sums(sums)
         s = sums.cpu().numpy().reshape((W, R), order="F")
         eto = parallel.eto_from_sums(s, M_total, d)
-        for r in range(R):
-            if not active[r]:
-                continue
-            g, sd = eto[2:2 + d, r], eto[2 + d:2 + 2 * d, r]
-            if eswavs(g, sd ** 2, M_total):
-                active[r] = False
-                continue
-            opts[r].update(x0[:, r], g)
-            np.clip(x0[:, r], pb.lbs, pb.ubs, out=x0[:, r])
+        # eswavs + StandardSGA of every active restart at once (utils.jl:114-123, optimizers.jl:6-23)
+        sga_step_batch(x0, active, eto[2:2 + d], eto[2 + d:2 + 2 * d], M_total, args.eta, pb.lbs, pb.ubs)
         if timed:
             kernel_ms.append(plan.last_kernel_ms())
 

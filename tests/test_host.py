@@ -152,3 +152,31 @@ def test_flop_model_batched_starts():
     assert packed == pytest.approx(want - 255 * ns * flops.f_start_table(N, d), rel=1e-12)
     assert flops.launch_flops(ev, N, d, h, info=dict(rpl=1, blocks=256, batch=0), nstarts=ns) == plain
     assert flops.f_batch_start(N, nf, d) < flops.f_value(N, nf, d) / 5
+
+
+def test_sga_step_batch_equals_per_restart_rules():
+    """bench.py's vectorised outer step == eswavs + StandardSGA.update + clip per restart."""
+    from mrbo.optimizers import StandardSGA
+    from mrbo.utils import eswavs, sga_step_batch
+    rng = np.random.default_rng(0)
+    d, R, M = 6, 64, 1024
+    lbs, ubs = np.zeros(d), np.ones(d)
+    for _ in range(30):
+        g = rng.standard_normal((d, R)) * rng.choice([1e-3, 1.0, 1e3])
+        sd = np.abs(rng.standard_normal((d, R))) * rng.choice([1e-3, 1.0, 1e3])
+        sd[:, rng.integers(0, R, 3)] = 0.0
+        g[0, rng.integers(0, R, 2)] = np.nan
+        x = rng.random((d, R))
+        act = rng.random(R) > 0.2
+        x1, a1 = x.copy(), act.copy()
+        for r in range(R):
+            if not a1[r]:
+                continue
+            if eswavs(g[:, r], sd[:, r] ** 2, M):
+                a1[r] = False
+                continue
+            StandardSGA(0.5).update(x1[:, r], g[:, r])
+            np.clip(x1[:, r], lbs, ubs, out=x1[:, r])
+        x2, a2 = sga_step_batch(x.copy(), act.copy(), g, sd, M, 0.5, lbs, ubs)
+        assert (a1 == a2).all()
+        np.testing.assert_array_equal(x1, x2)
