@@ -1402,14 +1402,29 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
       for (int r = 0; r < FMAX; ++r) ev[s2][r] = W.E[(long long)r * NR + i];
     }
     double* sums = W.SUMS;   // [ns][8]
+    // the kernel-row table entries of the next pair of starts are loaded while this pair is
+    // reduced (one L2 round trip in flight behind the reduction instead of one per pair)
+    auto load_pair = [&](int kc, double (&kxp)[2][RPL]) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int kq = (kc + kk < ns) ? kc + kk : (kc < ns ? kc : 0);
+#pragma unroll
+        for (int s2 = 0; s2 < RPL; ++s2) kxp[kk][s2] = W.KXB[(long long)kq * NR + lane + WAVE * s2];
+      }
+    };
+    double kxn[2][RPL];
+    load_pair(0, kxn);
     for (int kc = 0; kc < ns; kc += 2) {
+      double kxc[2][RPL];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int s2 = 0; s2 < RPL; ++s2) kxc[kk][s2] = kxn[kk][s2];
+      load_pair(kc + 2, kxn);
       double v[16];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        const int kq = (kc + kk < ns) ? kc + kk : kc;
-        double kx[RPL];
-#pragma unroll
-        for (int s2 = 0; s2 < RPL; ++s2) kx[s2] = W.KXB[(long long)kq * NR + lane + WAVE * s2];
+        const double* kx = kxc[kk];
         double a0 = 0.0;
 #pragma unroll
         for (int s2 = 0; s2 < RPL; ++s2) a0 = fma(cv[s2], kx[s2], a0);
