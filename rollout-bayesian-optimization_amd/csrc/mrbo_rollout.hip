@@ -862,9 +862,12 @@ __device__ __forceinline__ int condition(WaveCtx<D, RPL>& W, const KParams& kp, 
     const double fm = U[Ly::U_FMIN + S + 1];
     U[Ly::U_FMIN + S + 2] = (yv < fm) ? yv : fm;
   }
+  double gmine = 0.0;   // gy[lane] by unrolled select: a runtime index would put gy in scratch
+#pragma unroll
+  for (int a = 0; a < D; ++a) gmine = (a == lane) ? gy[a] : gmine;
   if (lane < D) {
     U[Ly::U_XF + nf * D + lane] = U[Ly::U_X + lane];
-    U[Ly::U_GF + nf * D + lane] = gy[lane];
+    U[Ly::U_GF + nf * D + lane] = gmine;
   }
   wave_sync();
   return 0;
@@ -1071,7 +1074,10 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
   const double sc = (pn > box) ? box / pn : 1.0;
   wave_sync();
   const int lane = W.ln();
-  if (lane < D) U[Ly::U_NP + lane] = (pn > box) ? p[lane] * sc : p[lane];
+  double pmine = 0.0;   // p[lane] by unrolled select (a runtime index puts p in scratch)
+#pragma unroll
+  for (int a = 0; a < D; ++a) pmine = (a == lane) ? p[a] : pmine;
+  if (lane < D) U[Ly::U_NP + lane] = (pn > box) ? pmine * sc : pmine;
   wave_sync();
   return true;
 }
