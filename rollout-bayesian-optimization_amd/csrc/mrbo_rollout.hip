@@ -1126,7 +1126,10 @@ __device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const K
 // variance; far from the data both vanish.  One radial evaluation per row and one reduction --
 // instead of the gradient columns (O(N²d)).  Factor 4 for rounding, as above; the oracle
 // (rbo_oracle.c grad_certified) applies the same test.
-template <int D, int RPL>
+// ROWS_KEPT: the VALUE evaluation at x just ran on surface S, so g1 = ψ'(ρ)/ρ of every base
+// row (G12) and fantasy row (U_HF) is still in LDS -- the same bits a new radial evaluation
+// would give; only ρ is recomputed.
+template <int D, int RPL, bool ROWS_KEPT = false>
 __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParams& kp, int S, double gm, double gs,
                                                 double sig) {
   using Ly = Lay<D, RPL>;
@@ -1151,7 +1154,8 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParam
 #pragma unroll
     for (int a = 0; a < D; ++a) { const double r = x[a] - W.X0[s][a]; rho2 = fma(r, r, rho2); }
     double psi, g1, g2;
-    rad_eval(W.rad, rho2, psi, g1, g2);
+    if constexpr (ROWS_KEPT) g1 = W.G12[3 * (lane + WAVE * s)];
+    else rad_eval(W.rad, rho2, psi, g1, g2);
     const double cb = W.C[(long long)(S + 1) * NR + lane + WAVE * s];
     v[0] += W.valid[s] ? fabs(cb) * fabs(g1) * sqrt(rho2) : 0.0;
   }
@@ -1160,7 +1164,8 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParam
 #pragma unroll
     for (int a = 0; a < D; ++a) { const double r = x[a] - U[Ly::U_XF + lane * D + a]; rho2 = fma(r, r, rho2); }
     double psi, g1, g2;
-    rad_eval(W.rad, rho2, psi, g1, g2);
+    if constexpr (ROWS_KEPT) g1 = U[Ly::U_HF + lane * (D + 2) + D];
+    else rad_eval(W.rad, rho2, psi, g1, g2);
     v[0] += fabs(U[Ly::U_CF + (S + 1) * FMAX + lane]) * fabs(g1) * sqrt(rho2);
   }
   wave_sync();
@@ -1265,7 +1270,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
     if (f != f) break;
     if (grad_certified<D, RPL>(W, kp)) break;     // ‖∇α‖ ≤ g_tol guaranteed: stationary
     if (kp.gcert_sig > 0.0 &&
-        tight_certified<D, RPL>(W, kp, S, U[Ly::U_SC + SC_GMU], U[Ly::U_SC + SC_GSIG], U[Ly::U_SC + SC_SIG]))
+        tight_certified<D, RPL, true>(W, kp, S, U[Ly::U_SC + SC_GMU], U[Ly::U_SC + SC_GSIG], U[Ly::U_SC + SC_SIG]))
       break;
     STAMP(W, 12);
     phase = P_GRAD;
