@@ -18,6 +18,9 @@
 #ifndef MRBO_WAVES_PER_SIMD
 #define MRBO_WAVES_PER_SIMD 2
 #endif
+#ifndef MRBO_WAVES_PER_SIMD_GL   // N ≤ 256 (L2-fed layout): 512 registers per wave at 1
+#define MRBO_WAVES_PER_SIMD_GL 1
+#endif
 
 namespace mrbo {
 
@@ -2037,7 +2040,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
 template <int RPL>
 struct KBounds {
   static constexpr int threads = RPL > 2 ? 256 : 512;
-  static constexpr int waves_per_simd = RPL > 2 ? 1 : MRBO_WAVES_PER_SIMD;
+  static constexpr int waves_per_simd = RPL > 2 ? MRBO_WAVES_PER_SIMD_GL : MRBO_WAVES_PER_SIMD;
 };
 
 template <int D, int RPL>
