@@ -37,6 +37,9 @@ def parse():
     ap.add_argument("--mc-per-gpu", type=int, default=0,
                     help="MC samples per GPU (default: the config's M; the metric config is C3 at M=1024)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--longest-first", action="store_true",
+                    help="hand trajectories to the waves longest first by the previous step's work "
+                         "counters (default: index order; measured 1 %% slower at C3, DESIGN.md §9)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--eta", type=float, default=0.5, help="StandardSGA step (optimizers.jl:6-23)")
     return ap.parse_args()
@@ -130,6 +133,8 @@ def main():
         plan.simulate(dx0, drn, dxs, out)
         sums = plan.partial_sums(out, hi - lo)
         evals_acc.add_(out["evals"])        # also in warmup: no first-use op inside the timed region
+        if args.longest_first:
+            plan.order_longest_first(out)   # the next step's schedule (same work)
         parallel.allreduce_sums(sums)
         s = sums.cpu().numpy().reshape((W, R), order="F")
         eto = parallel.eto_from_sums(s, M_total, d)
@@ -186,7 +191,8 @@ def main():
         "config": {"workload": f"{cfg.name}: {cfg.testfn} d={d} h={h} N={cfg.N} M={M_local}/GPU x R={R} restarts, "
                                f"18 inner starts, forward rollout + adjoint gradient per trajectory",
                    "trajectories_per_step": world * (hi - lo) * R, "M_per_gpu": hi - lo, "R": R, "h": h,
-                   "N": cfg.N, "d": d, "parallelism": f"mc-shard x{world}"},
+                   "N": cfg.N, "d": d, "parallelism": f"mc-shard x{world}",
+                   "schedule": "longest first (previous step's work counters)" if args.longest_first else "index order"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": f"rollout_kernel<{d},{info['rpl']},{info['spec']}>", "kernel_ms": kms, "flops_per_launch": fl,

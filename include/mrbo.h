@@ -202,6 +202,13 @@ double mrbo_last_gp_fit_ms(void);
  * (0/1), compile-time specialised kernel (0/1), LDS bytes per workgroup.  Writes min(n, 6). */
 int mrbo_plan_info(const mrbo_plan_t* plan, int32_t* info, int32_t n);
 
+/* Work order of the plan's later mrbo_simulate_mc / mrbo_simulate_ghq launches (no reference
+ * counterpart; scheduling only, results do not depend on it): `order` is a DEVICE array of n =
+ * M×R int32 trajectory indices (m + M·r), a permutation, handed to the persistent waves in that
+ * order -- e.g. longest first by the previous launch's work counters, which shortens the launch's
+ * tail.  Caller-owned; it must stay valid while launches use it.  NULL restores the identity. */
+int mrbo_plan_set_order(mrbo_plan_t* plan, const int32_t* order, int64_t n);
+
 #ifdef __cplusplus
 }
 #endif

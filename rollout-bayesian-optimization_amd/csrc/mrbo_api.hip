@@ -60,6 +60,7 @@ struct mrbo_plan {
   double* dgtab = nullptr;
   long long work_stride = 0;
   int* dqueue = nullptr;
+  const int32_t* order = nullptr;   // mrbo_plan_set_order: caller-owned device permutation of M×R
   int wpg = 4, blocks = 0;
   size_t smem = 0;
   int spec = 0;             // 1: rollout_kernel<D, RPL, 1> (Matérn-5/2 + EI fixed)
@@ -525,6 +526,7 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
   }
   kp.values = dvalues; kp.grad_x = with_grad ? dgx : nullptr; kp.grad_theta = with_grad ? dgt : nullptr;
   kp.status = (int*)dstatus; kp.policy = dpol; kp.obs = dobs; kp.evals = (long long*)devals;
+  kp.order = P->order;
   HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * 4, st));
 #ifdef MRBO_STAMPS
   static unsigned long long* dstamps = nullptr;
@@ -688,6 +690,13 @@ int mrbo_gp_fit(const mrbo_surrogate_t* s, int32_t np, const double* ells, doubl
 }
 
 double mrbo_last_gp_fit_ms(void) { return g_gpfit_ms; }
+
+int mrbo_plan_set_order(mrbo_plan_t* P, const int32_t* order, int64_t n) {
+  if (!P) return fail(MRBO_ERR_ARG, "null plan");
+  if (order && n != (int64_t)P->p.M * P->p.R) return fail(MRBO_ERR_ARG, "order length != M*R");
+  P->order = order;
+  return MRBO_OK;
+}
 
 int mrbo_plan_info(const mrbo_plan_t* P, int32_t* info, int32_t n) {
   if (!P || !info || n < 0) return fail(MRBO_ERR_ARG, "bad arguments");

@@ -76,6 +76,7 @@ struct KParams {
   const double* ghq_nodes;  // Gauss–Hermite estimator: M×(h+1) nodes and weights per sample (else null)
   const double* ghq_w;
   int* queue;           // work-queue head (zeroed before every launch)
+  const int* order;     // optional: queue position -> trajectory (mrbo_plan_set_order), else identity
   long long T;          // trajectories (or points for eval_base)
   const double* pts;    // eval_base: d×P
   double* pts_out;      // eval_base output

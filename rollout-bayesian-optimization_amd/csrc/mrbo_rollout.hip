@@ -2112,6 +2112,10 @@ __global__ void __launch_bounds__(KBounds<RPL>::threads, KBounds<RPL>::waves_per
     if (W.lane == 0) tr = atomicAdd(kp.queue, 1);
     tr = __shfl(tr, 0, WAVE);
     if (tr >= kp.T) break;
+    if (kp.order) {   // caller's schedule (a permutation; an out-of-range entry falls back to tr)
+      const long long id = kp.order[tr];
+      tr = (id >= 0 && id < kp.T) ? id : tr;
+    }
     trajectory<D, RPL>(W, kp, tr);
   }
 #ifdef MRBO_STAMPS

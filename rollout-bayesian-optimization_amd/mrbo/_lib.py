@@ -32,7 +32,7 @@ EXPORTS = [
     "mrbo_version", "mrbo_last_error", "mrbo_device_count", "mrbo_plan_create", "mrbo_plan_destroy",
     "mrbo_simulate_mc", "mrbo_simulate_ghq", "mrbo_eto_reduce", "mrbo_partial_sums", "mrbo_eval_base", "mrbo_rnstream",
     "mrbo_initial_guesses", "mrbo_dual_uniform", "mrbo_last_kernel_ms", "mrbo_gp_fit",
-    "mrbo_plan_info", "mrbo_last_gp_fit_ms",
+    "mrbo_plan_info", "mrbo_last_gp_fit_ms", "mrbo_plan_set_order",
 ]
 
 
@@ -93,6 +93,7 @@ def load():
     L.mrbo_last_kernel_ms.argtypes = [_vp]
     L.mrbo_last_kernel_ms.restype = ctypes.c_double
     L.mrbo_plan_info.argtypes = [_vp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]
+    L.mrbo_plan_set_order.argtypes = [_vp, _vp, ctypes.c_int64]
     L.mrbo_last_gp_fit_ms.restype = ctypes.c_double
     _lib = L
     return L

@@ -155,6 +155,34 @@ class RolloutPlan:
     def last_kernel_ms(self):
         return self.lib.mrbo_last_kernel_ms(self.handle)
 
+    # relative cost of one unit of each work counter (grad, value, hess, rich, pairs), in value
+    # evaluations -- only the ORDER of the work depends on these, never a result
+    ORDER_WEIGHTS = (2.5, 1.0, 3.0, 5.0, 3.0)
+
+    def set_order(self, order):
+        """mrbo_plan_set_order: an int32 device tensor holding a permutation of the M×R trajectory
+        indices (m + M·r), or None for the identity.  The plan keeps a reference."""
+        if order is None:
+            _lib.check(self.lib.mrbo_plan_set_order(self.handle, None, 0))
+            self._order = None
+            return
+        torch = _torch()
+        if order.dtype != torch.int32 or not order.is_cuda or order.numel() != self.M * self.R:
+            raise ValueError("order must be an int32 device tensor of M*R trajectory indices")
+        self._order = order.contiguous()
+        _lib.check(self.lib.mrbo_plan_set_order(self.handle, ctypes.c_void_p(self._order.data_ptr()),
+                                                self._order.numel()))
+
+    def order_longest_first(self, out):
+        """Schedule the next launches longest-first by the per-trajectory work counters of the
+        launch that filled `out` (on the device, no host round trip).  Consecutive SGA steps move
+        x0 a little and reuse the MC streams, so a trajectory's work repeats closely and the
+        longest ones no longer start last (the launch's tail)."""
+        torch = _torch()
+        ev = out["evals"].view(-1, _lib.NCOUNTERS).to(torch.float64)
+        w = torch.tensor(self.ORDER_WEIGHTS, dtype=torch.float64, device=ev.device)
+        self.set_order(torch.argsort(ev @ w, descending=True).to(torch.int32))
+
     def info(self):
         """Launch geometry: rows per lane, workgroups, waves per workgroup, batched start values,
         specialised kernel, LDS bytes per workgroup."""

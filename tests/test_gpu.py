@@ -341,3 +341,30 @@ def test_specialised_kernel_equals_generic(gpu, monkeypatch, name, M, R):
         np.testing.assert_allclose(r_spec[k], r_gen[k], rtol=1e-12, atol=1e-15, err_msg=k)
     for k in ("grad_x", "grad_theta"):
         _assert_grads_close(r_spec[k], r_gen[k], rtol=1e-10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,M,R", [("C3", 32, 4), ("C4", 8, 2)])
+def test_work_order_changes_nothing_but_the_schedule(gpu, name, M, R):
+    """mrbo_plan_set_order only reorders the work queue: a reversed permutation and the
+    longest-first schedule of a previous launch give bit-identical results and work counters;
+    a wrong-length order is rejected, None restores the identity."""
+    import torch
+    g = _problem_arrays(name, M, R)
+    plan = _plan(g)
+    r_id = _run(plan, g)
+    plan.set_order(torch.arange(M * R - 1, -1, -1, dtype=torch.int32, device="cuda:0"))
+    r_rev = _run(plan, g)
+    out = plan.alloc_outputs(with_gradient=True)
+    from mrbo.engine import to_device
+    plan.simulate(to_device(g["x0s"], "cuda:0"), to_device(g["rnstream"], "cuda:0"), to_device(g["xstarts"], "cuda:0"), out)
+    plan.order_longest_first(out)
+    r_lpt = _run(plan, g)
+    for r in (r_rev, r_lpt):
+        for k in r_id:
+            np.testing.assert_array_equal(r_id[k], r[k], err_msg=k)
+    with pytest.raises(Exception):
+        plan.set_order(torch.zeros(M * R + 1, dtype=torch.int32, device="cuda:0"))
+    plan.set_order(None)
+    r_none = _run(plan, g)
+    np.testing.assert_array_equal(r_id["values"], r_none["values"])
