@@ -3,20 +3,29 @@
 
 One *step* = one outer stochastic-gradient-ascent iteration of the rollout acquisition
 (utils.jl:235-265): simulate_trajectory_mc for R restarts × M MC samples (forward rollout +
-adjoint gradient, rollout.jl:279-340) on the device, per-restart partial sums, one all-reduce
-across ranks, ETO + eswavs + SGA update of the R start points.
+adjoint gradient, rollout.jl:279-340) on the device, the per-restart ETO (mean / std n−1,
+rollout.jl:328-339), eswavs and StandardSGA.update! of the R start points (utils.jl:114-123,
+optimizers.jl:16-22; η = 0.01, the reference default, no box clip).
 
 Workload C3 (headline): Hartmann6 d=6, horizon h=3, N=64 base observations, M=1024 MC
 samples × R=64 restarts per GPU, 18 inner starts, fp64.  With --gpus N the per-GPU work is
-fixed (weak scaling): rank k runs samples [kM, (k+1)M) of one N·M-sample rnstream.
+fixed (weak scaling): rank k runs samples [kM, (k+1)M) of one N·M-sample rnstream and the
+ranks exchange their per-restart moments once per step (one all-gather, Chan merge,
+mrbo/parallel.py).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--ell L | --mle]
+  N > 1 without WORLD_SIZE in the environment: this process starts N ranks itself
+  (python -m torch.distributed.run --nproc-per-node N ...) before touching the GPU, and exits
+  with their status; under torchrun (WORLD_SIZE set) each rank runs one GPU.
 """
 import argparse
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -26,6 +35,7 @@ import numpy as np  # noqa: E402
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X dense fp64 (vector = matrix), spec
 METRIC = "rollout trajectories/sec (MC samples × restarts) at horizon h=3, n=64 GP"
+KERNEL_BOUNDS = ([0.1], [5.0])   # optimize!(sur, lowerbounds=kernel_lbs, ...) nonmyopic_bayesopt.jl:230,285
 
 
 def parse():
@@ -36,58 +46,124 @@ def parse():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--mc-per-gpu", type=int, default=0,
                     help="MC samples per GPU (default: the config's M; the metric config is C3 at M=1024)")
+    ap.add_argument("--restarts", type=int, default=0, help="restarts R (default: the config's)")
+    ap.add_argument("--ell", type=float, default=0.0, help="Matérn-5/2 lengthscale (default 1.0, SURVEY §8d)")
+    ap.add_argument("--mle", action="store_true",
+                    help="fit the lengthscale first by optimize! (radial_basis_surrogates.jl:805-829) on the "
+                         "config's base data within [0.1, 5] (nonmyopic_bayesopt.jl:230)")
+    ap.add_argument("--cost", action="store_true",
+                    help="cost-weighted EI with NonUniformCost (cost_functions.jl:5-20; build-defined, "
+                         "parity unpinned)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--longest-first", action="store_true",
                     help="hand trajectories to the waves longest first by the previous step's work "
                          "counters (default: index order; measured 1 %% slower at C3, DESIGN.md §9)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--eta", type=float, default=0.5, help="StandardSGA step (optimizers.jl:6-23)")
+    ap.add_argument("--eta", type=float, default=0.01, help="StandardSGA step (optimizers.jl:6-23; default 0.01)")
+    ap.add_argument("--dump", default="", help="write the final ETO and x0 (npz) here (rank 0)")
     return ap.parse_args()
 
 
-def cpu_baseline(pb, M_full, R_full, budget_s):
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args):
+    """--gpus N > 1 outside torchrun: start the N ranks (one process per GPU) and return their exit
+    status.  Runs before anything initialises the GPU in this process (device_count() does not)."""
+    import torch
+    ndev = torch.cuda.device_count()
+    rehearse = os.environ.get("MRBO_DIST_BACKEND", "nccl") == "gloo"
+    if args.gpus > ndev and not rehearse:
+        print(f"bench.py: --gpus {args.gpus} but only {ndev} GPU(s) visible", file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def julia_probe():
+    """BASELINE.md CPU-baseline step 1: is the Julia reference runnable on this host?"""
+    j = shutil.which("julia")
+    return f"julia at {j} (reference not timed: Optim/Sobol/ForwardDiff are unpinned)" if j else \
+        "unavailable (no julia on this host): the baseline is the C restatement of the same path"
+
+
+def oracle_timing_lib():
+    """The oracle built for timing: -O3 -march=native on THIS host when gcc is present (compiled
+    into a temp dir, a few seconds; the checker build stays -O2 -ffp-contract=off), else the
+    shipped -O3 -march=x86-64-v3 build.  Returns (path, flags)."""
+    src = os.path.join(ROOT, "oracle", "rbo_oracle.c")
+    gcc = shutil.which("gcc")
+    if gcc:
+        out = os.path.join(tempfile.mkdtemp(prefix="rbo_native_"), "librbo_oracle_native.so")
+        flags = ["-O3", "-march=native", "-fPIC", "-fopenmp", "-shared"]
+        r = subprocess.run([gcc] + flags + ["-o", out, src, "-lm"], capture_output=True)
+        if r.returncode == 0:
+            return out, " ".join(flags)
+    fast = os.path.join(ROOT, "oracle", "build", "librbo_oracle_fast.so")
+    return fast, "-O3 -march=x86-64-v3 -fopenmp (prebuilt)"
+
+
+def cpu_baseline(pb, M_full, R_full, budget_s, cost=None):
     """The oracle (C restatement, 'port') on the same workload, bounded sample, host cores."""
     from oracle import oracle as O
-    nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    path, flags = oracle_timing_lib()
+    O.use_library(path)
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
     s = pb.surrogate
     n = s.observed
-    osur = O.OracleSurrogate(s.X[:, :n], s.L[:n, :n], s.c[:n], s.y[:n], fmini=s.fmini())
+    osur = O.OracleSurrogate(s.X[:, :n], s.L[:n, :n], s.c[:n], s.y[:n], ell=s.ψ.lengthscale, fmini=s.fmini())
     rn = pb.tp.rnstream_sequence[:M_full]
     xs = pb.es.get_starts()
 
-    def run(Ms, Rs):
+    def run(Ms, Rs, nt):
         t = time.perf_counter()
         O.simulate_mc(osur, pb.x0s[:, :Rs], np.asfortranarray(rn[:Ms]), xs, pb.lbs, pb.ubs, pb.cfg.h,
-                      nthreads=nthreads, want_policy=False)
+                      nthreads=nt, want_policy=False, cost=cost)
         return time.perf_counter() - t
 
-    def run1(Ms):   # the reference itself is single-process, single-thread
-        t = time.perf_counter()
-        O.simulate_mc(osur, pb.x0s[:, :1], np.asfortranarray(rn[:Ms]), xs, pb.lbs, pb.ubs, pb.cfg.h,
-                      nthreads=1, want_policy=False)
-        return time.perf_counter() - t
-
-    Ms, Rs = min(M_full, max(nthreads * 4, 32)), 1
-    dt = run(Ms, Rs)
-    rate = Ms * Rs / dt
+    Ms = min(M_full, max(nthreads * 4, 32))
+    dt = run(Ms, 1, nthreads)
+    rate = Ms / dt
     # scale the sample to ~budget_s seconds of CPU work (never beyond the full workload)
     target = int(rate * budget_s)
     Rs = max(1, min(R_full, target // M_full)) if target >= M_full else 1
     Ms = M_full if target >= M_full else max(Ms, min(M_full, target))
-    dt = run(Ms, Rs)
+    dt = run(Ms, Rs, nthreads)
     M1 = min(M_full, 64)
-    dt1 = run1(M1)
+    dt1 = run(M1, 1, 1)
     M1 = min(M_full, max(M1, int(M1 / dt1 * budget_s * 0.3)))
-    dt1 = run1(M1)
+    dt1 = run(M1, 1, 1)
+    O.use_library(None)
     return dict(value=Ms * Rs / dt, unit="trajectories/s", cores=nthreads, kind="port",
                 sample=f"{pb.cfg.name} workload, first {Rs} restart(s) x {Ms} MC samples "
                        f"({Ms * Rs} trajectories, {dt:.1f} s), oracle/rbo_oracle.c OpenMP x{nthreads}",
+                build=flags, host_cpus=os.cpu_count(), affinity_cpus=aff, reference=julia_probe(),
                 single_thread={"value": M1 / dt1, "cores": 1,
                                "sample": f"first restart x {M1} MC samples ({dt1:.1f} s), 1 thread"})
 
 
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if world == 0:
+        if args.gpus > 1:
+            return launch_ranks(args)
+        world = 1
+    elif world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
     from mrbo import configs, flops, parallel
@@ -95,9 +171,6 @@ def main():
     from mrbo.rollout import _plan_for
     from mrbo.utils import sga_step_batch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; MRBO_DIST_BACKEND=gloo + device wrap-around only for rehearsing the
     # multi-rank path on a box with fewer GPUs than ranks
     ndev = torch.cuda.device_count()
@@ -110,13 +183,22 @@ def main():
         else:
             dist.init_process_group(backend)
     cfg = configs.CONFIGS[args.config]
-    M_local, R, d, h = (args.mc_per_gpu or cfg.M), cfg.R, cfg.d, cfg.h
+    M_local, R, d, h = (args.mc_per_gpu or cfg.M), (args.restarts or cfg.R), cfg.d, cfg.h
     M_total = M_local * world
-    lo, hi = parallel.shard(M_total, world, rank)
-    pb = configs.problem(args.config, M=M_total)
+    shards = [parallel.shard(M_total, world, k) for k in range(world)]
+    lo, hi = shards[rank]
+    pb = configs.problem(args.config, M=M_total, R=R, cost=args.cost)
+    mle = None
+    if args.mle:
+        from mrbo import mle as mle_mod
+        mle = mle_mod.optimize(pb.surrogate, *KERNEL_BOUNDS)
+    elif args.ell > 0:
+        from mrbo.kernels import Matern52
+        pb.surrogate.set_kernel(Matern52([args.ell]))
+    ell = pb.surrogate.ψ.lengthscale
     T = pb.T
     plan = _plan_for(T.s, h, hi - lo, R, pb.es.get_starts().shape[1], pb.lbs, pb.ubs, T.θ[0], local,
-                     dict(sample_offset=lo, samples_total=M_total))
+                     dict(sample_offset=lo, samples_total=M_total, **pb.plan_opts()))
     dev = f"cuda:{local}"
     drn = to_device(np.asfortranarray(pb.tp.rnstream_sequence[lo:hi]), dev)   # resident in HBM
     dxs = to_device(pb.es.get_starts(), dev)
@@ -125,21 +207,27 @@ def main():
     out = plan.alloc_outputs(with_gradient=True)
     evals_acc = torch.zeros_like(out["evals"])
     active = np.ones(R, dtype=bool)
-    W = 2 + 2 * d + 2
+    W = parallel.width(d)
     kernel_ms = []
+    last = {}
 
     def step(timed):
         dx0.copy_(torch.from_numpy(x0.ravel(order="F")), non_blocking=False)
         plan.simulate(dx0, drn, dxs, out)
-        sums = plan.partial_sums(out, hi - lo)
+        if world == 1:
+            e = plan.eto(out)                           # two-pass mean / std(n-1) on the device
+        else:
+            e = plan.partial_moments(out, hi - lo)     # this shard's (Σ, M2) rows
         evals_acc.add_(out["evals"])        # also in warmup: no first-use op inside the timed region
         if args.longest_first:
             plan.order_longest_first(out)   # the next step's schedule (same work)
-        parallel.allreduce_sums(sums)
-        s = sums.cpu().numpy().reshape((W, R), order="F")
-        eto = parallel.eto_from_sums(s, M_total, d)
-        # eswavs + StandardSGA of every active restart at once (utils.jl:114-123, optimizers.jl:6-23)
-        sga_step_batch(x0, active, eto[2:2 + d], eto[2 + d:2 + 2 * d], M_total, args.eta, pb.lbs, pb.ubs)
+        if world == 1:
+            eto = e.cpu().numpy().reshape((W, R), order="F")
+        else:
+            eto = parallel.sharded_eto(e, [b - a for a, b in shards], d)
+        last["eto"] = eto
+        # eswavs + StandardSGA of every active restart at once (utils.jl:114-123, optimizers.jl:16-22)
+        sga_step_batch(x0, active, eto[2:2 + d], eto[2 + d:2 + 2 * d], M_total, args.eta)
         if timed:
             kernel_ms.append(plan.last_kernel_ms())
 
@@ -170,11 +258,13 @@ def main():
     kms = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
     achieved = fl / (kms * 1e-3) / 1e12
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", f"traffic_{cfg.name}.json")
+    tag = cfg.name + ("" if ell == 1.0 and not args.cost else f"_ell{ell:.4g}" + ("_cost" if args.cost else ""))
+    tpath = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
     if os.path.exists(tpath):
         with open(tpath) as f:
             traffic = json.load(f).get("bytes_per_launch")
-    total = world * (hi - lo) * R * args.steps
+    total = world * (hi - lo) * R * args.steps if world == 1 else sum(b - a for a, b in shards) * R * args.steps
+    rule = "cost-weighted EI (NonUniformCost)" if args.cost else "EI"
     res = {
         "metric": METRIC,
         "value": total / elapsed,
@@ -190,8 +280,14 @@ def main():
         "data": "synthetic (Kronecker base design on the test function, Sobol/Box-Muller(log10) rnstream)",
         "config": {"workload": f"{cfg.name}: {cfg.testfn} d={d} h={h} N={cfg.N} M={M_local}/GPU x R={R} restarts, "
                                f"18 inner starts, forward rollout + adjoint gradient per trajectory",
-                   "trajectories_per_step": world * (hi - lo) * R, "M_per_gpu": hi - lo, "R": R, "h": h,
-                   "N": cfg.N, "d": d, "parallelism": f"mc-shard x{world}",
+                   "trajectories_per_step": sum(b - a for a, b in shards) * R, "M_per_gpu": hi - lo, "R": R,
+                   "h": h, "N": cfg.N, "d": d, "kernel": f"Matern52(ℓ={ell:.6g})",
+                   "lengthscale_source": "optimize! MLE in [0.1, 5]" if mle else ("--ell" if args.ell > 0 else
+                                                                                 "ℓ = 1 (SURVEY §8d)"),
+                   "rule": rule, "parallelism": f"mc-shard x{world}",
+                   "exchange": "none" if world == 1 else f"all-gather of (Σ, M2) moments, {W * R * 8} B/rank/step",
+                   "outer_step": f"eswavs + StandardSGA η={args.eta:g}, no clip (utils.jl:114-123, "
+                                 f"optimizers.jl:16-22)",
                    "schedule": "longest first (previous step's work counters)" if args.longest_first else "index order"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
@@ -201,19 +297,25 @@ def main():
                              "peak on MI355X; the kernel issues VALU v_fma_f64 (matrix-vector work, not "
                              "GEMM-shaped); algorithmic FLOP model in DESIGN.md §5; HBM algorithmic "
                              "bytes/traj ~0.3 KB so an HBM roofline does not bind; traffic = PMC bytes per "
-                             "launch from profiles/traffic_<config>.json"},
+                             f"launch from profiles/traffic_{tag}.json"},
         "status_errors": int((st != 0).sum()),
         "work_per_traj": {"grad_evals": float(ev[0].mean()), "value_evals": float(ev[1].mean()),
                           "hessians": float(ev[2].mean()), "rich_evals": float(ev[3].mean()),
                           "pairs": float(ev[4].mean())},
     }
+    if mle:
+        res["config"]["mle"] = {"theta": float(mle["theta"][0]), "neg_log_likelihood": float(mle["neg_log_likelihood"]),
+                                "iterations": int(mle["iterations"])}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(pb, M_local, R, args.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(pb, M_local, R, args.cpu_seconds, cost=pb.cost_model())
     if rank == 0:
-        print(json.dumps(res))
+        print(json.dumps(res), flush=True)
+        if args.dump:
+            np.savez(args.dump, eto=last["eto"], x0=x0, active=active)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -35,12 +35,12 @@
 extern "C" {
 #endif
 
-#define MRBO_ABI_VERSION 1
+#define MRBO_ABI_VERSION 2
 
 typedef enum {
   MRBO_OK = 0,
   MRBO_ERR_ARG = -1,      /* invalid argument (dimension, size, null pointer)            */
-  MRBO_ERR_UNSUPPORTED = -2, /* shape outside the compiled kernels (d > 8, N > 128, h > 5) */
+  MRBO_ERR_UNSUPPORTED = -2, /* shape outside the compiled kernels (d > 8, N > 256, h > 5) */
   MRBO_ERR_HIP = -3,      /* HIP runtime error                                          */
   MRBO_ERR_NOMEM = -4
 } mrbo_err_t;
@@ -58,6 +58,14 @@ typedef enum {
   MRBO_RULE_POI = 1,  /* decision_rules.jl:101-115 probability of improvement           */
   MRBO_RULE_LCB = 2   /* decision_rules.jl:117-127 θσ − μ (negated lower confidence bound) */
 } mrbo_rule_t;
+
+/* NonUniformCost (cost_functions.jl:5-20: NonUniformCost(f) with ∇f, Hf) as closed-form families.
+ * The reference's cost is an arbitrary closure referenced by no rule, surrogate or trajectory;
+ * the build defines the cost-weighted acquisition f(x) = α(x)/c(x) of the inner policy solve
+ * (α, ∇f, Hf, ∂∇f/∂θ and the adjoint perturbations all weighted; parity unpinned, the oracle
+ * implements the same definition).  u_a = (x_a − lb_a)/(ub_a − lb_a) over the plan's box:
+ *   MRBO_COST_QUADRATIC  c(x) = c0 + Σ_a w_a u_a²        MRBO_COST_LOGLINEAR  c(x) = c0·exp(Σ_a w_a u_a) */
+typedef enum { MRBO_COST_NONE = 0, MRBO_COST_QUADRATIC = 1, MRBO_COST_LOGLINEAR = 2 } mrbo_cost_t;
 
 /* per-trajectory status bits: the reference's exceptions (SURVEY.md §8b "Errors") */
 enum {
@@ -110,6 +118,9 @@ typedef struct {
   uint64_t seed;        /* δx for solve_dual_y (rollout.jl:133) when dual_y_dx == NULL */
   int32_t sample_offset;/* global index of this plan's first MC sample (multi-GPU shard), 0 */
   int32_t samples_total;/* global MC samples per restart (0 → M); keys the δx counter RNG  */
+  int32_t cost;         /* mrbo_cost_t: NonUniformCost weighting of the inner-solve rule      */
+  double cost_c0;       /* cost family parameter c0                                          */
+  const double* cost_w; /* d weights, HOST (NULL with MRBO_COST_NONE)                        */
 } mrbo_params_t;
 
 typedef struct mrbo_plan mrbo_plan_t;
@@ -165,10 +176,12 @@ int mrbo_simulate_ghq(mrbo_plan_t* plan, const double* x0s, const double* nodes,
 int mrbo_eto_reduce(mrbo_plan_t* plan, const double* values, const double* grad_x, const double* grad_theta,
                     double* eto, uint32_t flags, void* stream);
 
-/* Partial sums for the multi-GPU allreduce: sums R×(2+2d+2) = [Σα, Σα², Σ∇x(d), Σ∇x²(d), Σ∇θ, Σ∇θ²]
- * over the M_local samples of this rank (rollout.jl:328-339 in two-pass-free form).     */
-int mrbo_partial_sums(mrbo_plan_t* plan, const double* values, const double* grad_x, const double* grad_theta,
-                      int32_t M_local, double* sums, uint32_t flags, void* stream);
+/* Shard moments for the multi-GPU exchange: moments R×(2+2d+2) = [Σα, M2α, Σ∇x(d), M2∇x(d), Σ∇θ, M2∇θ]
+ * over the M_local samples of this rank, M2 = Σ(x − x̄_local)² by two passes.  Ranks all-gather
+ * (n, Σ, M2) and merge them with Chan's formula (mrbo/parallel.py merge_moments), which gives the
+ * two-pass mean / std(n-1) of rollout.jl:328-339 without one-pass cancellation.            */
+int mrbo_partial_moments(mrbo_plan_t* plan, const double* values, const double* grad_x, const double* grad_theta,
+                         int32_t M_local, double* moments, uint32_t flags, void* stream);
 
 /* eval(s, x, θ) of the base surrogate at P points xs (d×P); out stride 3+4d+d²:
  * [μ, σ, α, ∇μ(d), ∇σ(d), ∇α(d), Hα(d×d col-major), d2α/dxdθ(d)].                       */

@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "librbo_oracle.so")
 _lib = None
 
+COSTS = {"none": 0, "quadratic": 1, "loglinear": 2}
 KERNELS = {"matern52": 0, "matern32": 1, "matern12": 2, "se": 3, "periodic": 4}
 TESTFNS = {"gramacylee": 0, "braninhoo": 1, "hartmann6d": 2, "ackley": 3, "rosenbrock": 4, "rastrigin": 5}
 
@@ -35,19 +36,32 @@ class Params(ctypes.Structure):
                 ("x_tol", ctypes.c_double), ("f_tol", ctypes.c_double), ("g_tol", ctypes.c_double),
                 ("htol", ctypes.c_double), ("sigma_tol", ctypes.c_double), ("seed", ctypes.c_uint64),
                 ("sample_offset", ctypes.c_int32), ("samples_total", ctypes.c_int32),
-                ("with_gradient", ctypes.c_int32), ("nthreads", ctypes.c_int32), ("rule", ctypes.c_int32)]
+                ("with_gradient", ctypes.c_int32), ("nthreads", ctypes.c_int32), ("rule", ctypes.c_int32),
+                ("cost", ctypes.c_int32), ("cost_c0", ctypes.c_double), ("cost_w", _dp)]
 
 
 def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
 
+_override = None
+
+
+def use_library(path):
+    """Load the oracle from `path` (e.g. the -O3 -march=native timing build of bench.py's
+    cpu_baseline leg) for later calls; None restores the checker build."""
+    global _lib, _override
+    _override = path
+    _lib = None
+
+
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH):
+        path = _override or _LIB_PATH
+        if path == _LIB_PATH and not os.path.exists(_LIB_PATH):
             build()
-        L = ctypes.CDLL(_LIB_PATH)
+        L = ctypes.CDLL(path)
         L.rbo_gen_uniform.argtypes = [ctypes.c_int32, ctypes.c_int32, _dp]
         L.rbo_gen_low_discrepancy_sequence.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _dp]
         L.rbo_generate_initial_guesses.argtypes = [ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp]
@@ -58,6 +72,7 @@ def lib():
         L.rbo_testfn.restype = ctypes.c_double
         L.rbo_eval_base.argtypes = [ctypes.POINTER(Surrogate), ctypes.c_int32, ctypes.c_double, ctypes.c_double,
                                     ctypes.c_int32, _dp, _dp]
+        L.rbo_eval_base_p.argtypes = [ctypes.POINTER(Surrogate), ctypes.POINTER(Params), ctypes.c_int32, _dp, _dp]
         L.rbo_simulate_mc.argtypes = [ctypes.POINTER(Surrogate), ctypes.POINTER(Params), _dp, _dp, _dp, _dp, _dp,
                                       _dp, _dp, _dp, _ip, _dp, _dp, _dp, _lp]
         L.rbo_log_likelihood.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_double,
@@ -139,22 +154,32 @@ def log_likelihood(X, y, kernel="matern52", ell=1.0, sigma_n2=1e-6, want_fit=Fal
     return (ll.value, dll.value, L, c) if want_fit else (ll.value, dll.value)
 
 
-def eval_base(osur, xs, theta=0.0, sigma_tol=1e-8, rule="EI"):
+def eval_base(osur, xs, theta=0.0, sigma_tol=1e-8, rule="EI", cost=None, lbs=None, ubs=None):
+    """Base-surrogate evaluation, columns [μ, σ, α, ∇μ, ∇σ, ∇α, Hα, ∂∇α/∂θ] per point; with
+    cost=(kind, c0, w) (and the box lbs, ubs) the NonUniformCost-weighted α/c(x) and its derivatives."""
     xs = _f64(xs)
     d, P = xs.shape
     stride = 3 + 4 * d + d * d
     out = np.zeros((stride, P), order="F")
-    assert lib().rbo_eval_base(ctypes.byref(osur.s), RULES[rule], theta, sigma_tol, P, _p(xs), _p(out)) == 0
+    if cost is None:
+        assert lib().rbo_eval_base(ctypes.byref(osur.s), RULES[rule], theta, sigma_tol, P, _p(xs), _p(out)) == 0
+        return out
+    lbs, ubs, cw = _f64(lbs).ravel(), _f64(ubs).ravel(), _f64(cost[2]).ravel()
+    ck = COSTS[cost[0]] if isinstance(cost[0], str) else int(cost[0])
+    prm = Params(0, 1, 1, 1, theta, _p(lbs), _p(ubs), 0, 0, 0.0, 0.0, 0.0, 0.0, sigma_tol, 0, 0, 0, 0, 1,
+                 RULES[rule], ck, float(cost[1]), _p(cw))
+    assert lib().rbo_eval_base_p(ctypes.byref(osur.s), ctypes.byref(prm), P, _p(xs), _p(out)) == 0
     return out
 
 
 def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=None, replay_x=None,
                 max_iters=50, max_ls=20, x_tol=1e-3, f_tol=1e-3, g_tol=1e-8, htol=1e-4, sigma_tol=1e-8,
                 seed=1906, with_gradient=True, nthreads=0, want_policy=True, sample_offset=0,
-                samples_total=0, rule="EI", ghq=None):
+                samples_total=0, rule="EI", ghq=None, cost=None):
     """Run the oracle's simulate_trajectory_mc for every restart column of x0s (d×R).
     ghq=(nodes, weights), each M×(h+1): the Gauss–Hermite estimator (rbo_simulate_ghq) instead
-    of the rnstream draws (rnstream is then only used for its M)."""
+    of the rnstream draws (rnstream is then only used for its M).
+    cost=(kind, c0, w): NonUniformCost weighting of the inner-solve rule (rbo_oracle.h RBO_COST_*)."""
     x0s, xstarts = _f64(x0s), _f64(xstarts)
     lbs, ubs = _f64(lbs), _f64(ubs)
     d, R = x0s.shape
@@ -166,9 +191,16 @@ def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=
         rnstream = _f64(rnstream)
         M = rnstream.shape[0]
         assert rnstream.shape == (M, d + 1, h + 1), rnstream.shape
+    cw = None
+    ck, c0 = 0, 1.0
+    if cost is not None:
+        ck = COSTS[cost[0]] if isinstance(cost[0], str) else int(cost[0])
+        c0 = float(cost[1])
+        cw = _f64(cost[2]).ravel()
+        assert cw.size == d, (cw.size, d)
     prm = Params(h, M, R, xstarts.shape[1], theta, _p(lbs), _p(ubs), max_iters, max_ls, x_tol, f_tol, g_tol,
                  htol, sigma_tol, seed, sample_offset, samples_total, 1 if with_gradient else 0, nthreads,
-                 RULES[rule])
+                 RULES[rule], ck, c0, _p(cw))
     values = np.zeros((M, R), order="F")
     grad_x = np.zeros((d, M, R), order="F")
     grad_t = np.zeros((1, M, R), order="F")

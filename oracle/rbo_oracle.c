@@ -404,10 +404,17 @@ typedef struct {
   double* cs;  /* (h+2) × cap : cs[s+1] = coefficient vector of fantasy_index s */
   int nfant;   /* fantasies_observed */
   int rule;    /* RBO_RULE_*: the trajectory's base decision rule */
+  int cost;    /* RBO_COST_*: cost weighting of the rule (inner solve), see cost_eval */
+  double c0, cw[16], clb[16], cub[16];
 } fsur_t;
 
-static int fsur_alloc(fsur_t* fs, const rbo_surrogate* s, int h, int rule) {
+static int fsur_alloc(fsur_t* fs, const rbo_surrogate* s, int h, int rule, const rbo_params* p) {
   fs->d = s->d; fs->N = s->N; fs->h = h; fs->cap = s->N + h + 1; fs->rule = rule;
+  fs->cost = (p && p->cost_w) ? p->cost : RBO_COST_NONE;
+  if (fs->cost) {
+    fs->c0 = p->cost_c0;
+    for (int a = 0; a < s->d; ++a) { fs->cw[a] = p->cost_w[a]; fs->clb[a] = p->lbs[a]; fs->cub[a] = p->ubs[a]; }
+  }
   fs->k.kind = s->kernel; fs->k.ell = s->ell; fs->k.per = s->period; fs->sn2 = s->sigma_n2;
   fs->X = (double*)calloc((size_t)fs->d * fs->cap, sizeof(double));
   fs->L = (double*)calloc((size_t)fs->cap * fs->cap, sizeof(double));
@@ -460,6 +467,7 @@ typedef struct {
   double mu, sigma, fmin, alpha;
   double gmu[16], gsig[16], galpha[16], mixed[16];
   double Halpha[256];
+  double alpha_raw, cost, gcost[16], gcmax; /* NonUniformCost: rule value g, c(x), ∇c(x), max|∇c| */
   ei_t e;
   double *kx, *gkx, *w, *Dw; /* n, d×n, n, n×d  (scratch owned by caller) */
   int status;
@@ -482,7 +490,37 @@ static void scratch_free(scratch_t* sc) {
   free(sc->kx); free(sc->gkx); free(sc->w); free(sc->Dw); free(sc->tmp); free(sc->tmp2); free(sc->tmp3);
 }
 
-/* value_only: α only (the line-search path); full: gradient, Hessian, mixed partials. */
+/* NonUniformCost families (rbo_oracle.h RBO_COST_*): c(x), ∇c(x) and Hc = diag(hd) + β v vᵀ. */
+static void cost_eval(const fsur_t* fs, const double* x, double* c, double* gc, double* hd, double* beta, double* v) {
+  const int d = fs->d;
+  if (fs->cost == RBO_COST_QUADRATIC) {
+    double s = fs->c0;
+    for (int a = 0; a < d; ++a) {
+      const double del = fs->cub[a] - fs->clb[a], u = (x[a] - fs->clb[a]) / del;
+      s += fs->cw[a] * u * u;
+      gc[a] = 2.0 * fs->cw[a] * u / del;
+      hd[a] = 2.0 * fs->cw[a] / (del * del);
+      v[a] = 0.0;
+    }
+    *c = s;
+    *beta = 0.0;
+  } else {
+    double t = 0;
+    for (int a = 0; a < d; ++a) t += fs->cw[a] * (x[a] - fs->clb[a]) / (fs->cub[a] - fs->clb[a]);
+    const double cv = fs->c0 * exp(t);
+    for (int a = 0; a < d; ++a) {
+      v[a] = fs->cw[a] / (fs->cub[a] - fs->clb[a]);
+      gc[a] = cv * v[a];
+      hd[a] = 0.0;
+    }
+    *c = cv;
+    *beta = cv;
+  }
+}
+
+/* value_only: α only (the line-search path); full: gradient, Hessian, mixed partials.
+ * With a cost model the acquisition is f = α/c (cost-weighted rule, build-defined):
+ *   ∇f = ∇α/c − α∇c/c²,  Hf = (Hα − ∇f∇cᵀ − ∇c∇fᵀ)/c − (α/c²)Hc,  ∂∇f/∂θ = ∂∇α/∂θ/c − g_θ∇c/c². */
 static void fsur_eval(const fsur_t* fs, const double* x, double theta, double sigma_tol, int fi,
                       int value_only, sx_t* sx, scratch_t* sc) {
   const int d = fs->d, cap = fs->cap, n = fs->N + fi + 1;
@@ -517,6 +555,15 @@ static void fsur_eval(const fsur_t* fs, const double* x, double theta, double si
   sx->fmin = fmin;
   sx->e = rule_partials(fs->rule, sx->mu, sx->sigma, theta, fmin, sigma_tol);
   sx->alpha = sx->e.g;
+  sx->alpha_raw = sx->e.g;
+  sx->cost = 1.0;
+  sx->gcmax = 0.0;
+  double chd[16], cbeta = 0.0, cv[16];
+  if (fs->cost) {
+    cost_eval(fs, x, &sx->cost, sx->gcost, chd, &cbeta, cv);
+    for (int a = 0; a < d; ++a) sx->gcmax = fmax(sx->gcmax, fabs(sx->gcost[a]));
+    sx->alpha = sx->e.g / sx->cost;
+  }
   if (value_only) return;
   /* ∇μ, Dw, ∇σ */
   for (int a = 0; a < d; ++a) {
@@ -558,6 +605,19 @@ static void fsur_eval(const fsur_t* fs, const double* x, double theta, double si
     for (int a = 0; a < d; ++a)
       sx->Halpha[a + d * b] = e->gmumu * sx->gmu[a] * sx->gmu[b] + e->gmu * Hmu[a + d * b] +
                               e->gsigsig * sx->gsig[a] * sx->gsig[b] + e->gsig * Hsig[a + d * b];
+  if (fs->cost) {
+    const double c = sx->cost, ac2 = sx->alpha_raw / (c * c);
+    for (int a = 0; a < d; ++a) {
+      sx->galpha[a] = sx->galpha[a] / c - ac2 * sx->gcost[a];
+      sx->mixed[a] = sx->mixed[a] / c - e->gth * sx->gcost[a] / (c * c);
+    }
+    for (int b = 0; b < d; ++b)
+      for (int a = 0; a < d; ++a) {
+        const double hc = ((a == b) ? chd[a] : 0.0) + cbeta * cv[a] * cv[b];
+        sx->Halpha[a + d * b] =
+            (sx->Halpha[a + d * b] - sx->galpha[a] * sx->gcost[b] - sx->gcost[a] * sx->galpha[b]) / c - ac2 * hc;
+      }
+  }
 }
 
 /* gp_draw(fs, x, θ; stdnormal, with_gradient=true, fantasy_index) :588-611; sx.dσ :530-539 */
@@ -639,14 +699,19 @@ static void k_gcert(const kern_t* k, double* gmu, double* gsig) {
  * ∇α zero or NaN, which stops the iteration as well.  When that cheap bound fails, the tight
  * one at the point itself: |∂_a μ| ≤ Σ_j |c_j| |ψ'(ρ_j)| over the surface's data rows, and
  * |∂_a σ| = |∂_a kxᵀK⁻¹kx|/σ ≤ √(−ψ''(0)) √(kxᵀK⁻¹kx)/σ with kxᵀK⁻¹kx = ψ(0) − σ². */
+/* With a cost model, f = α/c: |∂_a f| ≤ B/c + |α|·max|∇c|/c² for any bound B on |∂_a α|, and
+ * gμ = gσ = 0 certifies only where α = 0 as well (POI can sit at Φ = 1 with ∇f = −∇c/c²). */
 static int grad_certified(const solve_ctx* cx, const sx_t* sx, const double* x) {
   const double gm = sx->e.gmu, gs = sx->e.gsig;
-  if (gm == 0.0 && gs == 0.0) return 1;
+  const int cost = cx->fs->cost;
+  if (gm == 0.0 && gs == 0.0 && (!cost || sx->alpha_raw == 0.0)) return 1;
+  const double isc = cost ? 1.0 / sx->cost : 1.0;
+  const double add = cost ? fabs(sx->alpha_raw) * sx->gcmax / (sx->cost * sx->cost) : 0.0;
   double cmu, csig;
   k_gcert(&cx->fs->k, &cmu, &csig);
   if (!(csig > 0.0)) return 0;
   const double bound = fabs(gm) * cmu * cx->cabs + fabs(gs) * csig / sx->sigma;
-  if (bound <= 0.25 * cx->p->g_tol) return 1;
+  if (bound * isc + add <= 0.25 * cx->p->g_tol) return 1;
   const fsur_t* fs = cx->fs;
   const int d = fs->d, n = fs->N + cx->fi + 1;
   const double* c = fs->cs + (int64_t)(cx->fi + 1) * fs->cap;
@@ -658,7 +723,7 @@ static int grad_certified(const solve_ctx* cx, const sx_t* sx, const double* x) 
   const double psi0 = k_psi(&fs->k, 0.0), d2 = k_d2psi(&fs->k, 0.0);
   const double q = fmax(psi0 - sx->sigma * sx->sigma, 0.0);
   const double tight = fabs(gm) * bmu + fabs(gs) * 1.01 * sqrt(-d2) * sqrt(q) / sx->sigma;
-  return tight <= 0.25 * cx->p->g_tol;
+  return tight * isc + add <= 0.25 * cx->p->g_tol;
 }
 
 static double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -864,6 +929,10 @@ static void perturb_grad(const fsur_t* fs, const sx_t* sx, int S, int q, const d
     else
       out[a] = sx->e.gmu * dgmu[a] + sx->e.gsig * dgsig[a] + de.gmu * sx->gmu[a] + de.gsig * sx->gsig[a];
   }
+  if (fs->cost) {   /* δ∇(α/c) = δ∇α/c − δα ∇c/c², δα = gμ δμ + gσ δσ (first order; build-defined) */
+    const double c = sx->cost, da = sx->e.gmu * dmu + sx->e.gsig * dsig;
+    for (int a = 0; a < d; ++a) out[a] = out[a] / c - da * sx->gcost[a] / (c * c);
+  }
 }
 
 /* ------------------------------------------------------------------------------------
@@ -1062,7 +1131,7 @@ static int simulate_impl(const rbo_surrogate* s, const rbo_params* p, const doub
   {
     fsur_t fs;
     scratch_t sc;
-    fsur_alloc(&fs, s, h, p->rule);
+    fsur_alloc(&fs, s, h, p->rule, p);
     scratch_alloc(&sc, fs.cap, d);
 #pragma omp for schedule(dynamic, 1)
     for (int64_t tr = 0; tr < T; ++tr) {
@@ -1191,12 +1260,12 @@ int rbo_log_likelihood(int32_t d, int32_t N, int32_t kernel, double ell, double 
   return rc == 0 ? 0 : 1;
 }
 
-int rbo_eval_base(const rbo_surrogate* s, int32_t rule, double theta, double sigma_tol, int32_t P, const double* xs,
-                  double* out) {
+static int eval_base_impl(const rbo_surrogate* s, int32_t rule, double theta, double sigma_tol, int32_t P,
+                          const double* xs, double* out, const rbo_params* cost_p) {
   fsur_t fs;
   scratch_t sc;
   if (rule < 0 || rule > RBO_RULE_LCB) return -1;
-  if (fsur_alloc(&fs, s, 0, rule)) return -2;
+  if (fsur_alloc(&fs, s, 0, rule, cost_p)) return -2;
   scratch_alloc(&sc, fs.cap, s->d);
   const int d = s->d, stride = 3 + 4 * d + d * d;
   sx_t sx;
@@ -1211,4 +1280,14 @@ int rbo_eval_base(const rbo_surrogate* s, int32_t rule, double theta, double sig
   scratch_free(&sc);
   fsur_free(&fs);
   return 0;
+}
+
+int rbo_eval_base(const rbo_surrogate* s, int32_t rule, double theta, double sigma_tol, int32_t P, const double* xs,
+                  double* out) {
+  return eval_base_impl(s, rule, theta, sigma_tol, P, xs, out, NULL);
+}
+
+int rbo_eval_base_p(const rbo_surrogate* s, const rbo_params* p, int32_t P, const double* xs, double* out) {
+  if (!p) return -1;
+  return eval_base_impl(s, p->rule, p->theta, p->sigma_tol, P, xs, out, p);
 }

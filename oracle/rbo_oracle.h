@@ -71,7 +71,17 @@ typedef struct {
   int32_t with_gradient;
   int32_t nthreads;        /* OpenMP threads for the (restart, sample) loop      */
   int32_t rule;            /* RBO_RULE_* base decision rule of the trajectory    */
+  int32_t cost;            /* RBO_COST_*: NonUniformCost weighting of the inner-solve rule */
+  double cost_c0;          /* cost family parameters (see RBO_COST_*)            */
+  const double* cost_w;    /* d weights, or NULL when cost == RBO_COST_NONE      */
 } rbo_params;
+
+/* NonUniformCost (cost_functions.jl:5-20) as closed-form families.  The reference's cost is an
+ * arbitrary closure that no rule, surrogate or trajectory references (SURVEY.md §0 finding 5);
+ * the build defines the cost-weighted acquisition α(x)/c(x) of the inner policy solve with it
+ * (parity unpinned).  u_a = (x_a − lb_a)/(ub_a − lb_a):
+ *   QUADRATIC  c(x) = c0 + Σ_a w_a u_a²        LOGLINEAR  c(x) = c0 · exp(Σ_a w_a u_a)      */
+enum { RBO_COST_NONE = 0, RBO_COST_QUADRATIC = 1, RBO_COST_LOGLINEAR = 2 };
 
 /* base decision rules (decision_rules.jl:84-127) */
 enum { RBO_RULE_EI = 0, RBO_RULE_POI = 1, RBO_RULE_LCB = 2 };
@@ -92,6 +102,9 @@ double rbo_dual_uniform(uint64_t seed, int64_t traj, int32_t j, int32_t k);
  * [3+3d..3+3d+d²)=Hα (col-major), then d2α/dxdθ (d).  stride = 3+4d+d². */
 int rbo_eval_base(const rbo_surrogate* s, int32_t rule, double theta, double sigma_tol, int32_t P,
                   const double* xs, double* out);
+/* The same with the rule, θ, σtol and the NonUniformCost model of p (the cost-weighted α/c(x),
+ * ∇, H and ∂∇/∂θ; p->lbs / p->ubs define u).                                              */
+int rbo_eval_base_p(const rbo_surrogate* s, const rbo_params* p, int32_t P, const double* xs, double* out);
 
 /* simulate_trajectory_mc (rollout.jl:279-340) for R restarts x0s (d×R).
  * Outputs (caller-allocated, Julia layout):

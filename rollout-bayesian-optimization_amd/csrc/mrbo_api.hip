@@ -43,7 +43,7 @@ struct mrbo_plan {
   int device = 0;
   int d = 0, N = 0, RPL = 1, NR = 64, Npad = 64;
   mrbo_params_t p{};
-  std::vector<double> lbs, ubs;
+  std::vector<double> lbs, ubs, cost_w;
   int kernel = 0;
   double ell = 1, cK = 1, cP = 0, psi0 = 1, d2psi0 = -1, sn2 = 1e-6;
   double gcert_mu = 0, gcert_sig = -1;
@@ -54,6 +54,7 @@ struct mrbo_plan {
   double* dLinv = nullptr;  // L0⁻¹ in the kernel's LDS layout (Lay::SQ)
   double* dlbs = nullptr;
   double* dubs = nullptr;
+  double* dcost = nullptr;  // NonUniformCost table [lb (d), ub − lb (d), w (d)] (cost models only)
   double* dwork = nullptr;
   double* dytab = nullptr;  // batched starts: per-workgroup Y0(x_start) slices (square layout)
   double* dkxb = nullptr;   // batched starts, packed layouts: global start tables (start_tables_kernel)
@@ -149,8 +150,9 @@ int pick_grid(const void* fn, size_t fixed_bytes, size_t wave_bytes, int ncu, in
 }
 
 // ---- reductions: per (restart, component) block, deterministic tree order --------------
-// comp 0: values, 1..d: grad_x[a], d+1: grad_theta.  mode 0: ETO (mean, std n-1) -> eto;
-// mode 1: partial sums (Σ, Σ²) -> sums.
+// comp 0: values, 1..d: grad_x[a], d+1: grad_theta.  Two passes (mean, then centred squares)
+// in both modes.  mode 0: ETO (mean, std n-1) -> eto; mode 1: shard moments (Σx, M2 = Σ(x − x̄)²)
+// -> moments, merged across ranks by Chan's formula (mrbo/parallel.py).
 __global__ void __launch_bounds__(256) reduce_kernel(const double* values, const double* grad_x,
                                                      const double* grad_theta, int M, int d, int mode,
                                                      double* out) {
@@ -178,12 +180,8 @@ __global__ void __launch_bounds__(256) reduce_kernel(const double* values, const
   for (int m = tid; m < M; m += 256) s += elem(m);
   const double tot = block_sum(s);
   double s2 = 0.0;
-  if (mode == 0) {
-    const double mu = tot / M;
-    for (int m = tid; m < M; m += 256) { const double dv = elem(m) - mu; s2 += dv * dv; }
-  } else {
-    for (int m = tid; m < M; m += 256) { const double v = elem(m); s2 += v * v; }
-  }
+  const double mu = tot / M;
+  for (int m = tid; m < M; m += 256) { const double dv = elem(m) - mu; s2 += dv * dv; }
   const double tot2 = block_sum(s2);
   if (tid == 0) {
     int c0, c1;
@@ -251,6 +249,9 @@ static void fill_common(const mrbo_plan_t* P, KParams& kp) {
   kp.samples_total = P->p.samples_total > 0 ? P->p.samples_total : P->p.M;
   kp.X0 = P->dX0; kp.c0 = P->dc0; kp.Linv = P->dLinv; kp.lbs = P->dlbs; kp.ubs = P->dubs;
   kp.work = P->dwork; kp.work_stride = P->work_stride; kp.queue = P->dqueue; kp.ytab = P->dytab;
+  kp.cost = P->p.cost;
+  kp.cost_c0 = P->p.cost_c0;
+  kp.cost_tab = P->dcost;
 }
 
 // staging helper for MRBO_FLAG_HOST_POINTERS
@@ -304,7 +305,7 @@ static int reduce_common(mrbo_plan_t* P, const double* values, const double* gra
 // =========================================================================================
 extern "C" {
 
-const char* mrbo_version(void) { return "mrbo 0.1.0 (gfx950, fp64, ABI 1)"; }
+const char* mrbo_version(void) { return "mrbo 0.2.0 (gfx950, fp64, ABI 2)"; }
 const char* mrbo_last_error(void) { return g_err.c_str(); }
 
 int mrbo_device_count(void) {
@@ -325,6 +326,9 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   if (p->rule != MRBO_RULE_EI && p->rule != MRBO_RULE_POI && p->rule != MRBO_RULE_LCB)
     return fail(MRBO_ERR_ARG, "unknown decision rule %d", (int)p->rule);
   if (s->kernel < 0 || s->kernel > 4) return fail(MRBO_ERR_ARG, "kernel id %d", s->kernel);
+  if (p->cost < MRBO_COST_NONE || p->cost > MRBO_COST_LOGLINEAR) return fail(MRBO_ERR_ARG, "cost model %d", p->cost);
+  if (p->cost != MRBO_COST_NONE && !p->cost_w) return fail(MRBO_ERR_ARG, "cost model without weights");
+  if (p->cost != MRBO_COST_NONE && d > MAXD) return fail(MRBO_ERR_UNSUPPORTED, "cost model at d=%d > %d", d, MAXD);
   if (s->kernel == MRBO_KERNEL_PERIODIC && !(s->period > 0.0)) return fail(MRBO_ERR_ARG, "period %g", s->period);
   const int ldL = s->ldL > 0 ? s->ldL : N;
 
@@ -340,6 +344,8 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   P->ubs.assign(p->ubs, p->ubs + d);
   P->p.lbs = nullptr;
   P->p.ubs = nullptr;
+  if (p->cost != MRBO_COST_NONE) P->cost_w.assign(p->cost_w, p->cost_w + d);
+  P->p.cost_w = nullptr;
   P->kernel = s->kernel;
   P->ell = s->lengthscale;
   P->sn2 = s->sigma_n2;
@@ -386,7 +392,10 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) { delete P; return fail(MRBO_ERR_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e)); }
   KernelSet ks;
-  get_kset(d, P->RPL, ks);
+  if (!get_kset(d, P->RPL, ks)) {
+    delete P;
+    return fail(MRBO_ERR_UNSUPPORTED, "d=%d (rows per lane %d) not compiled into this library", d, P->RPL);
+  }
   // the kernel's image of L0⁻¹ (zero above the diagonal and on padded rows); the global
   // variant appends a row-packed copy (row k: columns 0..k) for the backward product
   std::vector<double> packed((size_t)ks.linv_dev, 0.0);
@@ -423,7 +432,8 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   // Matérn-5/2 + EI: the compile-time specialised rollout kernel
   // (MRBO_GENERIC_KERNEL=1 forces the generic instantiation, for A/B runs and tests)
   const char* gen = getenv("MRBO_GENERIC_KERNEL");
-  P->spec = (P->kernel == MRBO_KERNEL_MATERN52 && P->p.rule == MRBO_RULE_EI && !(gen && gen[0] == '1')) ? 1 : 0;
+  P->spec = (P->kernel == MRBO_KERNEL_MATERN52 && P->p.rule == MRBO_RULE_EI && P->p.cost == MRBO_COST_NONE &&
+             !(gen && gen[0] == '1')) ? 1 : 0;
   const void* rk = P->spec ? ks.rollout_spec : ks.rollout;
   const int waves0 =
       pick_grid(rk, fixed, ks.wave_bytes, prop.multiProcessorCount, wpg0, blocks0, smem0, 0, maxw);
@@ -459,7 +469,17 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
             (!P->batch || ks.square ||
              (hipMalloc(&P->dkxb, sizeof(double) * (size_t)P->NR * ns) == hipSuccess &&
               hipMalloc(&P->dgtab, sizeof(double) * (size_t)ns * ng) == hipSuccess)) &&
-            hipMalloc(&P->dqueue, sizeof(int) * 4) == hipSuccess;
+            hipMalloc(&P->dqueue, sizeof(int) * 4) == hipSuccess &&
+            (P->p.cost == MRBO_COST_NONE || hipMalloc(&P->dcost, sizeof(double) * 3 * d) == hipSuccess);
+  if (ok && P->p.cost != MRBO_COST_NONE) {
+    std::vector<double> tab(3 * (size_t)d);
+    for (int a = 0; a < d; ++a) {
+      tab[a] = P->lbs[a];
+      tab[d + a] = P->ubs[a] - P->lbs[a];
+      tab[2 * d + a] = P->cost_w[a];
+    }
+    ok = hipMemcpy(P->dcost, tab.data(), sizeof(double) * 3 * d, hipMemcpyHostToDevice) == hipSuccess;
+  }
   ok = ok && hipMemcpy(P->dX0, X0.data(), sizeof(double) * X0.size(), hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(P->dc0, c0.data(), sizeof(double) * c0.size(), hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(P->dLinv, packed.data(), sizeof(double) * packed.size(), hipMemcpyHostToDevice) == hipSuccess &&
@@ -478,7 +498,7 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
 int mrbo_plan_destroy(mrbo_plan_t* P) {
   if (!P) return MRBO_OK;
   for (void* b : {(void*)P->dX0, (void*)P->dc0, (void*)P->dLinv, (void*)P->dlbs, (void*)P->dubs, (void*)P->dwork, (void*)P->dytab,
-                  (void*)P->dkxb, (void*)P->dgtab, (void*)P->dqueue})
+                  (void*)P->dkxb, (void*)P->dgtab, (void*)P->dqueue, (void*)P->dcost})
     if (b) (void)hipFree(b);
   if (P->ev0) (void)hipEventDestroy(P->ev0);
   if (P->ev1) (void)hipEventDestroy(P->ev1);
@@ -604,9 +624,10 @@ int mrbo_eto_reduce(mrbo_plan_t* P, const double* values, const double* grad_x, 
   return reduce_common(P, values, grad_x, grad_theta, P ? P->p.M : 0, eto, 0, flags, stream);
 }
 
-int mrbo_partial_sums(mrbo_plan_t* P, const double* values, const double* grad_x, const double* grad_theta,
-                      int32_t M_local, double* sums, uint32_t flags, void* stream) {
-  return reduce_common(P, values, grad_x, grad_theta, M_local, sums, 1, flags, stream);
+int mrbo_partial_moments(mrbo_plan_t* P, const double* values, const double* grad_x, const double* grad_theta,
+                         int32_t M_local, double* moments, uint32_t flags, void* stream) {
+  if (P && (M_local < 1 || M_local > P->p.M)) return fail(MRBO_ERR_ARG, "M_local=%d outside [1, %d]", M_local, P->p.M);
+  return reduce_common(P, values, grad_x, grad_theta, M_local, moments, 1, flags, stream);
 }
 
 int mrbo_eval_base(mrbo_plan_t* P, int32_t npts, const double* xs, double* out, uint32_t flags, void* stream) {

@@ -22,6 +22,8 @@ constexpr int NCOUNT = 5;
 constexpr int NSTAMP = 17;  // MRBO_STAMPS regions (names in mrbo_api.hip)
 constexpr int FMAX = 6;    // fantasy points per trajectory = h+1  (h ≤ 5)
 constexpr int WAVE = 64;
+constexpr int MAXD = 16;   // widest input dimension of a cost model (mrbo_plan_create check)
+enum { COST_NONE = 0, COST_QUADRATIC = 1, COST_LOGLINEAR = 2 };   // mrbo_cost_t
 
 // evaluation modes (wave-uniform).  The front part (kernel rows, forward product, Gram, μ, σ,
 // EI and its gradient) runs in every mode but BACK; the back part (backward product w, and
@@ -81,7 +83,14 @@ struct KParams {
   const double* pts;    // eval_base: d×P
   double* pts_out;      // eval_base output
   unsigned long long* stamps;  // MRBO_STAMPS builds: per-region cycle totals (else null)
+  // NonUniformCost weighting of the inner-solve rule (mrbo_cost_t; 0 = none): f = α/c(x) with
+  // u_a = (x_a − lb_a)/del_a, QUADRATIC c = c0 + Σ w_a u_a², LOGLINEAR c = c0·exp(Σ w_a u_a)
+  // (a pointer, not arrays: array members would put the kernel's copy of KParams in scratch)
+  int cost;
+  double cost_c0;
+  const double* cost_tab;   // device [lb (d), del = ub − lb (d), w (d)]
 };
+
 
 // ---- packed L0⁻¹ layout: column j holds rows j..Npad-1 contiguously ----------------------
 __host__ __device__ __forceinline__ constexpr long long linv_colstart(int j, int Npad) {
@@ -344,6 +353,8 @@ __device__ __forceinline__ void rad_eval2(const Radial& k, double rho2a, double 
 struct EIp {
   double g, gmu, gsig, gmumu, gsigsig, gmuth, gsigth;
 };
+// ∂g/∂θ: −Φ (EI) and −φ/σ (POI) equal ∂g/∂μ; σ for LCB
+__device__ __forceinline__ double rule_gth(int rule, double gmu, double sig) { return rule == 2 ? sig : gmu; }
 enum { RULE_EI = 0, RULE_POI = 1, RULE_LCB = 2 };
 __device__ __forceinline__ EIp rule_partials(int rule, double mu, double sig, double theta, double fmin,
                                              double sigma_tol) {
@@ -392,6 +403,40 @@ __device__ __forceinline__ void rule_first(int rule, double mu, double sig, doub
   const EIp e = rule_partials(rule, mu, sig, theta, fmin, sigma_tol);
   gmu = e.gmu;
   gsig = e.gsig;
+}
+
+// c(x) and ∇c(x) of the cost model (lane-uniform; D compile-time).  Hc = diag(hd) + β v vᵀ:
+// QUADRATIC hd_a = 2w_a/del_a², β = 0; LOGLINEAR hd = 0, β = c, v_a = w_a/del_a.
+template <int D>
+__device__ __forceinline__ double cost_eval(const KParams& kp, const double (&x)[D], double (&gc)[D]) {
+  const double* lb = kp.cost_tab;
+  const double* del = kp.cost_tab + D;
+  const double* w = kp.cost_tab + 2 * D;
+  if (kp.cost == COST_QUADRATIC) {
+    double c = kp.cost_c0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+      const double u = (x[a] - lb[a]) / del[a];
+      c = fma(w[a] * u, u, c);
+      gc[a] = 2.0 * w[a] * u / del[a];
+    }
+    return c;
+  }
+  double t = 0.0;
+#pragma unroll
+  for (int a = 0; a < D; ++a) t = fma(w[a], (x[a] - lb[a]) / del[a], t);
+  const double c = kp.cost_c0 * xexp(t);
+#pragma unroll
+  for (int a = 0; a < D; ++a) gc[a] = c * (w[a] / del[a]);
+  return c;
+}
+// entry (a, b) of Hc at cost c (d = D)
+template <int D>
+__device__ __forceinline__ double cost_hess(const KParams& kp, double c, int a, int b) {
+  const double* del = kp.cost_tab + D;
+  const double* w = kp.cost_tab + 2 * D;
+  if (kp.cost == COST_QUADRATIC) return (a == b) ? 2.0 * w[a] / (del[a] * del[a]) : 0.0;
+  return c * (w[a] / del[a]) * (w[b] / del[b]);
 }
 
 // counter-based uniform (bit-identical to the host / oracle version)

@@ -61,8 +61,8 @@ struct Lay {
   static constexpr int U_DINV = U_GF + FMAX * D;         // Dinv row-major        FMAX*FMAX
   static constexpr int U_CF = U_DINV + FMAX * FMAX;      // fantasy coeffs/surf.  (FMAX+1)*FMAX
   static constexpr int U_FMIN = U_CF + (FMAX + 1) * FMAX;// fmin per surface      FMAX+1
-  static constexpr int U_SC = U_FMIN + FMAX + 1;         // scalars: μ,σ,α,G00,σ²,... 16
-  static constexpr int U_GMU = U_SC + 16;                // ∇μ   D
+  static constexpr int U_SC = U_FMIN + FMAX + 1;         // scalars: μ,σ,α,G00,σ²,... 18
+  static constexpr int U_GMU = U_SC + 18;                // ∇μ   D
   static constexpr int U_GSIG = U_GMU + D;               // ∇σ   D
   static constexpr int U_GAL = U_GSIG + D;               // ∇α   D
   static constexpr int U_MIX = U_GAL + D;                // d2α/dxdθ D
@@ -109,7 +109,18 @@ struct Lay {
 };
 // scalar slots in U_SC
 enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, SC_GSIG = 6, SC_GMUMU = 7,
-       SC_GSIGSIG = 8, SC_GMUTH = 9, SC_GSIGTH = 10, SC_FMIN = 11, SC_ST = 12, SC_CABS = 13 };
+       SC_GSIGSIG = 8, SC_GMUTH = 9, SC_GSIGTH = 10, SC_FMIN = 11, SC_ST = 12, SC_CABS = 13,
+       // NonUniformCost (kp.cost): the rule value g before weighting, c(x), max_a |∂_a c(x)|
+       SC_ARAW = 14, SC_COSTC = 15, SC_GCMAX = 16 };
+
+// ∂_lane c(x) by unrolled select (lane < D; a runtime index would put gc in scratch)
+template <int D>
+__device__ __forceinline__ double lane_pick(const double (&v)[D], int lane) {
+  double r = 0.0;
+#pragma unroll
+  for (int a = 0; a < D; ++a) r = (a == lane) ? v[a] : r;
+  return r;
+}
 
 // Per-workgroup LDS after L0⁻¹: [xstarts (d×nstarts)] [kxb (NR×nstarts)] [gtab (nstarts×NG)],
 // each rounded to an even number of doubles; then the per-wave areas.  gtab[k] is the base
@@ -621,10 +632,24 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   const double sig = sqrt(var);
   const double fmin = U[Ly::U_FMIN + S + 1];
   const EIp e = rule_partials(kp.rule, mu, sig, kp.theta, fmin, kp.sigma_tol);
+  double alpha = e.g;
+  if (kp.cost) {   // cost-weighted rule f = α/c(x) (NonUniformCost, cost_functions.jl:5-20)
+    double gc[D];
+    const double c = cost_eval<D>(kp, x, gc);
+    double gmax = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) gmax = fmax(gmax, fabs(gc[a]));
+    alpha = e.g / c;
+    if (lane == 0) {
+      U[Ly::U_SC + SC_ARAW] = e.g;
+      U[Ly::U_SC + SC_COSTC] = c;
+      U[Ly::U_SC + SC_GCMAX] = gmax;
+    }
+  }
   if (lane == 0) {
     U[Ly::U_SC + SC_SIG] = sig;
     U[Ly::U_SC + SC_VAR] = var;
-    U[Ly::U_SC + SC_ALPHA] = e.g;
+    U[Ly::U_SC + SC_ALPHA] = alpha;
     U[Ly::U_SC + SC_GMU] = e.gmu;
     U[Ly::U_SC + SC_GSIG] = e.gsig;
     U[Ly::U_SC + SC_GMUMU] = e.gmumu;
@@ -647,8 +672,18 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     const double gs = -U[Ly::U_G + (1 + lane) * D1] * (1.0 / sig_f);  // ∇σ = -(∇kx·w)/σ
     const double gm = U[Ly::U_GMU + lane];
     U[Ly::U_GSIG + lane] = gs;
-    U[Ly::U_GAL + lane] = e_f.gmu * gm + e_f.gsig * gs;                // ∇αx :567
-    U[Ly::U_MIX + lane] = gm * e_f.gmuth + gs * e_f.gsigth;            // d2α_dxdθ :575-577
+    double gal = e_f.gmu * gm + e_f.gsig * gs;                         // ∇αx :567
+    double mix = gm * e_f.gmuth + gs * e_f.gsigth;                     // d2α_dxdθ :575-577
+    if (kp.cost) {   // ∇(α/c) = ∇α/c − α∇c/c²,  ∂∇(α/c)/∂θ = ∂∇α/∂θ/c − g_θ∇c/c²
+      double gc[D];
+      (void)cost_eval<D>(kp, x, gc);
+      const double gca = lane_pick<D>(gc, lane);
+      const double c = U[Ly::U_SC + SC_COSTC], araw = U[Ly::U_SC + SC_ARAW];
+      gal = gal / c - (araw / (c * c)) * gca;
+      mix = mix / c - rule_gth(kp.rule, e_f.gmu, sig_f) * gca / (c * c);
+    }
+    U[Ly::U_GAL + lane] = gal;
+    U[Ly::U_MIX + lane] = mix;
   }
   if (mode == EV_GRAD || mode == EV_GRADC || mode == EV_GSTART) {   // a BACK evaluation may follow
     wave_sync();
@@ -821,6 +856,13 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       if (a == b) hv = fma(coef, hf[D], hv);
     }
     hv += e.gmumu * gma * gmb + e.gsigsig * gsa * gsb - gsig_over * (gsa * gsb + U[Ly::U_G + (1 + a) * D1 + 1 + b]);
+    if (kp.cost) {   // H(α/c) = (Hα − ∇f∇cᵀ − ∇c∇fᵀ)/c − (α/c²)Hc, ∇f = U_GAL (weighted)
+      double gc[D];
+      (void)cost_eval<D>(kp, x, gc);
+      const double gca = lane_pick<D>(gc, a), gcb = lane_pick<D>(gc, b);
+      const double c = U[Ly::U_SC + SC_COSTC], araw = U[Ly::U_SC + SC_ARAW];
+      hv = (hv - U[Ly::U_GAL + a] * gcb - gca * U[Ly::U_GAL + b]) / c - (araw / (c * c)) * cost_hess<D>(kp, c, a, b);
+    }
     U[Ly::U_H + a * D + b] = hv;
     U[Ly::U_H + b * D + a] = hv;
   }
@@ -883,11 +925,6 @@ __device__ __forceinline__ int draw(WaveCtx<D, RPL>& W, const KParams& kp, const
   using Ly = Lay<D, RPL>;
   constexpr int D1 = Ly::D1;
   const double* U = W.U;
-#ifdef MRBO_EXP_STUB_DRAW
-  yv = U[Ly::U_SC + SC_MU] + z[0];
-  for (int a = 0; a < D; ++a) gy[a] = U[Ly::U_GMU + a] + z[1 + a];
-  return 0;
-#endif
   double Lc[D1 * (D1 + 1) / 2];
 #define TRI(i, j) ((i) * ((i) + 1) / 2 + (j))
 #pragma unroll
@@ -1117,8 +1154,14 @@ __device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const K
   const double* U = W.U;
   const double gm = U[Ly::U_SC + SC_GMU], gs = U[Ly::U_SC + SC_GSIG];
   const double cabs = U[Ly::U_SC + SC_CABS], sig = U[Ly::U_SC + SC_SIG];   // unconditional loads
-  const double bound = fabs(gm) * kp.gcert_mu * cabs + fabs(gs) * kp.gcert_sig / sig;
-  return ((gm == 0.0) & (gs == 0.0)) | ((kp.gcert_sig > 0.0) & (bound <= 0.25 * kp.g_tol));
+  double bound = fabs(gm) * kp.gcert_mu * cabs + fabs(gs) * kp.gcert_sig / sig;
+  bool zero = (gm == 0.0) & (gs == 0.0);
+  if (kp.cost) {   // f = α/c: |∂f| ≤ B/c + |α| max|∇c|/c²; gμ = gσ = 0 certifies only where α = 0
+    const double araw = U[Ly::U_SC + SC_ARAW], c = U[Ly::U_SC + SC_COSTC];
+    bound = bound * (1.0 / c) + fabs(araw) * U[Ly::U_SC + SC_GCMAX] / (c * c);
+    zero = zero & (araw == 0.0);
+  }
+  return zero | ((kp.gcert_sig > 0.0) & (bound <= 0.25 * kp.g_tol));
 }
 
 // Tight certificate at x = U[U_X] on surface S, where grad_certified's cheap bound failed
@@ -1132,21 +1175,34 @@ __device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const K
 // ROWS_KEPT: the VALUE evaluation at x just ran on surface S, so g1 = ψ'(ρ)/ρ of every base
 // row (G12) and fantasy row (U_HF) is still in LDS -- the same bits a new radial evaluation
 // would give; only ρ is recomputed.
+// With a cost model (f = α/c, araw = α at x) every bound B on |∂α| becomes B/c + |α| max|∇c|/c².
 template <int D, int RPL, bool ROWS_KEPT = false>
 __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParams& kp, int S, double gm, double gs,
-                                                double sig) {
+                                                double sig, double araw = 0.0) {
   using Ly = Lay<D, RPL>;
   constexpr int NR = Ly::NR;
   const double* U = W.U;
   const int lane = W.ln();
   const int nf = S + 1;
+  double isc = 1.0, add = 0.0;
+  if (kp.cost) {
+    double xc[D], gc[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) xc[a] = U[Ly::U_X + a];
+    const double c = cost_eval<D>(kp, xc, gc);
+    double gmax = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) gmax = fmax(gmax, fabs(gc[a]));
+    isc = 1.0 / c;
+    add = fabs(araw) * gmax / (c * c);
+  }
   // the σ part needs no rows: if it alone exceeds the threshold the test fails, and with the
   // cheap μ part (Σ|c|·max|ψ'| ≥ the row sum) it may already pass -- same decisions as the
   // full test, without the row pass
   const double q = fmax(kp.psi0 - sig * sig, 0.0);
   const double bsig = fabs(gs) * kp.gcert_d2 * sqrt(q) / sig, thr = 0.25 * kp.g_tol;
-  if (!(bsig <= thr)) return false;
-  if (fabs(gm) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + bsig <= thr) return true;
+  if (!(bsig * isc + add <= thr)) return false;
+  if ((fabs(gm) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + bsig) * isc + add <= thr) return true;
   double x[D];
 #pragma unroll
   for (int a = 0; a < D; ++a) x[a] = U[Ly::U_X + a];
@@ -1176,7 +1232,7 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParam
   wave_sync();
   const double bmu = W.red[0];
   wave_sync();
-  return fabs(gm) * bmu + bsig <= thr;
+  return (fabs(gm) * bmu + bsig) * isc + add <= thr;
 }
 
 // Deterministic projected Newton on f = -α over the box, from start k.
@@ -1189,7 +1245,7 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParam
 template <int D, int RPL>
 __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, int S, int k, Counters& nevals,
                                          int& st, LaneRes<D, RPL>& lr, double f0, bool have_f0, double gm0 = 0.0,
-                                         double gs0 = 0.0, double sig0 = 0.0) {
+                                         double gs0 = 0.0, double sig0 = 0.0, double a0 = 0.0) {
   using Ly = Lay<D, RPL>;
   double* U = W.U;
   const int lane = W.ln();
@@ -1202,7 +1258,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
   wave_sync();
   // a batched start whose cheap certificate failed: the tight one at x_start (gμ, gσ, σ of the
   // batched value) before any gradient work
-  if (have_f0 && kp.gcert_sig > 0.0 && tight_certified<D, RPL>(W, kp, S, gm0, gs0, sig0)) {
+  if (have_f0 && kp.gcert_sig > 0.0 && tight_certified<D, RPL>(W, kp, S, gm0, gs0, sig0, a0)) {
     wave_sync();
     return f0;
   }
@@ -1273,7 +1329,8 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
     if (f != f) break;
     if (grad_certified<D, RPL>(W, kp)) break;     // ‖∇α‖ ≤ g_tol guaranteed: stationary
     if (kp.gcert_sig > 0.0 &&
-        tight_certified<D, RPL, true>(W, kp, S, U[Ly::U_SC + SC_GMU], U[Ly::U_SC + SC_GSIG], U[Ly::U_SC + SC_SIG]))
+        tight_certified<D, RPL, true>(W, kp, S, U[Ly::U_SC + SC_GMU], U[Ly::U_SC + SC_GSIG], U[Ly::U_SC + SC_SIG],
+                                      kp.cost ? U[Ly::U_SC + SC_ARAW] : 0.0))
       break;
     STAMP(W, 12);
     phase = P_GRAD;
@@ -1371,8 +1428,8 @@ __device__ __forceinline__ void stage_start_tables(const KParams& kp, double* sm
 template <int D, int RPL>
 __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KParams& kp, int S, double& f_lane,
                                                    double& gm_lane, double& gs_lane, double& sig_lane,
-                                                   unsigned long long& stopmask, unsigned long long& xnanmask,
-                                                   bool& varneg) {
+                                                   double& a_lane, unsigned long long& stopmask,
+                                                   unsigned long long& xnanmask, bool& varneg) {
   using Ly = Lay<D, RPL>;
   constexpr int NR = Ly::NR;
   const double* U = W.U;
@@ -1530,10 +1587,22 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   const double var = kp.psi0 - g00;
   const double sig = sqrt(var);
   const EIp e = rule_partials(kp.rule, mu, sig, kp.theta, U[Ly::U_FMIN + S + 1], kp.sigma_tol);
-  bool cert = (e.gmu == 0.0 && e.gsig == 0.0);
-  if (!cert && kp.gcert_sig > 0.0)
-    cert = fabs(e.gmu) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + fabs(e.gsig) * kp.gcert_sig / sig <= 0.25 * kp.g_tol;
-  f_lane = -e.g;
+  double fval = e.g, cval = 1.0, gcm = 0.0;
+  if (kp.cost) {   // cost-weighted rule at the start point (see grad_certified)
+    double gc[D];
+    cval = cost_eval<D>(kp, x, gc);
+#pragma unroll
+    for (int a = 0; a < D; ++a) gcm = fmax(gcm, fabs(gc[a]));
+    fval = e.g / cval;
+  }
+  bool cert = (e.gmu == 0.0 && e.gsig == 0.0) && (!kp.cost || e.g == 0.0);
+  if (!cert && kp.gcert_sig > 0.0) {
+    double b = fabs(e.gmu) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + fabs(e.gsig) * kp.gcert_sig / sig;
+    if (kp.cost) b = b * (1.0 / cval) + fabs(e.g) * gcm / (cval * cval);
+    cert = b <= 0.25 * kp.g_tol;
+  }
+  f_lane = -fval;
+  a_lane = e.g;
   gm_lane = e.gmu;
   gs_lane = e.gsig;
   sig_lane = sig;
@@ -1570,12 +1639,12 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
     if (lane == 0) U[Ly::U_SC + SC_CABS] = cabs;
     wave_sync();
   }
-  double f_lane = 0.0, gm_lane = 0.0, gs_lane = 0.0, sig_lane = 0.0;
+  double f_lane = 0.0, gm_lane = 0.0, gs_lane = 0.0, sig_lane = 0.0, a_lane = 0.0;
   unsigned long long stopmask = 0, xnanmask = 0;
   if (kp.batch) {
     bool varneg = false;
     STAMP(W, 16);
-    batch_start_values<D, RPL>(W, kp, S, f_lane, gm_lane, gs_lane, sig_lane, stopmask, xnanmask, varneg);
+    batch_start_values<D, RPL>(W, kp, S, f_lane, gm_lane, gs_lane, sig_lane, a_lane, stopmask, xnanmask, varneg);
     STAMP(W, 15);
     nevals.value += kp.nstarts;
     if (varneg) st |= 1;
@@ -1585,7 +1654,8 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
   for (int k = 0; k < kp.nstarts; ++k) {
     if ((stopmask >> k) & 1ull) continue;
     const double fo = kp.batch ? newton<D, RPL>(W, kp, S, k, nevals, st, lr, readlane_d(f_lane, k), true,
-                                                readlane_d(gm_lane, k), readlane_d(gs_lane, k), readlane_d(sig_lane, k))
+                                                readlane_d(gm_lane, k), readlane_d(gs_lane, k), readlane_d(sig_lane, k),
+                                                kp.cost ? readlane_d(a_lane, k) : 0.0)
                                : newton<D, RPL>(W, kp, S, k, nevals, st, lr, 0.0, false);
     bool xnan = false;
 #pragma unroll
@@ -1756,6 +1826,16 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
   const double dsig = wq * (udw - dkx) * isig;
   double dgm, dgs;
   rule_first(kp.rule, dmu, dsig, kp.theta, U[Ly::U_SC + SC_FMIN], kp.sigma_tol, dgm, dgs);
+  // cost-weighted rule: δ∇(α/c) = δ∇α/c − δα ∇c/c², δα = gμ δμ + gσ δσ (build-defined)
+  double gcx[D], cc = 1.0, dal = 0.0;
+  if (kp.cost) {
+    double xi[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) xi[a] = U[Ly::U_X + a];
+    (void)cost_eval<D>(kp, xi, gcx);
+    cc = U[Ly::U_SC + SC_COSTC];
+    dal = gmu * dmu + gsig * dsig;
+  }
   double contrib = 0.0;
 #pragma unroll
   for (int a = 0; a < D; ++a) {
@@ -1768,6 +1848,7 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
       const double dgsig = (Pqa * udw + Pu[a] * wq - dgkx[a] * wq - Pqa * dkx - dsig * gsa) * isig;
       da += gsig * dgsig;
     }
+    if (kp.cost) da = da / cc - dal * gcx[a] / (cc * cc);
     contrib = fma(da, U[Ly::U_XBAR + (i_pol - 1) * D + a], contrib);
   }
   if (lane < D) U[Ly::U_ACC + q * D + lane] += contrib;
@@ -1920,6 +2001,8 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
     kp.evals[NCOUNT * oidx + 0] = nevals.grad;
     kp.evals[NCOUNT * oidx + 1] = nevals.value;
     kp.evals[NCOUNT * oidx + 2] = nevals.hess;
+    kp.evals[NCOUNT * oidx + 3] = 0;   // adjoint counters: overwritten below unless the trajectory failed
+    kp.evals[NCOUNT * oidx + 4] = 0;
   }
   if (st) {
     if (lane == 0) { kp.values[oidx] = NAN; kp.status[oidx] = st; if (kp.grad_theta) kp.grad_theta[oidx] = NAN; }
@@ -2090,6 +2173,7 @@ __global__ void __launch_bounds__(KBounds<RPL>::threads, KBounds<RPL>::waves_per
   if constexpr (SPEC == 1) {
     kp.kernel = KERNEL_MATERN52;
     kp.rule = RULE_EI;
+    kp.cost = COST_NONE;
   }
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // stage L0⁻¹ (and the inner-solve start points) once per workgroup (the only block barrier)

@@ -13,6 +13,8 @@ LIB_PATH = os.environ.get("MRBO_LIB") or os.path.join(_HERE, "libmrbo.so")  # MR
 _dp = ctypes.POINTER(ctypes.c_double)
 _vp = ctypes.c_void_p
 
+# NonUniformCost families (mrbo_cost_t)
+COSTS = {"none": 0, "quadratic": 1, "loglinear": 2}
 MRBO_FLAG_HOST_POINTERS = 1
 MRBO_FLAG_NO_GRADIENT = 2
 # per-trajectory work counters of mrbo_simulate_mc `evals` (MRBO_NCOUNTERS in include/mrbo.h)
@@ -30,7 +32,7 @@ STATUS_BITS = {
 # exported symbols of include/mrbo.h (the library must export all of them)
 EXPORTS = [
     "mrbo_version", "mrbo_last_error", "mrbo_device_count", "mrbo_plan_create", "mrbo_plan_destroy",
-    "mrbo_simulate_mc", "mrbo_simulate_ghq", "mrbo_eto_reduce", "mrbo_partial_sums", "mrbo_eval_base", "mrbo_rnstream",
+    "mrbo_simulate_mc", "mrbo_simulate_ghq", "mrbo_eto_reduce", "mrbo_partial_moments", "mrbo_eval_base", "mrbo_rnstream",
     "mrbo_initial_guesses", "mrbo_dual_uniform", "mrbo_last_kernel_ms", "mrbo_gp_fit",
     "mrbo_plan_info", "mrbo_last_gp_fit_ms", "mrbo_plan_set_order",
 ]
@@ -48,7 +50,8 @@ class ParamsDesc(ctypes.Structure):
                 ("max_iters", ctypes.c_int32), ("max_ls", ctypes.c_int32), ("x_tol", ctypes.c_double),
                 ("f_tol", ctypes.c_double), ("g_tol", ctypes.c_double), ("htol", ctypes.c_double),
                 ("sigma_tol", ctypes.c_double), ("seed", ctypes.c_uint64),
-                ("sample_offset", ctypes.c_int32), ("samples_total", ctypes.c_int32)]
+                ("sample_offset", ctypes.c_int32), ("samples_total", ctypes.c_int32),
+                ("cost", ctypes.c_int32), ("cost_c0", ctypes.c_double), ("cost_w", _dp)]
 
 
 _lib = None
@@ -82,7 +85,7 @@ def load():
     L.mrbo_simulate_mc.argtypes = [_vp] + [_vp] * 12 + [ctypes.c_uint32, _vp]
     L.mrbo_simulate_ghq.argtypes = [_vp] + [_vp] * 13 + [ctypes.c_uint32, _vp]
     L.mrbo_eto_reduce.argtypes = [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]
-    L.mrbo_partial_sums.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_int32, _vp, ctypes.c_uint32, _vp]
+    L.mrbo_partial_moments.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_int32, _vp, ctypes.c_uint32, _vp]
     L.mrbo_eval_base.argtypes = [_vp, ctypes.c_int32, _vp, _vp, ctypes.c_uint32, _vp]
     L.mrbo_rnstream.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _dp]
     L.mrbo_initial_guesses.argtypes = [ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp]

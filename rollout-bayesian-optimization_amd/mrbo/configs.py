@@ -36,10 +36,15 @@ CONFIGS = {
     "C3": Config("C3", "hartmann6d", 6, 3, 1024, 64, 64, 1, "6D Hartmann, h=3, 1024 MC x 64 restarts, n=64 (headline)"),
     "C4": Config("C4", "hartmann6d", 6, 4, 8192, 256, 128, 8, "6D Hartmann, h=4, 8192 MC x 256 restarts, n=128"),
     # BASELINE names "8D Ackley + NonUniformCost": NonUniformCost (cost_functions.jl:5-20) is
-    # referenced by no decision rule, surrogate or trajectory (SURVEY.md §0 finding 5), so the
-    # rollout path is the plain EI one; the cost enters nothing here either
+    # referenced by no decision rule, surrogate or trajectory (SURVEY.md §0 finding 5); the build
+    # defines the cost-weighted inner-solve rule α/c(x) (include/mrbo.h mrbo_cost_t, parity
+    # unpinned) and C5 runs it with Problem(cost=True) / bench.py --cost
     "C5": Config("C5", "ackley", 8, 5, 16384, 512, 256, 8, "8D Ackley, h=5, 16384 MC x 512 restarts, n=256"),
 }
+
+# C5's NonUniformCost: c(x) = 1 + Σ_a u_a², u = (x − lb)/(ub − lb) -- a bowl from 1 at the lower
+# corner to 1 + d at the upper one (build-defined)
+C5_COST = ("quadratic", 1.0, 1.0)
 
 
 def make_testfn(name, d):
@@ -48,8 +53,9 @@ def make_testfn(name, d):
 
 
 class Problem:
-    def __init__(self, cfg, M=None, R=None, capacity=None, nstarts=16):
+    def __init__(self, cfg, M=None, R=None, capacity=None, nstarts=16, cost=False):
         self.cfg = cfg
+        self.cost = (C5_COST[0], C5_COST[1], np.full(cfg.d, C5_COST[2])) if cost else None
         tf = make_testfn(cfg.testfn, cfg.d)
         lbs, ubs = tf.get_bounds()
         self.lbs, self.ubs = lbs, ubs
@@ -66,6 +72,18 @@ class Problem:
         self.es = ExperimentSetup(tp=self.tp, number_of_starts=nstarts)
         self.fs = FantasySurrogate(self.surrogate, cfg.h)
         self.T = Trajectory(self.surrogate, self.fs, start=self.x0s[:, 0], hypers=[0.0], horizon=cfg.h)
+
+
+    def cost_model(self):
+        """(kind, c0, w) of the NonUniformCost weighting, or None"""
+        return self.cost
+
+    def plan_opts(self):
+        """RolloutPlan options of this problem beyond the defaults (the cost model)"""
+        if self.cost is None:
+            return {}
+        kind, c0, w = self.cost
+        return dict(cost=kind, cost_c0=float(c0), cost_w=tuple(float(v) for v in w))
 
 
 def problem(name, **kw):

@@ -11,7 +11,7 @@ import numpy as np
 from . import _lib
 
 DEFAULTS = dict(max_iters=50, max_ls=20, x_tol=1e-3, f_tol=1e-3, g_tol=1e-8, htol=1e-4, sigma_tol=1e-8, seed=1906,
-                sample_offset=0, samples_total=0)
+                sample_offset=0, samples_total=0, cost="none", cost_c0=1.0, cost_w=())
 
 
 def _torch():
@@ -55,11 +55,16 @@ class RolloutPlan:
         sd = _lib.SurrogateDesc(self.d, self.N, int(kernel), float(lengthscale), float(sigma_n2), float(fmini),
                                 self._X.ctypes.data_as(dp), self._L.ctypes.data_as(dp), self.N,
                                 self._c.ctypes.data_as(dp), self._y.ctypes.data_as(dp), float(period))
+        ck = _lib.COSTS[o["cost"]] if isinstance(o["cost"], str) else int(o["cost"])
+        self._cost_w = _f64(o["cost_w"]).ravel() if ck else None
+        if ck and self._cost_w.size != self.d:
+            raise ValueError(f"cost_w has {self._cost_w.size} weights for d = {self.d}")
         pd = _lib.ParamsDesc(self.h, self.M, self.R, self.nstarts, int(o.get("rule", 0)), self.theta,
                              self._lbs.ctypes.data_as(dp),
                              self._ubs.ctypes.data_as(dp), int(o["max_iters"]), int(o["max_ls"]), float(o["x_tol"]),
                              float(o["f_tol"]), float(o["g_tol"]), float(o["htol"]), float(o["sigma_tol"]),
-                             int(o["seed"]), int(o.get("sample_offset", 0)), int(o.get("samples_total", 0)))
+                             int(o["seed"]), int(o.get("sample_offset", 0)), int(o.get("samples_total", 0)),
+                             ck, float(o["cost_c0"]), self._cost_w.ctypes.data_as(dp) if ck else None)
         h_ = ctypes.c_void_p()
         _lib.check(self.lib.mrbo_plan_create(ctypes.byref(sd), ctypes.byref(pd), int(device), ctypes.byref(h_)))
         self.handle = h_
@@ -127,13 +132,14 @@ class RolloutPlan:
                                             p(out.get("grad_theta")), p(e), 0, ctypes.c_void_p(st.cuda_stream)))
         return e
 
-    def partial_sums(self, out, M_local, stream=None):
+    def partial_moments(self, out, M_local, stream=None):
+        """mrbo_partial_moments: this shard's (W·R) [Σ, M2] rows, device tensor (parallel.py)."""
         torch = _torch()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         W = 2 + 2 * self.d + 2
         e = torch.empty(W * self.R, dtype=torch.float64, device=f"cuda:{self.device}")
         p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
-        _lib.check(self.lib.mrbo_partial_sums(self.handle, p(out["values"]), p(out.get("grad_x")),
+        _lib.check(self.lib.mrbo_partial_moments(self.handle, p(out["values"]), p(out.get("grad_x")),
                                               p(out.get("grad_theta")), int(M_local), p(e), 0,
                                               ctypes.c_void_p(st.cuda_stream)))
         return e

@@ -1,10 +1,13 @@
 """Multi-GPU sharding of the rollout: one process per GPU.
 
 The M Monte-Carlo samples of every restart are split into contiguous blocks of the shared
-rnstream; each rank runs its block for all R restarts (no data-path communication), reduces
-its per-restart partial sums [Σα, Σα², Σ∇x, Σ∇x², Σ∇θ, Σ∇θ²] on the device, and ONE
-all-reduce (RCCL over xGMI on the GPU box, gloo on CPU tests) per outer SGA step combines
-them.  Every rank then derives the same ETO and takes the same ascent step.
+rnstream; each rank runs its block for all R restarts (no data-path communication) and reduces
+its per-restart moments on the device -- the local sum Σx and the local centred second moment
+M2 = Σ(x − x̄_local)² of [α, ∇x (d), ∇θ] (two passes over its samples, mrbo_partial_moments).
+ONE all-gather (RCCL over xGMI on the GPU box, gloo on CPU tests) per outer SGA step hands every
+rank the world's (n_k, Σ_k, M2_k); each rank merges them with Chan's parallel formula in rank
+order, so all ranks derive the same ETO -- the two-pass mean and n−1 std of rollout.jl:328-337,
+without the cancellation of a one-pass Σx² − (Σx)²/n -- and take the same ascent step.
 """
 import numpy as np
 
@@ -17,33 +20,90 @@ def shard(M, world, rank):
     return lo, hi
 
 
-def eto_from_sums(sums, M, d):
-    """sums: (W, R) of [Σα, Σα², Σ∇x(d), Σ∇x²(d), Σ∇θ, Σ∇θ²] over all M samples → ETO rows
-    [μ, σ(n-1), grad_μx, σ∇x, grad_μθ, σ∇θ] (rollout.jl:328-339)."""
-    sums = np.asarray(sums, dtype=np.float64)
-    W, R = sums.shape
-    out = np.zeros_like(sums)
+def width(d):
+    """rows per restart of an ETO / moments block: [α, σα, ∇x (d), σ∇x (d), ∇θ, σ∇θ]"""
+    return 2 + 2 * d + 2
 
-    def ms(s1, s2):
-        mu = s1 / M
-        var = (s2 - s1 * mu) / (M - 1) if M > 1 else np.full_like(s1, np.nan)
-        return mu, np.sqrt(np.maximum(var, 0.0))
 
-    out[0], out[1] = ms(sums[0], sums[1])
-    mu, sd = ms(sums[2:2 + d], sums[2 + d:2 + 2 * d])
-    out[2:2 + d], out[2 + d:2 + 2 * d] = mu, sd
-    out[2 + 2 * d], out[3 + 2 * d] = ms(sums[2 + 2 * d], sums[3 + 2 * d])
+def _split(a, d):
+    """(first moments, second moments) rows of a (W, R) block, component order [α, ∇x (d), ∇θ]"""
+    s = np.concatenate([a[0:1], a[2:2 + d], a[2 + 2 * d:3 + 2 * d]])
+    q = np.concatenate([a[1:2], a[2 + d:2 + 2 * d], a[3 + 2 * d:4 + 2 * d]])
+    return s, q
+
+
+def _join(s, q, d):
+    out = np.empty((width(d), s.shape[1]))
+    out[0], out[1] = s[0], q[0]
+    out[2:2 + d], out[2 + d:2 + 2 * d] = s[1:1 + d], q[1:1 + d]
+    out[2 + 2 * d], out[3 + 2 * d] = s[1 + d], q[1 + d]
     return out
 
 
-def allreduce_sums(sums_tensor, group=None):
-    """one sum all-reduce of the (W·R) partial sums (fp64)."""
+def local_moments(values, grad_x, grad_theta):
+    """Host restatement of mrbo_partial_moments for one shard: values (M, R), grad_x (d, M, R),
+    grad_theta (M, R) -> (W, R) rows [Σα, M2α, Σ∇x, M2∇x, Σ∇θ, M2∇θ] (two-pass M2)."""
+    v = np.asarray(values, dtype=np.float64)
+    gx = np.asarray(grad_x, dtype=np.float64)
+    gt = np.asarray(grad_theta, dtype=np.float64).reshape(v.shape)
+    d = gx.shape[0]
+    comps = np.concatenate([v[None], gx, gt[None]])          # (d+2, M, R)
+    n = comps.shape[1]
+    s = comps.sum(axis=1)
+    q = ((comps - (s / n)[:, None, :]) ** 2).sum(axis=1)
+    return _join(s, q, d)
+
+
+def merge_moments(parts, d):
+    """Chan et al.'s pairwise merge of per-shard moments, left to right (rank order).
+    parts: sequence of (n_k, (W, R) moments block).  Returns (n, merged block)."""
+    n, acc = None, None
+    for nk, blk in parts:
+        sk, qk = _split(np.asarray(blk, dtype=np.float64), d)
+        if nk == 0:
+            continue
+        if acc is None:
+            n, s, q = nk, sk.copy(), qk.copy()
+            acc = True
+            continue
+        delta = sk / nk - s / n
+        q = q + qk + delta * delta * (n * nk / (n + nk))
+        s = s + sk
+        n = n + nk
+    if acc is None:
+        raise ValueError("no samples in any shard")
+    return n, _join(s, q, d)
+
+
+def eto_from_moments(moments, M, d):
+    """(W, R) merged [Σ, M2] rows over all M samples -> ETO rows [μ, σ(n-1), ∇μx, σ∇x, ∇μθ, σ∇θ]
+    (rollout.jl:328-339; M = 1 gives NaN std, Q14)."""
+    s, q = _split(np.asarray(moments, dtype=np.float64), d)
+    mu = s / M
+    with np.errstate(invalid="ignore", divide="ignore"):
+        sd = np.sqrt(q / (M - 1)) if M > 1 else np.full_like(q, np.nan)
+    return _join(mu, sd, d)
+
+
+def allgather_moments(moments_tensor, group=None):
+    """ONE all-gather of every rank's flat (W·R) moments tensor; returns a list, rank order.
+    gloo cannot gather device tensors: they travel through host memory on that backend."""
+    import torch
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        if sums_tensor.is_cuda and dist.get_backend(group) == "gloo":
-            host = sums_tensor.cpu()
-            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
-            sums_tensor.copy_(host)
-        else:
-            dist.all_reduce(sums_tensor, op=dist.ReduceOp.SUM, group=group)
-    return sums_tensor
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1):
+        return [moments_tensor]
+    src = moments_tensor
+    if src.is_cuda and dist.get_backend(group) == "gloo":
+        src = src.cpu()
+    outs = [torch.empty_like(src) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(outs, src, group=group)
+    return outs
+
+
+def sharded_eto(moments_tensor, shard_sizes, d, group=None):
+    """all-gather + Chan merge + ETO: the per-SGA-step exchange of the sharded rollout."""
+    gathered = allgather_moments(moments_tensor, group)
+    R = moments_tensor.numel() // width(d)
+    parts = [(n, g.cpu().numpy().reshape((width(d), R), order="F")) for n, g in zip(shard_sizes, gathered)]
+    n, merged = merge_moments(parts, d)
+    return eto_from_moments(merged, n, d)

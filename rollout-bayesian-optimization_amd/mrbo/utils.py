@@ -72,18 +72,20 @@ def early_stopping_without_a_validation_set(grad_f, var_grad_f, sample_size):
 eswavs = early_stopping_without_a_validation_set
 
 
-def sga_step_batch(x0, active, grad, std_grad, sample_size, eta, lbs, ubs):
+def sga_step_batch(x0, active, grad, std_grad, sample_size, eta, lbs=None, ubs=None, clip=False):
     """One outer step of R restarts at once (columns of x0, d×R), in place: eswavs per restart
-    (utils.jl:114-123) retires the restarts it stops, then StandardSGA (optimizers.jl:6-23)
-    x += η·∇ and the box clip for the rest -- per column the arithmetic of eswavs and
-    StandardSGA.update (NaN ratios keep iterating), without a Python loop over restarts."""
+    (utils.jl:114-123) retires the restarts it stops, then StandardSGA.update! (optimizers.jl:16-22)
+    x += η·∇ for the rest -- per column exactly the arithmetic of eswavs and StandardSGA (NaN ratios
+    keep iterating), without a Python loop over restarts.  The reference does not clip x to the
+    box; clip=True (build-defined, off by default) projects onto [lbs, ubs] after the step."""
     d = x0.shape[0]
     with np.errstate(divide="ignore", invalid="ignore"):
         ratio = np.sum(grad ** 2 / std_grad ** 2, axis=0)
     active &= ~((1.0 - (sample_size / d) * ratio) > 0.0)
     if active.any():
-        x0[:, active] = np.clip(x0[:, active] + eta * grad[:, active], np.asarray(lbs)[:, None],
-                                np.asarray(ubs)[:, None])
+        x0[:, active] = x0[:, active] + eta * grad[:, active]
+        if clip:
+            x0[:, active] = np.clip(x0[:, active], np.asarray(lbs)[:, None], np.asarray(ubs)[:, None])
     return x0, active
 
 

@@ -92,23 +92,52 @@ def test_trajectory_parameters_contract():
                              spatial_lowerbounds=[0, 0], spatial_upperbounds=[1, 1])
 
 
-def test_eto_from_sums_matches_two_pass():
-    from mrbo.parallel import eto_from_sums
+def _moments_data(rng, M, R, d, mean, spread):
+    v = rng.normal(mean, spread, size=(M, R))
+    gx = mean * 1e-3 + rng.normal(size=(d, M, R)) * spread * 1e-3
+    gt = mean + rng.normal(size=(M, R)) * spread
+    return v, gx, gt
+
+
+@pytest.mark.parametrize("mean,spread", [(0.2, 0.1), (1e6, 1.0), (1e8, 1e-3)])
+def test_moments_merge_equals_two_pass(mean, spread):
+    """Chan merge of per-shard (Σ, M2) == the two-pass mean / std(n-1) of rollout.jl:328-337, also
+    where a one-pass Σx² − (Σx)²/n cancels catastrophically (mean/std ≈ 1e6 … 1e11)."""
+    from mrbo.parallel import eto_from_moments, local_moments, merge_moments, shard
     rng = np.random.default_rng(3)
-    M, R, d = 37, 3, 2
-    v = rng.normal(0.2, 0.1, size=(M, R))
-    gx = rng.normal(size=(d, M, R)) * 1e-3
-    gt = rng.normal(size=(M, R))
-    W = 2 + 2 * d + 2
-    sums = np.zeros((W, R))
-    sums[0], sums[1] = v.sum(0), (v ** 2).sum(0)
-    sums[2:2 + d], sums[2 + d:2 + 2 * d] = gx.sum(1), (gx ** 2).sum(1)
-    sums[2 + 2 * d], sums[3 + 2 * d] = gt.sum(0), (gt ** 2).sum(0)
-    e = eto_from_sums(sums, M, d)
-    np.testing.assert_allclose(e[0], v.mean(0), rtol=1e-13)
-    np.testing.assert_allclose(e[1], v.std(0, ddof=1), rtol=1e-10)
-    np.testing.assert_allclose(e[2:2 + d], gx.mean(1), rtol=1e-12)
-    np.testing.assert_allclose(e[2 + d:2 + 2 * d], gx.std(1, ddof=1), rtol=1e-9)
+    M, R, d = 1000, 3, 2
+    v, gx, gt = _moments_data(rng, M, R, d, mean, spread)
+    want_mu, want_sd = v.mean(0), v.std(0, ddof=1)
+    # both sides round x − x̄ at ~eps·|x|: agreement to ~eps·mean/spread is the two-pass bound
+    tol = max(1e-10, 100 * np.finfo(float).eps * mean / spread)
+    if mean / spread >= 1e9:   # the one-pass form this replaced loses all digits here
+        s1, s2 = v.sum(0), (v ** 2).sum(0)
+        one_pass = np.sqrt(np.maximum((s2 - s1 * (s1 / M)) / (M - 1), 0.0))
+        assert np.max(np.abs(one_pass / want_sd - 1)) > 1e-3
+    for world in (1, 2, 3, 8):
+        parts = []
+        for k in range(world):
+            lo, hi = shard(M, world, k)
+            parts.append((hi - lo, local_moments(v[lo:hi], gx[:, lo:hi], gt[lo:hi])))
+        n, merged = merge_moments(parts, d)
+        assert n == M
+        e = eto_from_moments(merged, M, d)
+        np.testing.assert_allclose(e[0], want_mu, rtol=1e-14)
+        np.testing.assert_allclose(e[1], want_sd, rtol=tol)
+        np.testing.assert_allclose(e[2:2 + d], gx.mean(1), rtol=1e-12)
+        np.testing.assert_allclose(e[2 + d:2 + 2 * d], gx.std(1, ddof=1), rtol=tol)
+        np.testing.assert_allclose(e[2 + 2 * d], gt.mean(0), rtol=1e-14)
+        np.testing.assert_allclose(e[3 + 2 * d], gt.std(0, ddof=1), rtol=tol)
+        assert (e[1] > 0).all()
+
+
+def test_moments_single_sample_and_empty_shard():
+    """M = 1: std(n-1) is NaN (Q14); a rank with no samples contributes nothing."""
+    from mrbo.parallel import eto_from_moments, local_moments, merge_moments
+    v, gx, gt = np.array([[2.0]]), np.ones((2, 1, 1)), np.array([[3.0]])
+    n, m = merge_moments([(1, local_moments(v, gx, gt)), (0, np.zeros((8, 1)))], 2)
+    e = eto_from_moments(m, n, 2)
+    assert n == 1 and e[0, 0] == 2.0 and np.isnan(e[1, 0])
 
 
 def test_shard_partition():
@@ -155,13 +184,15 @@ def test_flop_model_batched_starts():
 
 
 def test_sga_step_batch_equals_per_restart_rules():
-    """bench.py's vectorised outer step == eswavs + StandardSGA.update + clip per restart."""
+    """bench.py's vectorised outer step == eswavs + StandardSGA.update! per restart (no clip: the
+    reference's update! has none, optimizers.jl:16-22); clip=True adds the build-defined box clip."""
     from mrbo.optimizers import StandardSGA
     from mrbo.utils import eswavs, sga_step_batch
     rng = np.random.default_rng(0)
     d, R, M = 6, 64, 1024
     lbs, ubs = np.zeros(d), np.ones(d)
-    for _ in range(30):
+    for trial in range(30):
+        clip = trial % 2 == 1
         g = rng.standard_normal((d, R)) * rng.choice([1e-3, 1.0, 1e3])
         sd = np.abs(rng.standard_normal((d, R))) * rng.choice([1e-3, 1.0, 1e3])
         sd[:, rng.integers(0, R, 3)] = 0.0
@@ -175,8 +206,9 @@ def test_sga_step_batch_equals_per_restart_rules():
             if eswavs(g[:, r], sd[:, r] ** 2, M):
                 a1[r] = False
                 continue
-            StandardSGA(0.5).update(x1[:, r], g[:, r])
-            np.clip(x1[:, r], lbs, ubs, out=x1[:, r])
-        x2, a2 = sga_step_batch(x.copy(), act.copy(), g, sd, M, 0.5, lbs, ubs)
+            StandardSGA(0.01).update(x1[:, r], g[:, r])
+            if clip:
+                np.clip(x1[:, r], lbs, ubs, out=x1[:, r])
+        x2, a2 = sga_step_batch(x.copy(), act.copy(), g, sd, M, 0.01, lbs, ubs, clip=clip)
         assert (a1 == a2).all()
         np.testing.assert_array_equal(x1, x2)

@@ -1,11 +1,13 @@
 """CPU tests of the oracle (oracle/rbo_oracle.c): pinned against scipy's Sobol, the golden
 fixtures of the independent NumPy restatement (tests/golden), closed forms, and the
 finite-difference methodology of the reference's own test harness (runtests.jl:11-157)."""
+import os
+
 import numpy as np
 import pytest
 from scipy.stats import qmc
 
-from conftest import GOLDEN_CASES, load_golden
+from conftest import GOLDEN_CASES, ROOT, load_golden
 
 
 @pytest.mark.parametrize("dim", [1, 2, 3, 4, 7, 8, 10, 16])
@@ -274,3 +276,89 @@ def test_tight_gradient_certificate_bounds_the_gradient(oracle, case):
     bound = np.abs(gm) * bmu + np.abs(gs) * bsig
     assert np.all(np.abs(galpha).max(axis=0) <= bound * (1 + 1e-9) + 1e-300)
     assert np.median(bound / np.maximum(np.abs(galpha).max(axis=0), 1e-300)) < 1e6   # not vacuous
+
+
+def _cost_py(kind, c0, w, lbs, ubs, x):
+    """NonUniformCost families of include/mrbo.h in numpy: c, ∇c, Hc (independent restatement)."""
+    del_ = ubs - lbs
+    u = (x - lbs) / del_
+    if kind == "quadratic":
+        return c0 + np.sum(w * u * u), 2 * w * u / del_, np.diag(2 * w / del_ ** 2)
+    c = c0 * np.exp(np.sum(w * u))
+    v = w / del_
+    return c, c * v, c * np.outer(v, v)
+
+
+@pytest.mark.parametrize("kind", ["quadratic", "loglinear"])
+@pytest.mark.parametrize("rule,theta", [("EI", 0.0), ("POI", 0.05), ("LCB", 2.0)])
+def test_cost_weighted_eval_fd(oracle, kind, rule, theta):
+    """NonUniformCost (cost_functions.jl:5-20, build-defined α/c): the oracle's weighted value,
+    gradient, Hessian and θ-mixed partials equal the closed-form transform of its unweighted ones,
+    and the gradient / Hessian / mixed partials match central differences of the weighted values
+    (Hessian with the Q11 μσ cross term restored, as test_rule_partials_fd)."""
+    g = load_golden("c2near")
+    s = _osur(oracle, g)
+    d = g["X"].shape[0]
+    lbs, ubs = g["lbs"], g["ubs"]
+    w = np.linspace(0.5, 1.5, d)
+    cost = (kind, 1.3, w)
+    x = g["x0s"][:, 0] + 0.3
+    colw = lambda xx, th=theta: oracle.eval_base(s, xx.reshape(-1, 1), theta=th, rule=rule, cost=cost, lbs=lbs,
+                                                 ubs=ubs)[:, 0]
+    o = oracle.eval_base(s, x.reshape(-1, 1), theta=theta, rule=rule)[:, 0]
+    ow = colw(x)
+    c, gc, Hc = _cost_py(kind, 1.3, w, lbs, ubs, x)
+    alpha, galpha = o[2], o[3 + 2 * d:3 + 3 * d]
+    H = o[3 + 3 * d:3 + 3 * d + d * d].reshape(d, d, order="F")
+    mixed = o[3 + 3 * d + d * d:]
+    G = galpha / c - alpha * gc / c ** 2
+    gth = o[1] if rule == "LCB" else None
+    np.testing.assert_allclose(ow[:2], o[:2], rtol=0, atol=0)          # μ, σ untouched
+    np.testing.assert_allclose(ow[2], alpha / c, rtol=1e-14)
+    np.testing.assert_allclose(ow[3:3 + 2 * d], o[3:3 + 2 * d], rtol=0, atol=0)
+    np.testing.assert_allclose(ow[3 + 2 * d:3 + 3 * d], G, rtol=1e-12, atol=1e-15)
+    Hw = ow[3 + 3 * d:3 + 3 * d + d * d].reshape(d, d, order="F")
+    np.testing.assert_allclose(Hw, (H - np.outer(G, gc) - np.outer(gc, G)) / c - alpha / c ** 2 * Hc, rtol=1e-11,
+                               atol=1e-14)
+    # FD of the weighted value / gradient / θ-derivative
+    np.testing.assert_allclose(G, _fd(lambda xx: colw(xx)[2], x), rtol=1e-6, atol=1e-10)
+    mu, sig = o[0], o[1]
+    gmu, gsig = o[3:3 + d], o[3 + d:3 + 2 * d]
+    z = (np.min(g["y"]) - mu - theta) / sig
+    phi = np.exp(-z * z / 2) / np.sqrt(2 * np.pi)
+    gmusig = {"EI": z * phi / sig, "POI": phi * (1 - z * z) / sig ** 2, "LCB": 0.0}[rule]
+    cross = gmusig * (np.outer(gmu, gsig) + np.outer(gsig, gmu)) / c
+    Hfd = np.column_stack([_fd(lambda xx: colw(xx)[3 + 2 * d + a], x) for a in range(d)])
+    np.testing.assert_allclose(Hw + cross, Hfd, rtol=1e-5, atol=1e-8)
+    th_fd = np.array([(colw(x, theta + 1e-6)[3 + 2 * d + a] - colw(x, theta - 1e-6)[3 + 2 * d + a]) / 2e-6
+                      for a in range(d)])
+    np.testing.assert_allclose(ow[3 + 3 * d + d * d:], th_fd, rtol=1e-5, atol=1e-9)
+    _ = (mixed, gth)
+
+
+def test_cost_weighted_rollout_replay_consistent(oracle):
+    """A cost-weighted rollout: the oracle's own policy points replay exactly, the work differs
+    from the unweighted rule's (the cost moves the inner-solve optimum), and the resolution
+    values stay max(fmini − min obs, 0)."""
+    g = load_golden("c2near")
+    s = _osur(oracle, g)
+    h = int(g["h"])
+    cost = ("quadratic", 1.0, np.ones(g["X"].shape[0]))
+    a = oracle.simulate_mc(s, g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], h, cost=cost)
+    assert (a["status"] == 0).all()
+    rp = np.asfortranarray(a["policy_x"][:, 1:])
+    b = oracle.simulate_mc(s, g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], h, replay_x=rp, cost=cost)
+    np.testing.assert_array_equal(a["values"], b["values"])
+    np.testing.assert_array_equal(a["grad_x"], b["grad_x"])
+    u = oracle.simulate_mc(s, g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], h)
+    assert not np.allclose(a["policy_x"][:, 1:], u["policy_x"][:, 1:])
+    np.testing.assert_array_equal(a["values"], np.maximum(float(g["fmini"]) - a["obs"].min(axis=0), 0.0))
+
+
+def test_oracle_sanitizer_check():
+    """the oracle under ASan + UBSan (oracle/check_main.c drives every entry point)."""
+    import subprocess
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "check"], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "clean" in r.stdout
