@@ -51,6 +51,9 @@ struct MrboParamsC
     seed::UInt64
     sample_offset::Int32
     samples_total::Int32
+    cost::Int32          # mrbo_cost_t: NonUniformCost weighting of the inner-solve rule (0 = none)
+    cost_c0::Float64
+    cost_w::Ptr{Float64}
 end
 
 struct MrboBackend
@@ -93,7 +96,7 @@ function MrboPlan(s::Surrogate, tp::TrajectoryParameters, θ::Vector{Float64}, n
         sd = MrboSurrogateC(size(X, 1), N, kernel_id(get_kernel(s)), get_kernel(s).θ[1], s.σn2, fmini,
                             pointer(X), pointer(L), N, pointer(c), pointer(y), kernel_period(get_kernel(s)))
         pd = MrboParamsC(tp.horizon, M, 1, nstarts, rule_id(get_decision_rule(s)), θ[1], pointer(lbs), pointer(ubs),
-                         max_iters, max_ls, 1e-3, 1e-3, 1e-8, 1e-4, 1e-8, seed, 0, 0)
+                         max_iters, max_ls, 1e-3, 1e-3, 1e-8, 1e-4, 1e-8, seed, 0, 0, 0, 1.0, C_NULL)
         h = Ref{Ptr{Cvoid}}(C_NULL)
         check(ccall((:mrbo_plan_create, libmrbo), Cint,
                     (Ref{MrboSurrogateC}, Ref{MrboParamsC}, Cint, Ref{Ptr{Cvoid}}), sd, pd, device, h))
