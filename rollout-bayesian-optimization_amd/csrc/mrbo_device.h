@@ -20,7 +20,10 @@ namespace mrbo {
 // evals[NCOUNT·t + k], k = gradient evals, value evals, Hessians, adjoint rich evals, pairs
 constexpr int NCOUNT = 5;
 constexpr int NSTAMP = 17;  // MRBO_STAMPS regions (names in mrbo_api.hip)
-constexpr int FMAX = 6;    // fantasy points per trajectory = h+1  (h ≤ 5)
+#ifndef MRBO_FMAX
+#define MRBO_FMAX 6
+#endif
+constexpr int FMAX = MRBO_FMAX;   // fantasy points per trajectory = h+1  (h ≤ 5)
 constexpr int WAVE = 64;
 constexpr int MAXD = 16;   // widest input dimension of a cost model (mrbo_plan_create check)
 enum { COST_NONE = 0, COST_QUADRATIC = 1, COST_LOGLINEAR = 2 };   // mrbo_cost_t
