@@ -146,8 +146,10 @@ __device__ __forceinline__ double dpp_partner(double v) {
   static_assert(M == 8 || M == 4 || M == 2 || M == 1, "dpp_partner: M in {8,4,2,1}");
   int lo, hi;
   dsplit(v, lo, hi);
-  lo = __builtin_amdgcn_update_dpp(0, lo, ctrl, 0xF, 0xF, false);
-  hi = __builtin_amdgcn_update_dpp(0, hi, ctrl, 0xF, 0xF, false);
+  // every lane has an in-row source for these controls: mov_dpp needs no 'old' operand (an
+  // update_dpp with old = 0 materialised two zero moves per double)
+  lo = __builtin_amdgcn_mov_dpp(lo, ctrl, 0xF, 0xF, true);
+  hi = __builtin_amdgcn_mov_dpp(hi, ctrl, 0xF, 0xF, true);
   return djoin(lo, hi);
 }
 
@@ -348,6 +350,72 @@ __device__ __forceinline__ void rad_eval2(const Radial& k, double rho2a, double 
   g2b = c23 * (c * c) * e.b;
 }
 
+// φ(z) and Φ(z) of the EI / POI rules from ONE exponential.  With u = |z|/√2 and
+// E = exp(−z²/2) = exp(−u²):  φ = E/√(2π),  the tail Q = P(Z > |z|) = ½·E·erfcx(u), and
+// Φ = Q (z ≤ 0) or 1 − Q (z > 0).  erfcx(u) = P(t)/(1 + 2u) with t = (u − K)/(u + K), K = 3.5,
+// P a degree-23 polynomial from the Chebyshev series of (1 + 2u)·erfcx(u) on u ∈ [0, ∞)
+// (tools/fit_erfcx.py, mpmath at 60 digits): max relative error 4.2e-16 over [0, 27] in fp64.
+// Replaces two leaf calls (exp, erfc -- the latter with exponentials of its own) evaluated in
+// sequence by two independent inline chains (the exponential and the polynomial).  Sharing E
+// also makes φ + zΦ (the EI tail, where both nearly cancel) carry E's rounding as one factor.
+// Not bit-identical to libm erfc; GPU-vs-oracle parity is a tolerance.
+struct PhiPair {
+  double phi, Phi;
+};
+__device__ __forceinline__ PhiPair ei_phi_Phi(double z) {
+  const double u = fmin(fabs(z) * 0.7071067811865476, 40.0);   // E = 0 beyond; keeps t finite
+  const double E = fexp(-0.5 * (z * z));
+  // one reciprocal for both quotients: r = 1/((u + K)(1 + 2u)), t = (u − K)(1 + 2u)·r
+  const double a = u + 3.5, b = fma(2.0, u, 1.0), ab = a * b;
+  double r = __builtin_amdgcn_rcp(ab);
+  r = fma(r, fma(-ab, r, 1.0), r);
+  r = fma(r, fma(-ab, r, 1.0), r);
+  const double t = (u - 3.5) * b * r, t2 = t * t;
+  // even / odd halves of P(t) = Pe(t²) + t·Po(t²): two independent Horner chains
+  double pe = sconst<0xf1ab7ccbu, 0x3dd09a8bu>();
+  asm volatile("" : "+v"(pe));
+  pe = fma(t2, pe, sconst<0x73fda30du, 0x3e06db11u>());
+  pe = fma(t2, pe, sconst<0xf4266242u, 0xbe427e42u>());
+  pe = fma(t2, pe, sconst<0x1ed381c5u, 0xbe672292u>());
+  pe = fma(t2, pe, sconst<0xb901a919u, 0x3ec385e7u>());
+  pe = fma(t2, pe, sconst<0x645605dcu, 0xbf066e11u>());
+  pe = fma(t2, pe, sconst<0xfbfa9e67u, 0x3f427e65u>());
+  pe = fma(t2, pe, sconst<0xc891e642u, 0xbf7143c4u>());
+  pe = fma(t2, pe, sconst<0xf77381b3u, 0xbfa8ff5eu>());
+  pe = fma(t2, pe, sconst<0x0c35056au, 0xbfbd7683u>());
+  pe = fma(t2, pe, sconst<0x284b1971u, 0xbf859e2cu>());
+  pe = fma(t2, pe, sconst<0x9a0ee914u, 0x3ff3e0a9u>());
+  double po = sconst<0x617fb329u, 0xbe1406aau>();
+  asm volatile("" : "+v"(po));
+  po = fma(t2, po, sconst<0xdb5ecc9au, 0x3e4d421du>());
+  po = fma(t2, po, sconst<0x3786431fu, 0xbe79e096u>());
+  po = fma(t2, po, sconst<0xc09ddffau, 0x3ea42eb1u>());
+  po = fma(t2, po, sconst<0x97b263b0u, 0xbecffe87u>());
+  po = fma(t2, po, sconst<0x306b92a0u, 0x3ef97053u>());
+  po = fma(t2, po, sconst<0x5777da87u, 0xbf1fda8au>());
+  po = fma(t2, po, sconst<0xf98105c2u, 0xbf33cf36u>());
+  po = fma(t2, po, sconst<0x67477473u, 0x3f938ec6u>());
+  po = fma(t2, po, sconst<0x6045eed1u, 0x3fb68610u>());
+  po = fma(t2, po, sconst<0xec6b3bb9u, 0x3fb8f702u>());
+  po = fma(t2, po, sconst<0x20ea5946u, 0xbfc1ebd2u>());
+  const double P = fma(t, po, pe);
+  const double q = 0.5 * E * (P * (a * r));   // ½·E·erfcx(u)
+  PhiPair o;
+  o.phi = E * 0.3989422804014327;
+  o.Phi = (z > 0.0) ? 1.0 - q : q;
+  return o;
+}
+#ifdef MRBO_LIBM_EI   // A/B: the libm pair (two leaf calls)
+__device__ __forceinline__ PhiPair ei_pp(double z) {
+  PhiPair o;
+  o.phi = xexp(-0.5 * (z * z)) * 0.3989422804014327;
+  o.Phi = 0.5 * xerfc(-z * 0.7071067811865476);
+  return o;
+}
+#else
+__device__ __forceinline__ PhiPair ei_pp(double z) { return ei_phi_Phi(z); }
+#endif
+
 // The base decision rule g(μ, σ, θ) and the partials DecisionRule takes by ForwardDiff
 // (decision_rules.jl:23-34), in closed form.
 //   EI  (:84-99)   g = IΦ(z) + σφ(z), I = fmin − μ − θ, z = I/σ; zero when σ < σtol
@@ -377,8 +445,8 @@ __device__ __forceinline__ EIp rule_partials(int rule, double mu, double sig, do
   const double imp = fmin - mu - theta;
   const double isig = 1.0 / sig;
   const double z = imp * isig;
-  const double phi = xexp(-0.5 * (z * z)) * 0.3989422804014327;
-  const double Phi = 0.5 * xerfc(-z * 0.7071067811865476);
+  const PhiPair pp = ei_pp(z);
+  const double phi = pp.phi, Phi = pp.Phi;
   const double pis = phi * isig;
   if (rule == RULE_POI) {
     const double pis2 = pis * isig;
