@@ -187,14 +187,22 @@ int mrbo_partial_moments(mrbo_plan_t* plan, const double* values, const double* 
  * [μ, σ, α, ∇μ(d), ∇σ(d), ∇α(d), Hα(d×d col-major), d2α/dxdθ(d)].                       */
 int mrbo_eval_base(mrbo_plan_t* plan, int32_t P, const double* xs, double* out, uint32_t flags, void* stream);
 
-/* Base-GP fit at P lengthscales ells[p] (kernel, σn2, X d×N, y N from s; s->L, s->c unused):
- * K = Ψ(‖Xi−Xj‖)+σn2·I, L = chol(K), c = L'\(L\y), and
- *   ll[p]  = log_likelihood = −yᵀc/2 − Σ log L_ii − N·log(2π)/2
- *   dll[p] = ∂ll/∂ℓ = (cᵀ δK c − tr(L'\(L\δK)))/2,  δK = eval_Dθ_KXX(ψ, X, [1])
- * status[p] = 0, or 1 when cholesky throws PosDefException (ll, dll = NaN).  L_out (N×N×P,
- * lower, zeros above) and c_out (N×P) are optional (NULL).  ells / ll / dll / status / L_out /
- * c_out are device pointers unless MRBO_FLAG_HOST_POINTERS; N ≤ 256.  Allocates its
- * workspace (3·N²·P doubles) on the stream.                                                */
+/* Base-GP fit at P hyperparameter vectors θ_p = thetas[p·nt .. p·nt+nt−1] (kernel, σn2, X d×N,
+ * y N from s; s->L, s->c unused) -- the evaluations behind optimize!'s fg! (r_b_s.jl:810-814):
+ * K = Ψ(‖Xi−Xj‖; θ_p)+σn2·I, L = chol(K), c = L'\(L\y), and
+ *   ll[p]         = log_likelihood  (r_b_s.jl:770-776) = −yᵀc/2 − Σ log L_ii − N·log(2π)/2
+ *   grad[p·nt+t]  = ∇log_likelihood (r_b_s.jl:787-799) = (cᵀ δK_t c − tr(L'\(L\δK_t)))/2,
+ *                   δK_t = eval_Dθ_KXX(ψ, X, e_t) (radial_basis_functions.jl:264-284)
+ * θ = (ℓ) for Matérn-5/2, -3/2, -1/2 and SE (nt = 1); Periodic (radial_basis_functions.jl:98-103)
+ * takes θ = (ℓ, p) (nt = 2) or (ℓ) with p = s->period (nt = 1: ∂/∂ℓ only).
+ * status[p] = 0, or 1 when cholesky throws PosDefException (ll, grad = NaN).  L_out (N×N×P,
+ * lower, zeros above) and c_out (N×P) are optional (NULL).  thetas / ll / grad / status / L_out
+ * / c_out are device pointers unless MRBO_FLAG_HOST_POINTERS; N ≤ 256.  N ≤ 64 without L_out /
+ * c_out runs one wave per candidate with no workspace; otherwise 3·N²·P doubles of workspace are
+ * allocated for the call.  Synchronises the stream before returning.                        */
+int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t P, int32_t nt, const double* thetas, double* ll,
+                      double* grad, int32_t* status, double* L_out, double* c_out, uint32_t flags, void* stream);
+/* mrbo_gp_fit_theta with nt = 1: ells[p] = ℓ_p, dll[p] = ∂ll/∂ℓ (Periodic: p = s->period). */
 int mrbo_gp_fit(const mrbo_surrogate_t* s, int32_t P, const double* ells, double* ll, double* dll, int32_t* status,
                 double* L_out, double* c_out, uint32_t flags, void* stream);
 

@@ -77,6 +77,8 @@ def lib():
                                       _dp, _dp, _dp, _ip, _dp, _dp, _dp, _lp]
         L.rbo_log_likelihood.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_double,
                                          ctypes.c_double, _dp, _dp, _dp, _dp, _dp, _dp]
+        L.rbo_log_likelihood_theta.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _dp,
+                                               ctypes.c_double, ctypes.c_double, _dp, _dp, _dp, _dp, _dp, _dp]
         L.rbo_simulate_ghq.argtypes = [ctypes.POINTER(Surrogate), ctypes.POINTER(Params), _dp, _dp, _dp, _dp, _dp,
                                        _dp, _dp, _dp, _dp, _ip, _dp, _dp, _dp, _lp]
         _lib = L
@@ -152,6 +154,23 @@ def log_likelihood(X, y, kernel="matern52", ell=1.0, sigma_n2=1e-6, want_fit=Fal
     if rc < 0:
         raise ValueError(f"log_likelihood: kernel {kernel} not supported")
     return (ll.value, dll.value, L, c) if want_fit else (ll.value, dll.value)
+
+
+def log_likelihood_theta(X, y, kernel, theta, sigma_n2=1e-6, period=1.0, want_fit=False):
+    """(ll, grad[, L, c]): ∇log_likelihood over θ = (ℓ) or, for the Periodic kernel, (ℓ, p)
+    (a one-element θ keeps `period`).  NaNs on PosDefException."""
+    X, y = _f64(X), _f64(y).ravel()
+    th = _f64(theta).ravel()
+    d, N = X.shape
+    ll = ctypes.c_double()
+    grad = np.zeros(th.size)
+    L = np.zeros((N, N), order="F")
+    c = np.zeros(N)
+    rc = lib().rbo_log_likelihood_theta(d, N, KERNELS[kernel], th.size, _p(th), float(period), float(sigma_n2), _p(X),
+                                        _p(y), ctypes.byref(ll), _p(grad), _p(L), _p(c))
+    if rc < 0:
+        raise ValueError(f"log_likelihood_theta: kernel {kernel} with {th.size} hyperparameters")
+    return (ll.value, grad, L, c) if want_fit else (ll.value, grad)
 
 
 def eval_base(osur, xs, theta=0.0, sigma_tol=1e-8, rule="EI", cost=None, lbs=None, ubs=None):

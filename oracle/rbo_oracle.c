@@ -1204,7 +1204,7 @@ int rbo_simulate_ghq(const rbo_surrogate* s, const rbo_params* p, const double* 
  *   Surrogate ctor           radial_basis_surrogates.jl:77-118 (K, L = cholesky(K), c = L'\(L\y))
  *   log_likelihood           :770-776   −y'c/2 − Σ log diag(L) − n log(2π)/2
  *   δlog_likelihood          :778-785   (c'δK c − tr(L'\(L\δK)))/2
- *   ∇log_likelihood          :787-799   δθ = e_1 (one lengthscale)
+ *   ∇log_likelihood          :787-799   δθ = e_t for every hyperparameter (ℓ; Periodic ℓ, p)
  *   eval_Dθ_KXX              radial_basis_functions.jl:264-284 (δK_jj = ∇θψ(0)'δθ = 0)
  * ∇θ_ψ (ForwardDiff there, :43) in closed form.
  * ---------------------------------------------------------------------------------- */
@@ -1213,14 +1213,24 @@ static double k_dpsi_dell(const kern_t* k, double rho) {
     case RBO_K_MATERN52: { const double s = sqrt(5.0) / k->ell * rho; return (s * s / 3.0) * (1 + s) * exp(-s) / k->ell; }
     case RBO_K_MATERN32: { const double s = sqrt(3.0) / k->ell * rho; return s * s * exp(-s) / k->ell; }
     case RBO_K_MATERN12: { const double s = rho / k->ell; return s * exp(-s) / k->ell; }
+    case RBO_K_PERIODIC: {   /* ∂/∂ℓ exp(−2 sin²(πρ/p)/ℓ²) = ψ · 4 sin²(πρ/p)/ℓ³ */
+      const double sn = sin(JL_PI * rho / k->per);
+      return k_psi(k, rho) * 4 * sn * sn / (k->ell * k->ell * k->ell);
+    }
     default: { const double t = rho * rho / (k->ell * k->ell); return exp(-t / 2) * t / k->ell; }
   }
 }
+/* Periodic: ∂/∂p exp(−2 sin²(πρ/p)/ℓ²) = ψ · (4 sin(u) cos(u)/ℓ²) · πρ/p², u = πρ/p */
+static double k_dpsi_dper(const kern_t* k, double rho) {
+  const double u = JL_PI * rho / k->per;
+  return k_psi(k, rho) * 4 * sin(u) * cos(u) / (k->ell * k->ell) * (JL_PI * rho / (k->per * k->per));
+}
 
-int rbo_log_likelihood(int32_t d, int32_t N, int32_t kernel, double ell, double sigma_n2, const double* X,
-                       const double* y, double* ll, double* dll, double* L_out, double* c_out) {
-  const kern_t k = {kernel, ell, 1.0};
-  if (kernel == RBO_K_PERIODIC) return -1;   /* two hyperparameters: ∂/∂ℓ alone is not ∇log_likelihood */
+int rbo_log_likelihood_theta(int32_t d, int32_t N, int32_t kernel, int32_t nt, const double* theta, double period,
+                             double sigma_n2, const double* X, const double* y, double* ll, double* grad,
+                             double* L_out, double* c_out) {
+  if (nt < 1 || nt > (kernel == RBO_K_PERIODIC ? 2 : 1)) return -1;
+  const kern_t k = {kernel, theta[0], (kernel == RBO_K_PERIODIC) ? (nt == 2 ? theta[1] : period) : 1.0};
   const int64_t NN = (int64_t)N * N;
   double* K = (double*)calloc((size_t)NN, sizeof(double));
   double* dK = (double*)calloc((size_t)NN, sizeof(double));
@@ -1234,30 +1244,46 @@ int rbo_log_likelihood(int32_t d, int32_t N, int32_t kernel, double ell, double 
       for (int a = 0; a < d; ++a) r[a] = X[a + (int64_t)d * i] - X[a + (int64_t)d * j];
       const double rho = vnorm(r, d);
       K[i + (int64_t)N * j] = (i == j) ? k_psi(&k, 0.0) + sigma_n2 : k_psi(&k, rho);
-      dK[i + (int64_t)N * j] = (i == j) ? 0.0 : k_dpsi_dell(&k, rho);
     }
   int rc = chol_small(K, N, L);
   if (rc == 0) {
     kinv(L, N, N, y, c, tmp);
-    double yc = 0, ld = 0, cgc = 0, tr = 0;
+    double yc = 0, ld = 0;
     for (int i = 0; i < N; ++i) { yc += y[i] * c[i]; ld += log(L[i + (int64_t)N * i]); }
-    for (int j = 0; j < N; ++j) {
-      double sj = 0;
-      for (int i = 0; i < N; ++i) sj += dK[i + (int64_t)N * j] * c[i];
-      cgc += c[j] * sj;
-      kinv(L, N, N, dK + (int64_t)N * j, col, tmp);   /* column j of L'\(L\δK) */
-      tr += col[j];
-    }
     *ll = -yc / 2 - ld - N * log(2 * JL_PI) / 2;
-    *dll = (cgc - tr) / 2;
+    /* ∇log_likelihood (:787-799): δlog_likelihood (:778-785) at δθ = e_t, δK = eval_Dθ_KXX */
+    for (int t = 0; t < nt; ++t) {
+      for (int j = 0; j < N; ++j)
+        for (int i = 0; i < N; ++i) {
+          for (int a = 0; a < d; ++a) r[a] = X[a + (int64_t)d * i] - X[a + (int64_t)d * j];
+          const double rho = vnorm(r, d);
+          dK[i + (int64_t)N * j] = (i == j) ? 0.0 : (t == 0 ? k_dpsi_dell(&k, rho) : k_dpsi_dper(&k, rho));
+        }
+      double cgc = 0, tr = 0;
+      for (int j = 0; j < N; ++j) {
+        double sj = 0;
+        for (int i = 0; i < N; ++i) sj += dK[i + (int64_t)N * j] * c[i];
+        cgc += c[j] * sj;
+        kinv(L, N, N, dK + (int64_t)N * j, col, tmp);   /* column j of L'\(L\δK) */
+        tr += col[j];
+      }
+      grad[t] = (cgc - tr) / 2;
+    }
     if (L_out) memcpy(L_out, L, sizeof(double) * NN);
     if (c_out) memcpy(c_out, c, sizeof(double) * N);
   } else {
     *ll = NAN;
-    *dll = NAN;
+    for (int t = 0; t < nt; ++t) grad[t] = NAN;
   }
   free(K); free(dK); free(L); free(c); free(col); free(tmp);
   return rc == 0 ? 0 : 1;
+}
+
+/* one lengthscale (Periodic: ∂/∂ℓ at period 1 is not ∇log_likelihood -- use the θ form) */
+int rbo_log_likelihood(int32_t d, int32_t N, int32_t kernel, double ell, double sigma_n2, const double* X,
+                       const double* y, double* ll, double* dll, double* L_out, double* c_out) {
+  if (kernel == RBO_K_PERIODIC) return -1;
+  return rbo_log_likelihood_theta(d, N, kernel, 1, &ell, 1.0, sigma_n2, X, y, ll, dll, L_out, c_out);
 }
 
 static int eval_base_impl(const rbo_surrogate* s, int32_t rule, double theta, double sigma_tol, int32_t P,

@@ -134,6 +134,11 @@ int rbo_simulate_ghq(const rbo_surrogate* s, const rbo_params* p, const double* 
 /* Base-GP refit at lengthscale ell (Surrogate ctor, radial_basis_surrogates.jl:77-118) and its
  * log_likelihood (:770-776) and ∂/∂ℓ (∇log_likelihood :787-799 via δlog_likelihood :778-785).
  * Returns 1 (ll = dll = NaN) on PosDefException.  L_out (N×N, lower) and c_out optional. */
+/* ∇log_likelihood over θ = (ℓ) or, for Periodic, (ℓ, p) (nt = 2; nt = 1 keeps `period`):
+ * grad[t] = (cᵀδK_t c − tr(L'\(L\δK_t)))/2.  Returns 0, 1 (PosDefException), −1 (bad nt). */
+int rbo_log_likelihood_theta(int32_t d, int32_t N, int32_t kernel, int32_t nt, const double* theta, double period,
+                             double sigma_n2, const double* X, const double* y, double* ll, double* grad,
+                             double* L_out, double* c_out);
 int rbo_log_likelihood(int32_t d, int32_t N, int32_t kernel, double ell, double sigma_n2, const double* X,
                        const double* y, double* ll, double* dll, double* L_out, double* c_out);
 

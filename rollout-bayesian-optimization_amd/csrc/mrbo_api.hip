@@ -658,33 +658,34 @@ int mrbo_eval_base(mrbo_plan_t* P, int32_t npts, const double* xs, double* out, 
   return MRBO_OK;
 }
 
-int mrbo_gp_fit(const mrbo_surrogate_t* s, int32_t np, const double* ells, double* ll, double* dll, int32_t* status,
-                double* L_out, double* c_out, uint32_t flags, void* stream) {
-  if (!s || !ells || !ll || !dll || !status || np < 1) return fail(MRBO_ERR_ARG, "null argument");
+int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const double* thetas, double* ll,
+                      double* grad, int32_t* status, double* L_out, double* c_out, uint32_t flags, void* stream) {
+  if (!s || !thetas || !ll || !grad || !status || np < 1) return fail(MRBO_ERR_ARG, "null argument");
   const int d = s->d, N = s->N;
   if (d < 1 || N < 1 || !s->X || !s->y) return fail(MRBO_ERR_ARG, "bad surrogate (d=%d N=%d)", d, N);
   if (N > 256) return fail(MRBO_ERR_UNSUPPORTED, "N=%d > 256", N);
-  // the Periodic kernel has two hyperparameters: ∂/∂ℓ alone is not its ∇log_likelihood
-  if (s->kernel < 0 || s->kernel > 3) return fail(MRBO_ERR_UNSUPPORTED, "gp_fit: kernel id %d", s->kernel);
+  if (s->kernel < 0 || s->kernel > 4) return fail(MRBO_ERR_UNSUPPORTED, "gp_fit: kernel id %d", s->kernel);
+  // θ = (ℓ) for the one-parameter kernels; Periodic takes (ℓ) (period fixed at s->period) or (ℓ, p)
+  if (nt < 1 || nt > (s->kernel == 4 ? 2 : 1)) return fail(MRBO_ERR_ARG, "gp_fit: nt=%d for kernel %d", nt, s->kernel);
+  if (s->kernel == 4 && nt == 1 && !(s->period > 0.0)) return fail(MRBO_ERR_ARG, "gp_fit: period %g", s->period);
   hipStream_t st = (hipStream_t)stream;
-  const size_t P = (size_t)np, NN = (size_t)N * N;
+  const size_t P = (size_t)np, NN = (size_t)N * N, NTP = (size_t)nt * P;
   Stage sg;
-  const double* dells = ells;
-  double *dll_ = ll, *ddll = dll, *dL = L_out, *dc = c_out;
+  const double* dth = thetas;
+  double *dll_ = ll, *dgr = grad, *dL = L_out, *dc = c_out;
   int32_t* dst = status;
   if (flags & MRBO_FLAG_HOST_POINTERS) {
-    if (sg.in(ells, P, &dells) || sg.out(P, ll, &dll_) || sg.out(P, dll, &ddll) || sg.out(P, status, &dst) ||
+    if (sg.in(thetas, NTP, &dth) || sg.out(P, ll, &dll_) || sg.out(NTP, grad, &dgr) || sg.out(P, status, &dst) ||
         sg.out(NN * P, L_out, &dL) || sg.out((size_t)N * P, c_out, &dc))
       return fail(MRBO_ERR_NOMEM, "staging allocation failed");
   }
   const double *dX = nullptr, *dy = nullptr;
   if (sg.in(s->X, (size_t)d * N, &dX) || sg.in(s->y, (size_t)N, &dy)) return fail(MRBO_ERR_NOMEM, "staging X, y");
-  double* work = nullptr;   // N ≤ 64 runs in LDS (gpfit_wave_kernel): no workspace
-  if (!gpfit_in_lds(N, d)) {
-    if (hipMalloc(&work, sizeof(double) * 3 * NN * P) != hipSuccess) return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
-    sg.bufs.push_back(work);
+  GpFitParams q{d, N, s->kernel, s->sigma_n2, dX, dy, nt, dth, s->period, dll_, dgr, (int*)dst, dL, dc, nullptr};
+  if (!gpfit_in_regs(q)) {   // the register kernel (N ≤ 64, no factor outputs) needs no workspace
+    if (hipMalloc(&q.work, sizeof(double) * 3 * NN * P) != hipSuccess) return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
+    sg.bufs.push_back(q.work);
   }
-  GpFitParams q{d, N, s->kernel, s->sigma_n2, dX, dy, dells, dll_, ddll, (int*)dst, dL, dc, work};
   static hipEvent_t gev[2] = {nullptr, nullptr};
   if (!gev[0]) {
     HIP_TRY(hipEventCreate(&gev[0]));
@@ -702,12 +703,17 @@ int mrbo_gp_fit(const mrbo_surrogate_t* s, int32_t np, const double* ells, doubl
   }
   if (flags & MRBO_FLAG_HOST_POINTERS) {
     HIP_TRY(hipMemcpy(ll, dll_, sizeof(double) * P, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(dll, ddll, sizeof(double) * P, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(grad, dgr, sizeof(double) * NTP, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(status, dst, sizeof(int32_t) * P, hipMemcpyDeviceToHost));
     if (L_out) HIP_TRY(hipMemcpy(L_out, dL, sizeof(double) * NN * P, hipMemcpyDeviceToHost));
     if (c_out) HIP_TRY(hipMemcpy(c_out, dc, sizeof(double) * N * P, hipMemcpyDeviceToHost));
   }
   return MRBO_OK;
+}
+
+int mrbo_gp_fit(const mrbo_surrogate_t* s, int32_t np, const double* ells, double* ll, double* dll, int32_t* status,
+                double* L_out, double* c_out, uint32_t flags, void* stream) {
+  return mrbo_gp_fit_theta(s, np, 1, ells, ll, dll, status, L_out, c_out, flags, stream);
 }
 
 double mrbo_last_gp_fit_ms(void) { return g_gpfit_ms; }

@@ -138,6 +138,22 @@ __device__ __forceinline__ double swap_fold(double a, double b) {
   }
 }
 
+// Register broadcast (rollout products, GP-fit Cholesky): blocks p and p+2 of v (lane j holds
+// row j), each replicated into all four 16-lane rows, so that DPP row_newbcast:n then reads
+// row 16b + n in every lane.
+template <int P>
+__device__ __forceinline__ void row_blocks(double v, double& blk_p, double& blk_p2) {
+  int lo, hi;
+  dsplit(v, lo, hi);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // [r0 r0 r2 r2], [r1 r1 r3 r3]
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const int tlo = P ? a[1] : a[0], thi = P ? b[1] : b[0];
+  const auto c = __builtin_amdgcn_permlane32_swap(tlo, tlo, false, false); // [rP ×4], [rP+2 ×4]
+  const auto d = __builtin_amdgcn_permlane32_swap(thi, thi, false, false);
+  blk_p = djoin(c[0], d[0]);
+  blk_p2 = djoin(c[1], d[1]);
+}
+
 // M = 8, 4, 2, 1: v from a partner lane that differs in bit M and agrees on all higher bits
 // (DPP row_mirror, row_half_mirror, quad_perm xor2 / xor1 -- one VALU move per dword).
 template <int M>

@@ -35,18 +35,23 @@ MRBO_DECLARE_D(5) MRBO_DECLARE_D(6) MRBO_DECLARE_D(7) MRBO_DECLARE_D(8)
 struct GpFitParams {
   int d, N, kernel;
   double sn2;
-  const double* X;     // d×N
-  const double* y;     // N
-  const double* ells;  // P
-  double* ll;          // P
-  double* dll;         // P
-  int* status;         // P: 0, or 1 = PosDefException
-  double* L_out;       // optional N×N×P
-  double* c_out;       // optional N×P
-  double* work;        // 3·N²·P
+  const double* X;       // d×N
+  const double* y;       // N
+  int nt;                // hyperparameters per candidate: 1 (ℓ) or 2 (ℓ, p: Periodic)
+  const double* thetas;  // nt×P
+  double period;         // Periodic with nt = 1: the surrogate's period
+  double* ll;            // P
+  double* grad;          // nt×P: ∂ll/∂θ_t
+  int* status;           // P: 0, or 1 = PosDefException
+  double* L_out;         // optional N×N×P
+  double* c_out;         // optional N×P
+  double* work;          // 3·N²·P (gpfit_kernel only)
 };
 void launch_gpfit(int P, hipStream_t st, const GpFitParams& q);
-// N ≤ 64 (and d ≤ 8): the one-wave-per-candidate kernel with the matrices in LDS (no workspace)
-inline bool gpfit_in_lds(int N, int d) { return N <= 64 && d <= 8; }
+// N ≤ 64, d ≤ 16 and no factor / coefficient outputs: the one-wave-per-candidate register kernel
+// (no workspace)
+inline bool gpfit_in_regs(const GpFitParams& q) {
+  return q.N <= 64 && q.d <= 16 && !q.L_out && !q.c_out;
+}
 
 }  // namespace mrbo

@@ -1,47 +1,65 @@
-// mrbo_gpfit.hip -- base-GP fit and its marginal likelihood for a batch of lengthscales.
+// mrbo_gpfit.hip -- base-GP fit and its marginal likelihood for a batch of hyperparameters.
 //
-// Restates, one workgroup per candidate lengthscale ℓ_p:
+// Restates, one candidate θ_p per wave / workgroup:
 //   Surrogate(ψ, X, y)       radial_basis_surrogates.jl:77-118   K = Ψ(‖Xi−Xj‖) + σn2·I, L = chol(K),
 //                                                               c = L'\(L\y)
 //   log_likelihood(s)        radial_basis_surrogates.jl:770-776  −yᵀc/2 − Σ log L_ii − n·log(2π)/2
 //   δlog_likelihood(s, δθ)   radial_basis_surrogates.jl:778-785  (cᵀ δK c − tr(L'\(L\δK)))/2,
-//   eval_Dθ_KXX              radial_basis_functions.jl:264-284   δK_ij = ∂ψ/∂ℓ(‖Xi−Xj‖), δK_jj = ∂ψ/∂ℓ(0) = 0
+//   ∇log_likelihood(s)       radial_basis_surrogates.jl:787-799  δθ = e_t for every hyperparameter t
+//   eval_Dθ_KXX              radial_basis_functions.jl:264-284   δK_ij = ∂ψ/∂θ_t(‖Xi−Xj‖), δK_jj = 0
 // which optimize! (radial_basis_surrogates.jl:805-829) evaluates once per L-BFGS iterate.
+// θ = (ℓ) for the Matérn / SE kernels, (ℓ, p) for Periodic (radial_basis_functions.jl:98-103).
 //
-// N ≤ 64 (gpfit_wave_kernel): ONE WAVE per candidate, lanes = rows (columns in the inverse), the
-// factor and L⁻¹ in the wave's LDS (leading dimension 65: row and column walks conflict free),
-// no workgroup barriers.  tr(K⁻¹δK) = Σ_ab (L⁻ᵀL⁻¹)_ab δK_ab from V = L⁻¹ (N³/6) and the lower
-// triangle of VᵀV (N³/6); δK lives in the unused upper triangle of the factor.
-// N > 64 (gpfit_kernel): one workgroup per candidate; N³/3 (Cholesky) + N³/2 (Z = L⁻¹δK) + N³/6
-// (L⁻¹) FMAs on a global workspace (3·N² doubles per candidate, L2-resident at N ≤ 256).
-// Column-parallel steps map one thread to one column; the right-looking Cholesky updates the
-// trailing triangle with all 256 threads between block barriers.
+// N ≤ 64, no factor output (gpfit_reg_kernel): one workgroup per candidate whose four waves
+// evaluate K and δK (one per SIMD); then ONE WAVE, lane i owning row i of K in REGISTERS.  The right-looking Cholesky broadcasts column k with DPP row_newbcast fused into
+// v_fmac_f64 (the column's 16-row blocks replicated by permlane swaps, gpfit_asm.h), so the
+// N³/6 trailing updates run at the FMA rate with no LDS round trip; c by substitution with
+// readlane broadcasts; V = L⁻¹ by columns (lane j = column j) and K⁻¹ = VᵀV with the same DPP
+// broadcasts; tr(K⁻¹δK) and cᵀδKc from K⁻¹.  K and δK are evaluated once per pair j ≤ i.  The
+// reference's operations (chol, then triangular solves); summation orders differ (tolerance).
+// Otherwise (N ≤ 256, or when L / c are requested) gpfit_kernel: one workgroup per candidate;
+// N³/3 (Cholesky) + N³/2 (Z = L⁻¹δK per θ component) + N³/6 (L⁻¹) FMAs on a global workspace
+// (3·N² doubles per candidate, L2-resident at N ≤ 256).  Column-parallel steps map one thread
+// to one column; the right-looking Cholesky updates the trailing triangle with all 256 threads
+// between block barriers.
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include "mrbo_dispatch.h"
+#include "gpfit_asm.h"
 
 namespace mrbo {
 
-// ψ(ρ) and ∂ψ/∂ℓ(ρ) for the radial kernels (radial_basis_functions.jl:60-96; ∇θ_ψ by
-// ForwardDiff there, closed forms here)
-__device__ __forceinline__ void psi_dell(int kind, double ell, double rho, double& psi, double& dpsi) {
+// ψ(ρ) and ∂ψ/∂θ_t(ρ) for the radial kernels (radial_basis_functions.jl:60-103; ∇θ_ψ by
+// ForwardDiff there, closed forms here).  dps[0] = ∂/∂ℓ; Periodic also dps[1] = ∂/∂p.
+__device__ __forceinline__ void psi_dtheta(int kind, double ell, double per, double rho, double& psi,
+                                           double (&dps)[2]) {
+  dps[1] = 0.0;
+  if (kind == 4) {  // Periodic: exp(−2 sin²(πρ/p)/ℓ²)
+    const double u = 3.141592653589793 * rho / per, su = sin(u), il2 = 1.0 / (ell * ell);
+    psi = exp(-2.0 * su * su * il2);
+    dps[0] = psi * 4.0 * su * su * il2 / ell;                                   // ∂/∂ℓ
+    dps[1] = psi * 2.0 * u * il2 * sin(2.0 * u) / per;                          // ∂/∂p = ψ·2πρ sin(2u)/(ℓ²p²)
+    return;
+  }
   if (kind == 3) {  // SE: exp(−ρ²/(2ℓ²))
     const double t = rho * rho / (ell * ell);
     psi = exp(-0.5 * t);
-    dpsi = psi * t / ell;
+    dps[0] = psi * t / ell;
     return;
   }
   const double c = (kind == 0) ? sqrt(5.0) / ell : (kind == 1) ? sqrt(3.0) / ell : 1.0 / ell;
   const double s = c * rho, e = exp(-s);
   if (kind == 0) {          // (1+s+s²/3)e⁻ˢ ; ∂/∂ℓ = (s²/3)(1+s)e⁻ˢ/ℓ
     psi = (1.0 + s * (1.0 + s / 3.0)) * e;
-    dpsi = (s * s / 3.0) * (1.0 + s) * e / ell;
+    dps[0] = (s * s / 3.0) * (1.0 + s) * e / ell;
   } else if (kind == 1) {   // (1+s)e⁻ˢ ; ∂/∂ℓ = s²e⁻ˢ/ℓ
     psi = (1.0 + s) * e;
-    dpsi = s * s * e / ell;
+    dps[0] = s * s * e / ell;
   } else {                  // e⁻ˢ ; ∂/∂ℓ = s e⁻ˢ/ℓ
     psi = e;
-    dpsi = s * e / ell;
+    dps[0] = s * e / ell;
   }
 }
 
@@ -60,19 +78,27 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
   return r;
 }
 
+// candidate p's hyperparameters: θ_p = thetas[p·nt .. p·nt + nt − 1] = (ℓ[, p]); with nt = 1 the
+// Periodic kernel keeps the surrogate's period
+__device__ __forceinline__ void cand_theta(const GpFitParams& q, int p, double& ell, double& per) {
+  ell = q.thetas[(size_t)p * q.nt];
+  per = (q.nt > 1) ? q.thetas[(size_t)p * q.nt + 1] : q.period;
+}
+
 // one workgroup per candidate p; work = 3·N² doubles per candidate: A (K → L, column-major),
-// G (δK, then L⁻¹δK row-major) and V (L⁻¹, row-major), leading dimension N
+// G (δK_t, then L⁻¹δK_t row-major, per hyperparameter t) and V (L⁻¹, row-major), leading dimension N
 __global__ void __launch_bounds__(GPFIT_THREADS) gpfit_kernel(GpFitParams q) {
   __shared__ double sh[GPFIT_THREADS];
   __shared__ double cv[256];
   __shared__ int fail;
   const int N = q.N, d = q.d, t = threadIdx.x, p = blockIdx.x;
-  const double ell = q.ells[p];
+  double ell, per;
+  cand_theta(q, p, ell, per);
   double* A = q.work + (size_t)3 * N * N * p;
   double* G = A + (size_t)N * N;
   double* V = G + (size_t)N * N;
   if (t == 0) fail = 0;
-  // K and δK (eval_KXX :161-178 with ψ(0) on the diagonal; eval_Dθ_KXX :264-284)
+  // K (eval_KXX :161-178 with ψ(0) on the diagonal)
   for (int idx = t; idx < N * N; idx += GPFIT_THREADS) {
     const int i = idx % N, j = idx / N;
     double r2 = 0.0;
@@ -80,10 +106,9 @@ __global__ void __launch_bounds__(GPFIT_THREADS) gpfit_kernel(GpFitParams q) {
       const double r = q.X[a + d * i] - q.X[a + d * j];
       r2 += r * r;
     }
-    double psi, dpsi;
-    psi_dell(q.kernel, ell, (i == j) ? 0.0 : sqrt(r2), psi, dpsi);
+    double psi, dps[2];
+    psi_dtheta(q.kernel, ell, per, (i == j) ? 0.0 : sqrt(r2), psi, dps);
     A[idx] = (i == j) ? psi + q.sn2 : psi;
-    G[idx] = (i == j) ? 0.0 : dpsi;
   }
   __syncthreads();
   // right-looking Cholesky, lower triangle of A in place (PosDefException → status 1)
@@ -106,7 +131,11 @@ __global__ void __launch_bounds__(GPFIT_THREADS) gpfit_kernel(GpFitParams q) {
   }
   __syncthreads();
   if (fail) {
-    if (t == 0) { q.ll[p] = NAN; q.dll[p] = NAN; q.status[p] = 1; }
+    if (t == 0) {
+      q.ll[p] = NAN;
+      for (int u = 0; u < q.nt; ++u) q.grad[(size_t)p * q.nt + u] = NAN;
+      q.status[p] = 1;
+    }
     return;
   }
   // c = L'\(L\y): column-oriented substitutions, c in LDS
@@ -126,44 +155,68 @@ __global__ void __launch_bounds__(GPFIT_THREADS) gpfit_kernel(GpFitParams q) {
     for (int i = t; i < k; i += GPFIT_THREADS) cv[i] -= A[k + N * i] * ck;
     __syncthreads();
   }
-  // log_likelihood (:770-776) and cᵀδKc (thread j: c_j Σ_i δK_ij c_i)
-  double yc = 0.0, ld = 0.0, cgc = 0.0;
+  // log_likelihood (:770-776)
+  double yc = 0.0, ld = 0.0;
   for (int j = t; j < N; j += GPFIT_THREADS) {
     yc += q.y[j] * cv[j];
     ld += log(A[j + N * j]);
-    double s = 0.0;
-    for (int i = 0; i < N; ++i) s += G[(size_t)N * i + j] * cv[i];   // δK symmetric: coalesced in j
-    cgc += cv[j] * s;
   }
   yc = block_sum(yc, sh);
   ld = block_sum(ld, sh);
-  cgc = block_sum(cgc, sh);
-  // tr(L'\(L\δK)) = tr(L⁻ᵀL⁻¹δK) = Σ_ij (L⁻¹δK)_ij (L⁻¹)_ij: thread j forward-substitutes
-  // column j of δK (in place → Z) and of the identity (→ V), rows ascending.  Z and V are kept
-  // row-major (entry (i, j) at i·N + j) so that the threads' loads are coalesced; δK is
-  // symmetric, so G read row-major is δK itself.  L[i][k] is a wave-uniform broadcast.
-  double tr = 0.0;
-  for (int j = t; j < N; j += GPFIT_THREADS) {
-    for (int i = 0; i < N; ++i) {
-      double z = G[(size_t)N * i + j], v = (i == j) ? 1.0 : 0.0;
-      for (int k = 0; k < i; ++k) {
-        const double lik = A[i + N * k];
-        z -= lik * G[(size_t)N * k + j];
-        v -= lik * V[(size_t)N * k + j];
-      }
-      const double li = A[i + N * i];
-      z /= li;
-      v /= li;
-      G[(size_t)N * i + j] = z;
-      V[(size_t)N * i + j] = v;
-      tr += z * v;
-    }
-  }
-  tr = block_sum(tr, sh);
   if (t == 0) {
     q.ll[p] = -0.5 * yc - ld - 0.5 * N * log(2.0 * 3.141592653589793);
-    q.dll[p] = 0.5 * (cgc - tr);
     q.status[p] = 0;
+  }
+  for (int u = 0; u < q.nt; ++u) {
+    // δK_u (eval_Dθ_KXX :264-284, δθ = e_u), symmetric: row-major = column-major
+    for (int idx = t; idx < N * N; idx += GPFIT_THREADS) {
+      const int i = idx % N, j = idx / N;
+      double r2 = 0.0;
+      for (int a = 0; a < d; ++a) {
+        const double r = q.X[a + d * i] - q.X[a + d * j];
+        r2 += r * r;
+      }
+      double psi, dps[2];
+      psi_dtheta(q.kernel, ell, per, (i == j) ? 0.0 : sqrt(r2), psi, dps);
+      G[idx] = (i == j) ? 0.0 : dps[u];
+    }
+    __syncthreads();
+    // cᵀδKc (thread j: c_j Σ_i δK_ij c_i)
+    double cgc = 0.0;
+    for (int j = t; j < N; j += GPFIT_THREADS) {
+      double s = 0.0;
+      for (int i = 0; i < N; ++i) s += G[(size_t)N * i + j] * cv[i];   // δK symmetric: coalesced in j
+      cgc += cv[j] * s;
+    }
+    cgc = block_sum(cgc, sh);
+    // tr(L'\(L\δK)) = tr(L⁻ᵀL⁻¹δK) = Σ_ij (L⁻¹δK)_ij (L⁻¹)_ij: thread j forward-substitutes
+    // column j of δK (in place → Z) and, for the first component, of the identity (→ V), rows
+    // ascending.  Z and V are kept row-major (entry (i, j) at i·N + j) so that the threads'
+    // loads are coalesced; δK is symmetric, so G read row-major is δK itself.  L[i][k] is a
+    // wave-uniform broadcast.
+    double tr = 0.0;
+    for (int j = t; j < N; j += GPFIT_THREADS) {
+      for (int i = 0; i < N; ++i) {
+        double z = G[(size_t)N * i + j], v = (i == j) ? 1.0 : 0.0;
+        for (int k = 0; k < i; ++k) {
+          const double lik = A[i + N * k];
+          z -= lik * G[(size_t)N * k + j];
+          if (u == 0) v -= lik * V[(size_t)N * k + j];
+        }
+        const double li = A[i + N * i];
+        z /= li;
+        G[(size_t)N * i + j] = z;
+        if (u == 0) {
+          v /= li;
+          V[(size_t)N * i + j] = v;
+        } else {
+          v = V[(size_t)N * i + j];
+        }
+        tr += z * v;
+      }
+    }
+    tr = block_sum(tr, sh);
+    if (t == 0) q.grad[(size_t)p * q.nt + u] = 0.5 * (cgc - tr);
   }
   // optional fit outputs: L (lower, zeros above) and c of each candidate
   if (q.L_out) {
@@ -177,136 +230,292 @@ __global__ void __launch_bounds__(GPFIT_THREADS) gpfit_kernel(GpFitParams q) {
     for (int i = t; i < N; i += GPFIT_THREADS) q.c_out[(size_t)N * p + i] = cv[i];
 }
 
-// ---- N ≤ 64: one wave per candidate ---------------------------------------------------
-#ifndef MRBO_GW_WAVES
-#define MRBO_GW_WAVES 1   // A/B at P = 256, N = 64: 1 wave per group 0.287 ms, 2 waves 0.292 ms
-#endif
-constexpr int GW_N = 64, GW_LD = GW_N + 1, GW_WAVES = MRBO_GW_WAVES;   // waves (candidates) per workgroup
-constexpr int GW_WAVE_DOUBLES = 2 * GW_N * GW_LD + GW_N;   // A, V, c
+// ---- N ≤ 64: one wave per candidate, K rows in registers --------------------------------
+constexpr int GR_LD = 65;   // LDS leading dimension (odd: row and column walks conflict free)
 
-__device__ __forceinline__ double gw_sum(double v) {
+__device__ __forceinline__ double gr_sum(double v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-
-__global__ void __launch_bounds__(64 * GW_WAVES) gpfit_wave_kernel(GpFitParams q, int P) {
-  extern __shared__ __attribute__((aligned(16))) double gsm[];
-  const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
-  const int p = blockIdx.x * GW_WAVES + w;
-  if (p >= P) return;   // whole waves: no barrier follows
-  double* A = gsm + (size_t)w * GW_WAVE_DOUBLES;   // L lower (row-major i·LD + j), δK strict upper (j·LD + i)
-  double* V = A + GW_N * GW_LD;                    // L⁻¹ lower, zeros above
-  double* cs = V + GW_N * GW_LD;
-  const int N = q.N, d = q.d, i = lane;
-  const bool act = i < N;
-  const double ell = q.ells[p];
-#ifdef MRBO_GPFIT_STAMPS
-  unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#define WSTAMP(id) do { const unsigned long long t1 = __builtin_amdgcn_s_memtime(); \
-    if (p == 0 && lane == 0) printf("gw %d %d\n", id, (int)(t1 - t0)); t0 = t1; } while (0)
-#else
-#define WSTAMP(id) ((void)0)
-#endif
-  // K (eval_KXX :161-178, ψ(0) + σn2 on the diagonal) and δK (eval_Dθ_KXX :264-284)
-  double xi[8];
-#pragma unroll
-  for (int a = 0; a < 8; ++a) xi[a] = (a < d && act) ? q.X[a + d * i] : 0.0;
-  for (int j = 0; j < N; ++j) {
-    double r2 = 0.0;
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-      if (a < d) { const double r = xi[a] - q.X[a + d * j]; r2 += r * r; }
-    double psi, dpsi;
-    psi_dell(q.kernel, ell, (i == j) ? 0.0 : sqrt(r2), psi, dpsi);
-    if (act && j <= i) A[i * GW_LD + j] = (i == j) ? psi + q.sn2 : psi;
-    if (act && j < i) A[j * GW_LD + i] = dpsi;
-    V[j * GW_LD + i] = 0.0;
-  }
+__device__ __forceinline__ void gr_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  WSTAMP(0);
-  // right-looking Cholesky in place (lane i owns row i); PosDefException → status 1
-  bool fail = false;
-  for (int k = 0; k < N; ++k) {
-    const double piv = A[k * GW_LD + k];
-    if (!(piv > 0.0)) { fail = true; break; }
-    const double lkk = sqrt(piv);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (act && i == k) A[k * GW_LD + k] = lkk;
-    if (act && i > k) A[i * GW_LD + k] /= lkk;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const double lik = (act && i > k) ? A[i * GW_LD + k] : 0.0;
-#pragma unroll 8
-    for (int j = k + 1; j < N; ++j) {
-      const double ljk = A[j * GW_LD + k];
-      if (act && j <= i) A[i * GW_LD + j] -= lik * ljk;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  }
-  if (fail) {
-    if (lane == 0) { q.ll[p] = NAN; q.dll[p] = NAN; q.status[p] = 1; }
-    return;
-  }
-  // c = L'\(L\y)
-  WSTAMP(1);
-  double c = act ? q.y[i] : 0.0;
-  for (int k = 0; k < N; ++k) {
-    const double ck = __shfl(c, k, 64) / A[k * GW_LD + k];
-    if (i == k) c = ck;
-    else if (act && i > k) c -= A[i * GW_LD + k] * ck;
-  }
-  for (int k = N - 1; k >= 0; --k) {
-    const double ck = __shfl(c, k, 64) / A[k * GW_LD + k];
-    if (i == k) c = ck;
-    else if (i < k) c -= A[k * GW_LD + i] * ck;
-  }
-  cs[lane] = act ? c : 0.0;
-  // log_likelihood (:770-776)
-  const double yc = gw_sum(act ? q.y[i] * c : 0.0);
-  const double ld = gw_sum(act ? log(A[i * GW_LD + i]) : 0.0);
-  WSTAMP(2);
-  // V = L⁻¹, lane j = column j, rows ascending (same order as a forward substitution of e_j)
-  for (int r = 0; r < N; ++r) {
-    double acc = (r == i) ? 1.0 : 0.0;
-#pragma unroll 8
-    for (int m = 0; m < r; ++m) acc -= A[r * GW_LD + m] * V[m * GW_LD + i];
-    if (r >= i) V[r * GW_LD + i] = acc / A[r * GW_LD + r];
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  WSTAMP(3);
-  // K⁻¹_ab = Σ_{m ≥ a} V_ma V_mb (lane a, b < a); tr(K⁻¹δK) and cᵀδKc over a > b (δK_aa = 0)
-  double tr = 0.0, cgc = 0.0;
-  for (int b = 0; b < N; ++b) {
-    double kab = 0.0;
-#pragma unroll 8
-    for (int m = b; m < N; ++m) kab += V[m * GW_LD + i] * V[m * GW_LD + b];
-    if (act && b < i) {
-      const double dk = A[b * GW_LD + i];
-      tr += kab * dk;
-      cgc += c * cs[b] * dk;
-    }
-  }
-  WSTAMP(4);
-  tr = 2.0 * gw_sum(tr);
-  cgc = 2.0 * gw_sum(cgc);
-  if (lane == 0) {
-    q.ll[p] = -0.5 * yc - ld - 0.5 * N * log(2.0 * 3.141592653589793);
-    q.dll[p] = 0.5 * (cgc - tr);
-    q.status[p] = 0;
-  }
-  if (q.L_out) {
-    double* Lo = q.L_out + (size_t)N * N * p;
-    for (int j = 0; j < N; ++j)
-      if (act) Lo[i + (size_t)N * j] = (i >= j) ? A[i * GW_LD + j] : 0.0;
-  }
-  if (q.c_out && act) q.c_out[(size_t)N * p + i] = c;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// a[j/16][j%16] += L[j][k]·m for j = k+1..63: the column (lane j holds L[j][k]) broadcast block by
+// block (replicated by permlane swaps, DPP row_newbcast inside the fused FMAs, gpfit_asm.h)
+template <int K>
+__device__ __forceinline__ void gr_rank1(double (&a)[4][16], double col, double m) {
+  constexpr int J0 = K + 1, B0 = J0 / 16, N0 = J0 % 16;
+  if constexpr (J0 < 64) {
+    double b0, b2, b1, b3;
+    if constexpr (B0 <= 2) row_blocks<0>(col, b0, b2);
+    if constexpr (B0 <= 3) row_blocks<1>(col, b1, b3);
+    if constexpr (B0 == 0) RankAsm<N0>::run(a[0], b0, m);
+    if constexpr (B0 <= 1) RankAsm<(B0 == 1) ? N0 : 0>::run(a[1], b1, m);
+    if constexpr (B0 <= 2) RankAsm<(B0 == 2) ? N0 : 0>::run(a[2], b2, m);
+    RankAsm<(B0 == 3) ? N0 : 0>::run(a[3], b3, m);
+  }
+}
+
+// Steps k ≥ N run too (straight-line code the scheduler can overlap across steps): the padding
+// rows are identity rows, so their pivots are 1 and their columns zero -- no change to rows < N.
+// Look-ahead: lane K+1 forms the next pivot a[K+1][K+1] − L[K+1][K]² itself (the same fused
+// multiply-add the broadcast update applies to that entry), so step K+1's pivot chain (readlane,
+// rsq, Newton steps) does not wait for step K's trailing update.
+template <int K>
+__device__ __forceinline__ bool gr_chol_step(double (&a)[4][16], double& dg, double& piv, int lane) {
+  double& akk = a[K / 16][K % 16];
+  const bool ok = piv > 0.0;   // PosDefException; NaNs propagate harmlessly until the end
+  double lkk, ilkk;
+  sqrt_rsqrt(piv, lkk, ilkk);   // √piv and 1/√piv: no IEEE sqrt + division in the step's chain
+  const double col = (lane > K) ? akk * ilkk : akk;
+  akk = (lane == K) ? lkk : col;
+  dg = (lane == K) ? lkk : dg;
+  if constexpr (K + 1 < 64) piv = readlane_d(fma(col, -col, a[(K + 1) / 16][(K + 1) % 16]), K + 1);
+  gr_rank1<K>(a, col, (lane > K) ? -col : 0.0);
+  return ok;
+}
+
+template <int... K>
+__device__ __forceinline__ bool gr_chol(double (&a)[4][16], double& dg, int lane, std::integer_sequence<int, K...>) {
+  bool ok = true;
+  double piv = readlane_d(a[0][0], 0);
+  ((ok = gr_chol_step<K>(a, dg, piv, lane) && ok), ...);
+  return ok;
+}
+
+// c = L'\(L\y), column-oriented substitutions with ck broadcast by readlane: forward step K uses
+// this lane's L[i][K] (register), backward step K its L[K][i] (LDS, row K of L)
+template <int K>
+__device__ __forceinline__ void gr_fwd(double& c, const double (&a)[4][16], double rdg, int lane, int N) {
+  const double ck = readlane_d(c, K) * readlane_d(rdg, K);
+  c = (lane == K) ? ck : ((lane > K) ? c - a[K / 16][K % 16] * ck : c);
+}
+template <int K>
+__device__ __forceinline__ void gr_bwd(double& c, const double* LV, double rdg, int lane, int N) {
+  const double ck = readlane_d(c, K) * readlane_d(rdg, K);
+  const double lki = LV[K * GR_LD + lane];
+  c = (lane == K) ? ck : ((lane < K) ? c - lki * ck : c);
+}
+template <int... K>
+__device__ __forceinline__ void gr_solve(double& c, const double (&a)[4][16], const double* LV, double rdg, int lane,
+                                         int N, std::integer_sequence<int, K...>) {
+  (gr_fwd<K>(c, a, rdg, lane, N), ...);
+  (gr_bwd<63 - K>(c, LV, rdg, lane, N), ...);
+}
+
+// row R of V = L⁻¹ by columns (lane j = column j): v[R] = (δ_Rj − Σ_{m<R} L[R][m] v[m]) / L[R][R].
+// lr = L[R][lane] (row R of L, read by lanes) is replicated block by block; lane j's sum over m
+// broadcasts L[R][m] from lane m (DPP row_newbcast in the fused FMAs, two chains).
+template <int R>
+__device__ __forceinline__ void gr_inv_row(double (&v)[64], const double* LV, double rdg, int lane, int N) {
+  const double lr = LV[R * GR_LD + lane];
+  double acc0 = (lane == R) ? 1.0 : 0.0, acc1 = 0.0;
+  constexpr int NB = (R + 15) / 16;   // blocks of m < R
+  if constexpr (NB > 0) {
+    double b0, b1, b2, b3;
+    row_blocks<0>(lr, b0, b2);
+    if constexpr (NB > 1) row_blocks<1>(lr, b1, b3);
+    double t0 = 0.0, t1 = 0.0;   // −Σ: accumulate the products, subtract once per row
+    DotAsm<(R < 16 ? R : 16)>::run(t0, t1, b0, &v[0]);
+    if constexpr (NB > 1) DotAsm<(R - 16 < 16 ? R - 16 : 16)>::run(t0, t1, b1, &v[16]);
+    if constexpr (NB > 2) DotAsm<(R - 32 < 16 ? R - 32 : 16)>::run(t0, t1, b2, &v[32]);
+    if constexpr (NB > 3) DotAsm<R - 48>::run(t0, t1, b3, &v[48]);
+    acc0 -= t0 + t1;
+  }
+  v[R] = (acc0 + acc1) * readlane_d(rdg, R);
+}
+template <int... R>
+__device__ __forceinline__ void gr_inv(double (&v)[64], const double* LV, double rdg, int lane, int N,
+                                       std::integer_sequence<int, R...>) {
+  (gr_inv_row<R>(v, LV, rdg, lane, N), ...);
+}
+
+// K⁻¹ = VᵀV by columns: lane i accumulates K⁻¹[i][b] = Σ_m V[m][i]·V[m][b] for the 16 columns b of
+// block P + 2·HI, broadcasting lane b's V[m][b] (its v[m]) with DPP (RankAsm)
+template <int P, int HI, int... M>
+__device__ __forceinline__ void gr_kinv_block(const double (&v)[64], double (&kb)[16], std::integer_sequence<int, M...>) {
+  auto step = [&](double vm) {
+    double r0, r2;
+    row_blocks<P>(vm, r0, r2);
+    RankAsm<0>::run(kb, HI ? r2 : r0, vm);
+  };
+  (step(v[M]), ...);
+}
+
+// -DMRBO_GPFIT_STAMPS: cycles per phase of candidate 0 (one printf at the end): X staging, K rows,
+// Cholesky, c, L⁻¹, K⁻¹·δK traces
+#ifdef MRBO_GPFIT_STAMPS
+#define GR_STAMP(id) do { gr_ts[id] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define GR_STAMP(id) ((void)0)
+#endif
+
+// GR_WAVES waves per candidate: all of them evaluate the K / δK pairs (one per SIMD), then wave 0
+// alone runs the register phases (no workgroup barrier after the pairs)
+constexpr int GR_WAVES = 4;
+
+template <int NT>
+__global__ void __launch_bounds__(64 * GR_WAVES) gpfit_reg_kernel(GpFitParams q, int P) {
+  extern __shared__ __attribute__((aligned(16))) double gsm[];
+  const int p = blockIdx.x, lane = threadIdx.x & 63, tid = threadIdx.x;
+  if (p >= P) return;   // whole workgroups
+#ifdef MRBO_GPFIT_STAMPS
+  unsigned long long gr_ts[6], gr_t0 = __builtin_amdgcn_s_memtime();
+#endif
+  double* LV = gsm;                     // K, then L, row-major (i·LD + j)
+  double* DK = LV + 64 * GR_LD;         // δK_t (symmetric) at t·64·LD + i·LD + j
+  double* cs = DK + NT * 64 * GR_LD;    // c
+  double* XS = cs + 64;                 // X[u][j] at u·64 + j (u < d)
+  const int N = q.N, d = q.d;
+  const bool act = lane < N;
+  double ell, per;
+  cand_theta(q, p, ell, per);
+  if (tid < 64)
+    for (int u = 0; u < d; ++u) XS[u * 64 + lane] = act ? q.X[u + d * lane] : 0.0;
+  __syncthreads();
+  GR_STAMP(0);
+  // K (eval_KXX :161-178, ψ(0) + σn2 on the diagonal; padding = identity) and δK_t (eval_Dθ_KXX
+  // :264-284) over the 2080 pairs j ≤ i of the lower triangle, lanes over pairs, both halves written
+  for (int q0 = 0; q0 < 64 * 65 / 2; q0 += 64 * GR_WAVES) {
+    const int qq = q0 + tid;
+    if (qq >= 64 * 65 / 2) break;
+    int i = (int)((sqrt(8.0 * qq + 1.0) - 1.0) * 0.5);
+    i += ((i + 1) * (i + 2) / 2 <= qq) ? 1 : 0;   // exact row of the triangle index
+    i -= (i * (i + 1) / 2 > qq) ? 1 : 0;
+    const int j = qq - i * (i + 1) / 2;
+    double r2 = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (u < d) { const double r = XS[u * 64 + i] - XS[u * 64 + j]; r2 = fma(r, r, r2); }
+    double psi, dps[2];
+    psi_dtheta(q.kernel, ell, per, (i == j) ? 0.0 : sqrt(r2), psi, dps);
+    const bool v = i < N;   // j ≤ i
+    const double kij = v ? ((i == j) ? psi + q.sn2 : psi) : ((i == j) ? 1.0 : 0.0);
+    LV[i * GR_LD + j] = kij;
+    LV[j * GR_LD + i] = kij;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const double dk = (v && i != j) ? dps[t] : 0.0;
+      DK[t * 64 * GR_LD + i * GR_LD + j] = dk;
+      DK[t * 64 * GR_LD + j * GR_LD + i] = dk;
+    }
+  }
+  __syncthreads();
+  GR_STAMP(1);
+  // wave 0: the register phases; the other waves wait at the next barrier
+  __shared__ double part[GR_WAVES][2 * NT + 2];   // per-wave partial sums; [0][2NT..] = yc, log det
+  __shared__ int failed;
+  if (tid < 64) {
+    double a[4][16];
+#pragma unroll
+    for (int j = 0; j < 64; ++j) a[j / 16][j % 16] = LV[lane * GR_LD + j];
+    // right-looking Cholesky in registers (PosDefException → status 1); dg = L_ii of this row
+    double dg = 1.0;
+    const bool chol_ok = gr_chol(a, dg, lane, std::make_integer_sequence<int, 64>{});
+    GR_STAMP(2);
+    gr_sync();
+#pragma unroll
+    for (int j = 0; j < 64; ++j) LV[lane * GR_LD + j] = a[j / 16][j % 16];
+    gr_sync();
+    // c = L'\(L\y), column-oriented substitutions (ck broadcast by readlane)
+    const double rdg = 1.0 / dg;
+    double c = act ? q.y[lane] : 0.0;
+    gr_solve(c, a, LV, rdg, lane, N, std::make_integer_sequence<int, 64>{});
+    GR_STAMP(3);
+    cs[lane] = c;
+    const double yc = gr_sum(act ? q.y[lane] * c : 0.0);
+    const double ld = gr_sum(act ? log(dg) : 0.0);
+    // V = L⁻¹ by columns (lane j = column j), rows ascending (rows ≥ N: identity, no effect on rows < N)
+    double v[64];
+#pragma unroll
+    for (int r = 0; r < 64; ++r) v[r] = 0.0;
+    gr_inv(v, LV, rdg, lane, N, std::make_integer_sequence<int, 64>{});
+    gr_sync();
+#pragma unroll
+    for (int m = 0; m < 64; ++m) LV[m * GR_LD + lane] = v[m];   // V row-major for every wave
+    if (lane == 0) {
+      failed = !chol_ok;
+      part[0][2 * NT] = yc;
+      part[0][2 * NT + 1] = ld;
+    }
+    GR_STAMP(4);
+  }
+  __syncthreads();
+  if (failed) {
+    if (tid == 0) {
+      q.ll[p] = NAN;
+      for (int t = 0; t < NT; ++t) q.grad[(size_t)p * NT + t] = NAN;
+      q.status[p] = 1;
+    }
+    return;
+  }
+  // tr(K⁻¹δK_t) = Σ_ib K⁻¹_ib δK_t[i][b] and cᵀδK_t c = Σ_ib c_i δK_t[i][b] c_b (full sums; δK_ii = 0).
+  // Wave w: K⁻¹ columns b of block w (K⁻¹ = VᵀV by DPP broadcasts of V[m][b]), lane i = row.
+  const int w = tid >> 6;
+  double v[64];
+#pragma unroll
+  for (int m = 0; m < 64; ++m) v[m] = LV[m * GR_LD + lane];
+  const double c = cs[lane];
+  double kb[16];
+#pragma unroll
+  for (int n = 0; n < 16; ++n) kb[n] = 0.0;
+  if (w == 0) gr_kinv_block<0, 0>(v, kb, std::make_integer_sequence<int, 64>{});
+  else if (w == 1) gr_kinv_block<1, 0>(v, kb, std::make_integer_sequence<int, 64>{});
+  else if (w == 2) gr_kinv_block<0, 1>(v, kb, std::make_integer_sequence<int, 64>{});
+  else gr_kinv_block<1, 1>(v, kb, std::make_integer_sequence<int, 64>{});
+  double tr[NT], cgc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) tr[t] = cgc[t] = 0.0;
+#pragma unroll
+  for (int n = 0; n < 16; ++n) {
+    const int b = 16 * w + n;
+    const double cb = cs[b];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const double dk = DK[t * 64 * GR_LD + b * GR_LD + lane];
+      tr[t] = fma(kb[n], dk, tr[t]);
+      cgc[t] = fma(c * cb, dk, cgc[t]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const double trs = gr_sum(act ? tr[t] : 0.0), cgs = gr_sum(act ? cgc[t] : 0.0);
+    if (lane == 0) {
+      part[w][t] = trs;
+      part[w][NT + t] = cgs;
+    }
+  }
+  GR_STAMP(5);
+  __syncthreads();
+  if (tid == 0) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const double trs = (part[0][t] + part[1][t]) + (part[2][t] + part[3][t]);
+      const double cgs = (part[0][NT + t] + part[1][NT + t]) + (part[2][NT + t] + part[3][NT + t]);
+      q.grad[(size_t)p * NT + t] = 0.5 * (cgs - trs);
+    }
+    q.ll[p] = -0.5 * part[0][2 * NT] - part[0][2 * NT + 1] - 0.5 * N * log(2.0 * 3.141592653589793);
+    q.status[p] = 0;
+  }
+#ifdef MRBO_GPFIT_STAMPS
+  if (p == 0 && tid == 0)
+    printf("gpfit_reg cycles: X %llu  K rows %llu  chol %llu  c %llu  inv %llu  traces %llu\n", gr_ts[0] - gr_t0,
+           gr_ts[1] - gr_ts[0], gr_ts[2] - gr_ts[1], gr_ts[3] - gr_ts[2], gr_ts[4] - gr_ts[3], gr_ts[5] - gr_ts[4]);
+#endif
+}
+
+size_t gpfit_reg_lds(int nt) { return sizeof(double) * ((size_t)(1 + nt) * 64 * GR_LD + 64 + 16 * 64); }
+
 void launch_gpfit(int P, hipStream_t st, const GpFitParams& q) {
-  if (gpfit_in_lds(q.N, q.d)) {
-    hipLaunchKernelGGL(gpfit_wave_kernel, dim3((P + GW_WAVES - 1) / GW_WAVES), dim3(64 * GW_WAVES),
-                       sizeof(double) * GW_WAVES * GW_WAVE_DOUBLES, st, q, P);
+  if (gpfit_in_regs(q)) {
+    if (q.nt == 2)
+      hipLaunchKernelGGL(gpfit_reg_kernel<2>, dim3(P), dim3(64 * GR_WAVES), gpfit_reg_lds(2), st, q, P);
+    else
+      hipLaunchKernelGGL(gpfit_reg_kernel<1>, dim3(P), dim3(64 * GR_WAVES), gpfit_reg_lds(1), st, q, P);
     return;
   }
   hipLaunchKernelGGL(gpfit_kernel, dim3(P), dim3(GPFIT_THREADS), 0, st, q);

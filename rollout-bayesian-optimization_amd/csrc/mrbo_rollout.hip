@@ -214,20 +214,6 @@ __device__ __forceinline__ void stamp_region(WaveCtx<D, RPL>& W, int k) {
 // fused into the FMA (bcast_asm.h: one software-pipelined asm statement per block).  V never goes through LDS: the only LDS traffic is one ds_read_b64 of
 // L0⁻¹ per step (the row broadcast through LDS cost 8× that and bounded the whole loop).
 
-// blocks p and p+2 of v, each replicated into all four 16-lane rows
-template <int P>
-__device__ __forceinline__ void row_blocks(double v, double& blk_p, double& blk_p2) {
-  int lo, hi;
-  dsplit(v, lo, hi);
-  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // [r0 r0 r2 r2], [r1 r1 r3 r3]
-  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  const int tlo = P ? a[1] : a[0], thi = P ? b[1] : b[0];
-  const auto c = __builtin_amdgcn_permlane32_swap(tlo, tlo, false, false); // [rP ×4], [rP+2 ×4]
-  const auto d = __builtin_amdgcn_permlane32_swap(thi, thi, false, false);
-  blk_p = djoin(c[0], d[0]);
-  blk_p2 = djoin(c[1], d[1]);
-}
-
 // LDS byte address of a pointer into the dynamic shared array
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;

@@ -33,7 +33,7 @@ STATUS_BITS = {
 EXPORTS = [
     "mrbo_version", "mrbo_last_error", "mrbo_device_count", "mrbo_plan_create", "mrbo_plan_destroy",
     "mrbo_simulate_mc", "mrbo_simulate_ghq", "mrbo_eto_reduce", "mrbo_partial_moments", "mrbo_eval_base", "mrbo_rnstream",
-    "mrbo_initial_guesses", "mrbo_dual_uniform", "mrbo_last_kernel_ms", "mrbo_gp_fit",
+    "mrbo_initial_guesses", "mrbo_dual_uniform", "mrbo_last_kernel_ms", "mrbo_gp_fit", "mrbo_gp_fit_theta",
     "mrbo_plan_info", "mrbo_last_gp_fit_ms", "mrbo_plan_set_order",
 ]
 
@@ -93,6 +93,8 @@ def load():
     L.mrbo_dual_uniform.restype = ctypes.c_double
     L.mrbo_gp_fit.argtypes = [ctypes.POINTER(SurrogateDesc), ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp,
                               ctypes.c_uint32, _vp]
+    L.mrbo_gp_fit_theta.argtypes = [ctypes.POINTER(SurrogateDesc), ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp,
+                                    _vp, _vp, _vp, ctypes.c_uint32, _vp]
     L.mrbo_last_kernel_ms.argtypes = [_vp]
     L.mrbo_last_kernel_ms.restype = ctypes.c_double
     L.mrbo_plan_info.argtypes = [_vp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]

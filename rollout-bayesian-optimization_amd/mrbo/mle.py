@@ -21,46 +21,53 @@ from . import _lib
 _STEPS = 0.5 ** np.arange(12)
 
 
-def gp_fit_batch(s, ells, want_fit=False):
-    """Refit the base GP of `s` at each lengthscale in `ells` on the device.
+def _nt(s):
+    """Hyperparameters of the kernel: (ℓ), or (ℓ, p) for Periodic (radial_basis_functions.jl:98-103)."""
+    return len(s.ψ.θ)
 
-    Returns dict(ll, dll, status[, L (N×N×P), c (N×P)]); status 1 = PosDefException."""
+
+def gp_fit_batch(s, thetas, want_fit=False):
+    """Refit the base GP of `s` at each hyperparameter vector on the device (mrbo_gp_fit_theta).
+
+    `thetas` is (P,) -- lengthscales -- or (P, nt) with nt = len(s.ψ.θ).  Returns dict(ll, grad
+    (P, nt), dll (= grad[:, 0]), status[, L (N×N×P), c (N×P)]); status 1 = PosDefException."""
     L = _lib.load()
-    ells = np.ascontiguousarray(np.asarray(ells, dtype=np.float64).ravel())
-    P = ells.size
+    th = np.asarray(thetas, dtype=np.float64)
+    th = np.ascontiguousarray(th.reshape(th.shape[0], -1) if th.ndim > 1 else th.reshape(-1, 1))
+    P, nt = th.shape
     n = s.observed
     X = np.asfortranarray(s.X[:, :n])
     y = np.ascontiguousarray(s.y[:n])
     dp = ctypes.POINTER(ctypes.c_double)
     sd = _lib.SurrogateDesc(X.shape[0], n, int(s.ψ.kind), float(s.ψ.lengthscale), float(s.σn2), float(s.fmini()),
-                            X.ctypes.data_as(dp), None, n, None, y.ctypes.data_as(dp))
-    ll, dll = np.zeros(P), np.zeros(P)
+                            X.ctypes.data_as(dp), None, n, None, y.ctypes.data_as(dp), float(s.ψ.period))
+    ll, grad = np.zeros(P), np.zeros((P, nt))
     st = np.zeros(P, dtype=np.int32)
     Lo = np.zeros((n, n, P), order="F") if want_fit else None
     co = np.zeros((n, P), order="F") if want_fit else None
     vp = lambda a: ctypes.c_void_p(a.ctypes.data) if a is not None else None
-    _lib.check(L.mrbo_gp_fit(ctypes.byref(sd), P, vp(ells), vp(ll), vp(dll), vp(st), vp(Lo), vp(co),
-                             _lib.MRBO_FLAG_HOST_POINTERS, None))
-    out = dict(ll=ll, dll=dll, status=st)
+    _lib.check(L.mrbo_gp_fit_theta(ctypes.byref(sd), P, nt, vp(th), vp(ll), vp(grad), vp(st), vp(Lo), vp(co),
+                                   _lib.MRBO_FLAG_HOST_POINTERS, None))
+    out = dict(ll=ll, grad=grad, dll=grad[:, 0].copy(), status=st)
     if want_fit:
         out["L"], out["c"] = Lo, co
     return out
 
 
 def log_likelihood(s):
-    """log_likelihood(s) at the surrogate's current lengthscale (radial_basis_surrogates.jl:770-776)."""
-    r = gp_fit_batch(s, [s.ψ.lengthscale])
+    """log_likelihood(s) at the surrogate's current hyperparameters (radial_basis_surrogates.jl:770-776)."""
+    r = gp_fit_batch(s, s.ψ.θ[None, :])
     if r["status"][0]:
         raise np.linalg.LinAlgError("PosDefException (cholesky of K)")
     return float(r["ll"][0])
 
 
 def grad_log_likelihood(s):
-    """∇log_likelihood(s): ∂/∂θ of log_likelihood for the kernel hyperparameters (one lengthscale)."""
-    r = gp_fit_batch(s, [s.ψ.lengthscale])
+    """∇log_likelihood(s) (radial_basis_surrogates.jl:787-799): ∂/∂θ_t for every kernel hyperparameter."""
+    r = gp_fit_batch(s, s.ψ.θ[None, :])
     if r["status"][0]:
         raise np.linalg.LinAlgError("PosDefException (cholesky of K)")
-    return np.array([r["dll"][0]])
+    return r["grad"][0].copy()
 
 
 def projected_lbfgs(fg_batch, x0, lower, upper, iterations=30, g_tol=1e-8, m=10, c1=1e-4):
@@ -122,13 +129,14 @@ def projected_lbfgs(fg_batch, x0, lower, upper, iterations=30, g_tol=1e-8, m=10,
 
 def optimize(s, lowerbounds, upperbounds, iterations=30):
     """optimize!(s; lowerbounds, upperbounds) (radial_basis_surrogates.jl:805-829): maximise the
-    log likelihood over the lengthscale within the box, then set_kernel! at the optimum."""
+    log likelihood over the kernel hyperparameters (ℓ; Periodic ℓ and p) within the box, then
+    set_kernel! at the optimum."""
     def fg(T):
-        r = gp_fit_batch(s, T[:, 0])
+        r = gp_fit_batch(s, T)
         f = np.where(r["status"] == 0, -r["ll"], np.nan)
-        return f, -r["dll"][:, None]
+        return f, -r["grad"]
 
-    θ, f, g, it = projected_lbfgs(fg, np.array([s.ψ.lengthscale]), lowerbounds, upperbounds, iterations)
+    θ, f, g, it = projected_lbfgs(fg, s.ψ.θ.copy(), lowerbounds, upperbounds, iterations)
     from .kernels import set_hyperparameters
     s.set_kernel(set_hyperparameters(s.ψ, θ))
     return dict(theta=θ, neg_log_likelihood=f, gradient=g, iterations=it)

@@ -127,14 +127,16 @@ def test_gp_fit_vs_oracle(gpu, oracle, kernel, d, N):
     ells = np.array([0.2, 0.5, 1.0, 2.0, 4.0]) * np.sqrt(d) * (0.15 if kernel == "se" else 1.0)
     s = _surrogate(X, y, kernel, 1.0)
     r = gp_fit_batch(s, ells, want_fit=True)
+    rr = gp_fit_batch(s, ells)   # N ≤ 64: the one-wave register kernel (no factor outputs)
     for p, ell in enumerate(ells):
         ll, dll, L, c = oracle.log_likelihood(X, y, kernel, ell, 1e-6, want_fit=True)
         if np.isnan(ll):
-            assert r["status"][p] == 1
+            assert r["status"][p] == 1 and rr["status"][p] == 1
             continue
-        assert r["status"][p] == 0
-        assert r["ll"][p] == pytest.approx(ll, rel=1e-10, abs=1e-9)
-        assert r["dll"][p] == pytest.approx(dll, rel=1e-8, abs=1e-8 * (1 + abs(ll)))
+        assert r["status"][p] == 0 and rr["status"][p] == 0
+        for q in (r, rr):
+            assert q["ll"][p] == pytest.approx(ll, rel=1e-10, abs=1e-9)
+            assert q["dll"][p] == pytest.approx(dll, rel=1e-8, abs=1e-8 * (1 + abs(ll)))
         np.testing.assert_allclose(r["L"][:, :, p], L, rtol=1e-10, atol=1e-12)
         np.testing.assert_allclose(r["c"][:, p], c, rtol=1e-8, atol=1e-8 * np.abs(c).max())
 
@@ -163,3 +165,93 @@ def test_optimize_on_device_vs_oracle_driven(gpu, oracle, kernel):
     assert s.ψ.lengthscale == pytest.approx(θo[0], rel=1e-7)
     assert log_likelihood(s) == pytest.approx(-fo, rel=1e-10)
     _assert_kkt(res["theta"][0], res["gradient"][0], 0.1, 5.0, 1e-5 * max(1.0, abs(fo)))
+
+
+# ---------------------------------------------------------------------------------- Periodic
+# θ = (ℓ, p) (radial_basis_functions.jl:98-103); ∇log_likelihood over both (r_b_s.jl:787-799).
+# The kernel of a Euclidean distance is positive definite in one dimension: 1-D data.
+def _per_data(N, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.random((1, N)) * 3.0
+    return X, np.sin(3 * X[0]) + 0.1 * rng.standard_normal(N)
+
+
+def _numpy_ll_per(X, y, th, sn2):
+    rho = np.abs(X[0][:, None] - X[0][None, :])
+    K = np.exp(-2 * np.sin(np.pi * rho / th[1]) ** 2 / th[0] ** 2) + sn2 * np.eye(len(y))
+    cf = cho_factor(K, lower=True)
+    c = cho_solve(cf, y)
+    return -y @ c / 2 - np.log(np.diag(cf[0])).sum() - len(y) * np.log(2 * np.pi) / 2
+
+
+@pytest.mark.parametrize("th", [(0.7, 1.3), (1.5, 0.8), (2.0, 2.5)])
+def test_oracle_periodic_grad_vs_fd(oracle, th):
+    X, y = _per_data(20)
+    sn2 = 1e-3
+    ll, g = oracle.log_likelihood_theta(X, y, "periodic", th, sn2)
+    assert ll == pytest.approx(_numpy_ll_per(X, y, th, sn2), rel=1e-9)
+    for t in range(2):
+        h = 1e-6 * th[t]
+        e = np.eye(2)[t] * h
+        fd = (_numpy_ll_per(X, y, np.add(th, e), sn2) - _numpy_ll_per(X, y, np.subtract(th, e), sn2)) / (2 * h)
+        assert g[t] == pytest.approx(fd, rel=1e-5, abs=1e-5 * (1 + abs(ll)))
+    # one-element θ keeps the period: ∂/∂ℓ only, equal to the first component
+    ll1, g1 = oracle.log_likelihood_theta(X, y, "periodic", th[:1], sn2, period=th[1])
+    assert ll1 == ll and g1[0] == g[0]
+
+
+def _per_surrogate(X, y, th, sn2):
+    from mrbo import kernels
+    from mrbo.surrogates import Surrogate
+    return Surrogate(kernels.Periodic(list(th)), X, y, capacity=X.shape[1], σn2=sn2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [16, 64, 100])
+def test_gp_fit_periodic_vs_oracle(gpu, oracle, N):
+    from mrbo.mle import gp_fit_batch
+    X, y = _per_data(N, seed=N)
+    sn2 = 1e-3
+    th = np.array([[0.7, 1.3], [1.5, 0.8], [2.0, 2.5], [0.5, 1.9]])
+    s = _per_surrogate(X, y, th[0], sn2)
+    for want_fit in (False, True):
+        r = gp_fit_batch(s, th, want_fit=want_fit)
+        for p in range(len(th)):
+            ll, g = oracle.log_likelihood_theta(X, y, "periodic", th[p], sn2)
+            assert r["status"][p] == 0
+            assert r["ll"][p] == pytest.approx(ll, rel=1e-10, abs=1e-9)
+            np.testing.assert_allclose(r["grad"][p], g, rtol=1e-8, atol=1e-8 * (1 + abs(ll)))
+    # one hyperparameter: ∂/∂ℓ at the surrogate's period
+    r1 = gp_fit_batch(s, th[:, 0])
+    for p in range(len(th)):
+        ll, g = oracle.log_likelihood_theta(X, y, "periodic", th[p, :1], sn2, period=th[0, 1])
+        assert r1["ll"][p] == pytest.approx(ll, rel=1e-10, abs=1e-9)
+        assert r1["dll"][p] == pytest.approx(g[0], rel=1e-8, abs=1e-8 * (1 + abs(ll)))
+
+
+@pytest.mark.gpu
+def test_optimize_periodic_on_device_vs_oracle_driven(gpu, oracle):
+    """optimize! over (ℓ, p) for the Periodic kernel: the device run and the oracle-driven run of
+    the same minimiser reach the same KKT point."""
+    from mrbo.mle import optimize, projected_lbfgs
+    rng = np.random.default_rng(7)   # period-1.2 data: the likelihood has a clear optimum in p
+    X = rng.random((1, 30)) * 3.0
+    y = np.sin(2 * np.pi * X[0] / 1.2) + 0.1 * rng.standard_normal(30)
+    sn2 = 1e-2
+    s = _per_surrogate(X, y, (1.0, 1.5), sn2)
+    lo, hi = [0.2, 0.5], [3.0, 3.0]
+    res = optimize(s, lo, hi, iterations=30)
+
+    def fg(T):
+        f, g = np.zeros(len(T)), np.zeros_like(T)
+        for i, t in enumerate(T):
+            ll, gr = oracle.log_likelihood_theta(X, y, "periodic", t, sn2)
+            f[i], g[i] = -ll, -gr
+        return f, g
+
+    θo, fo, go, _ = projected_lbfgs(fg, np.array([1.0, 1.5]), lo, hi, 30)
+    np.testing.assert_allclose(res["theta"], θo, rtol=1e-6)
+    np.testing.assert_allclose(s.ψ.θ, θo, rtol=1e-6)
+    assert abs(res["theta"][1] - 1.2) < 0.05      # the data's period
+    for t in range(2):
+        _assert_kkt(res["theta"][t], res["gradient"][t], lo[t], hi[t], 1e-4 * max(1.0, abs(fo)))
