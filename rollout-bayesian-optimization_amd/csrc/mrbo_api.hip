@@ -86,7 +86,7 @@ bool get_kset(int d, int rpl, KernelSet& ks) {
 #ifdef MRBO_ONLY_D
     CASE(MRBO_ONLY_D)
 #else
-    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
 #endif
     default: return false;
   }
@@ -102,7 +102,7 @@ void launch_tables(int d, int rpl, int nstarts, hipStream_t st, const KParams& k
 #ifdef MRBO_ONLY_D
   switch (d) { CASE(MRBO_ONLY_D) }
 #else
-  switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) }
+  switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) }
 #endif
 #undef CASE
 #undef CASE_
@@ -115,7 +115,7 @@ void launch_rollout(int d, int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStre
 #ifdef MRBO_ONLY_D
   switch (d) { CASE(MRBO_ONLY_D) }
 #else
-  switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) }
+  switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) }
 #endif
 #undef CASE
 #undef CASE_
@@ -127,7 +127,7 @@ void launch_evalb(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, con
 #ifdef MRBO_ONLY_D
   switch (d) { CASE(MRBO_ONLY_D) }
 #else
-  switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) }
+  switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) }
 #endif
 #undef CASE
 #undef CASE_
@@ -319,8 +319,9 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   *out = nullptr;
   const int d = s->d, N = s->N;
   if (d < 1 || N < 1 || !s->X || !s->L || !s->c || !s->y) return fail(MRBO_ERR_ARG, "bad surrogate (d=%d N=%d)", d, N);
-  if (d > 8) return fail(MRBO_ERR_UNSUPPORTED, "d=%d > 8 not compiled", d);
-  if (N > 256) return fail(MRBO_ERR_UNSUPPORTED, "N=%d > 256 not compiled", N);
+  if (d > 16) return fail(MRBO_ERR_UNSUPPORTED, "d=%d > 16 not compiled", d);
+  if (N > 512) return fail(MRBO_ERR_UNSUPPORTED, "N=%d > 512 not compiled", N);
+  if (d > 8 && N > 128) return fail(MRBO_ERR_UNSUPPORTED, "d=%d > 8 with N=%d > 128 not compiled", d, N);
   if (p->h < 0 || p->h > FMAX - 1) return fail(MRBO_ERR_UNSUPPORTED, "h=%d outside [0,%d]", p->h, FMAX - 1);
   if (p->M < 1 || p->R < 1 || p->nstarts < 1 || !p->lbs || !p->ubs) return fail(MRBO_ERR_ARG, "bad params");
   if (p->rule != MRBO_RULE_EI && p->rule != MRBO_RULE_POI && p->rule != MRBO_RULE_LCB)
@@ -336,7 +337,7 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   P->device = device;
   P->d = d;
   P->N = N;
-  P->RPL = (N <= 64) ? 1 : (N <= 128) ? 2 : 4;
+  P->RPL = (N <= 64) ? 1 : (N <= 128) ? 2 : (N <= 256) ? 4 : 8;
   P->NR = 64 * P->RPL;
   P->Npad = P->NR;
   P->p = *p;
@@ -433,7 +434,7 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   // (MRBO_GENERIC_KERNEL=1 forces the generic instantiation, for A/B runs and tests)
   const char* gen = getenv("MRBO_GENERIC_KERNEL");
   P->spec = (P->kernel == MRBO_KERNEL_MATERN52 && P->p.rule == MRBO_RULE_EI && P->p.cost == MRBO_COST_NONE &&
-             !(gen && gen[0] == '1')) ? 1 : 0;
+             ks.rollout_spec && !(gen && gen[0] == '1')) ? 1 : 0;
   const void* rk = P->spec ? ks.rollout_spec : ks.rollout;
   const int waves0 =
       pick_grid(rk, fixed, ks.wave_bytes, prop.multiProcessorCount, wpg0, blocks0, smem0, 0, maxw);

@@ -1,5 +1,5 @@
 // mrbo_dispatch.h -- interface between the host API (mrbo_api.hip) and the per-dimension
-// kernel translation units (mrbo_kernels.hip compiled once per d = 1..8 with -DMRBO_D=d).
+// kernel translation units (mrbo_kernels.hip compiled once per d = 1..16 with -DMRBO_D=d).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -10,7 +10,7 @@ namespace mrbo {
 // launch geometry and L0⁻¹ image of one rollout_kernel<D, RPL> / eval_base_kernel<D, RPL> pair
 struct KernelSet {
   const void* rollout;      // generic: kernel function and decision rule from KParams
-  const void* rollout_spec; // Matérn-5/2 + EI fixed at compile time (rollout_kernel SPEC = 1)
+  const void* rollout_spec; // Matérn-5/2 + EI fixed at compile time (rollout_kernel SPEC = 1), or null
   const void* evalb;
   size_t wave_bytes;        // per-wave LDS
   bool square;              // L0⁻¹ layout: dense square (ld) or packed triangle
@@ -29,6 +29,8 @@ struct KernelSet {
   void launch_tables_d##DD(int rpl, int nstarts, hipStream_t st, const KParams& kp);
 MRBO_DECLARE_D(1) MRBO_DECLARE_D(2) MRBO_DECLARE_D(3) MRBO_DECLARE_D(4)
 MRBO_DECLARE_D(5) MRBO_DECLARE_D(6) MRBO_DECLARE_D(7) MRBO_DECLARE_D(8)
+MRBO_DECLARE_D(9) MRBO_DECLARE_D(10) MRBO_DECLARE_D(11) MRBO_DECLARE_D(12)
+MRBO_DECLARE_D(13) MRBO_DECLARE_D(14) MRBO_DECLARE_D(15) MRBO_DECLARE_D(16)
 #undef MRBO_DECLARE_D
 
 // base-GP fit + marginal likelihood for P lengthscales (mrbo_gpfit.hip)

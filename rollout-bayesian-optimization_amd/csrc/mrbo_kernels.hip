@@ -1,10 +1,13 @@
 // mrbo_kernels.hip -- the rollout / eval_base kernels for ONE input dimension d = MRBO_D
 // (compiled once per d, in parallel; mrbo_api.hip dispatches through mrbo_dispatch.h).
+// Rows per lane (RPL) compiled: d ≤ 8: 1, 2, 4, 8 (N ≤ 64, 128, 256, 512); d = 9..16: 1, 2
+// (N ≤ 128).  The compile-time Matérn-5/2 + EI specialisation (SPEC = 1) exists for d ≤ 8 and
+// RPL ≤ 4 -- the configurations of BASELINE.json; everything else runs the generic kernel.
 #include "mrbo_dispatch.h"
 #include "mrbo_rollout.hip"
 
 #ifndef MRBO_D
-#error "compile with -DMRBO_D=<1..8>"
+#error "compile with -DMRBO_D=<1..16>"
 #endif
 
 #define MRBO_CAT_(a, b) a##b
@@ -12,28 +15,42 @@
 
 namespace mrbo {
 
+constexpr bool has_rpl(int d, int rpl) { return rpl == 1 || rpl == 2 || (d <= 8 && (rpl == 4 || rpl == 8)); }
+constexpr bool has_spec(int d, int rpl) { return d <= 8 && rpl <= 4; }
+
 template <int D, int RPL>
 static KernelSet kset() {
   using Ly = Lay<D, RPL>;
-  return KernelSet{(const void*)&rollout_kernel<D, RPL, 0>, (const void*)&rollout_kernel<D, RPL, 1>,
-                   (const void*)&eval_base_kernel<D, RPL>,
-                   sizeof(double) * Ly::WAVE_LDS, Ly::SQ, Ly::BC && !Ly::SQ, Ly::LD, Ly::LINV_DOUBLES, Ly::GL, Ly::LINV_GLOBAL,
-                   KBounds<RPL>::threads};
+  const void* spec = nullptr;
+  if constexpr (has_spec(D, RPL)) spec = (const void*)&rollout_kernel<D, RPL, 1>;
+  return KernelSet{(const void*)&rollout_kernel<D, RPL, 0>, spec, (const void*)&eval_base_kernel<D, RPL>,
+                   sizeof(double) * Ly::WAVE_LDS, Ly::SQ, Ly::BC && !Ly::SQ, Ly::LD, Ly::LINV_DOUBLES, Ly::GL,
+                   Ly::LINV_GLOBAL, KBounds<D, RPL>::threads};
 }
 
 bool MRBO_CAT(kset_d, MRBO_D)(int rpl, KernelSet& ks) {
   if (rpl == 1) ks = kset<MRBO_D, 1>();
   else if (rpl == 2) ks = kset<MRBO_D, 2>();
+#if MRBO_D <= 8
   else if (rpl == 4) ks = kset<MRBO_D, 4>();
+  else if (rpl == 8) ks = kset<MRBO_D, 8>();
+#endif
   else return false;
   return true;
 }
 
+template <int RPL, int SPEC>
+static void launch_one(dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
+  if constexpr (has_rpl(MRBO_D, RPL) && (SPEC == 0 || has_spec(MRBO_D, RPL)))
+    hipLaunchKernelGGL((rollout_kernel<MRBO_D, RPL, SPEC>), g, b, sm, st, kp);
+}
+
 template <int SPEC>
 static void launch_rollout_spec(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
-  if (rpl == 1) hipLaunchKernelGGL((rollout_kernel<MRBO_D, 1, SPEC>), g, b, sm, st, kp);
-  else if (rpl == 2) hipLaunchKernelGGL((rollout_kernel<MRBO_D, 2, SPEC>), g, b, sm, st, kp);
-  else hipLaunchKernelGGL((rollout_kernel<MRBO_D, 4, SPEC>), g, b, sm, st, kp);
+  if (rpl == 1) launch_one<1, SPEC>(g, b, sm, st, kp);
+  else if (rpl == 2) launch_one<2, SPEC>(g, b, sm, st, kp);
+  else if (rpl == 4) launch_one<4, SPEC>(g, b, sm, st, kp);
+  else launch_one<8, SPEC>(g, b, sm, st, kp);
 }
 
 void MRBO_CAT(launch_rollout_d, MRBO_D)(int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st,
@@ -42,15 +59,28 @@ void MRBO_CAT(launch_rollout_d, MRBO_D)(int rpl, int spec, dim3 g, dim3 b, size_
   else launch_rollout_spec<0>(rpl, g, b, sm, st, kp);
 }
 
+template <int RPL>
+static void launch_tables_one(int nstarts, hipStream_t st, const KParams& kp) {
+  if constexpr (has_rpl(MRBO_D, RPL))
+    hipLaunchKernelGGL((start_tables_kernel<MRBO_D, RPL>), dim3(nstarts), dim3(WAVE), 0, st, kp);
+}
+
 void MRBO_CAT(launch_tables_d, MRBO_D)(int rpl, int nstarts, hipStream_t st, const KParams& kp) {
-  if (rpl == 2) hipLaunchKernelGGL((start_tables_kernel<MRBO_D, 2>), dim3(nstarts), dim3(WAVE), 0, st, kp);
-  else if (rpl == 4) hipLaunchKernelGGL((start_tables_kernel<MRBO_D, 4>), dim3(nstarts), dim3(WAVE), 0, st, kp);
+  if (rpl == 2) launch_tables_one<2>(nstarts, st, kp);
+  else if (rpl == 4) launch_tables_one<4>(nstarts, st, kp);
+  else if (rpl == 8) launch_tables_one<8>(nstarts, st, kp);
+}
+
+template <int RPL>
+static void launch_evalb_one(dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
+  if constexpr (has_rpl(MRBO_D, RPL)) hipLaunchKernelGGL((eval_base_kernel<MRBO_D, RPL>), g, b, sm, st, kp);
 }
 
 void MRBO_CAT(launch_evalb_d, MRBO_D)(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
-  if (rpl == 1) hipLaunchKernelGGL((eval_base_kernel<MRBO_D, 1>), g, b, sm, st, kp);
-  else if (rpl == 2) hipLaunchKernelGGL((eval_base_kernel<MRBO_D, 2>), g, b, sm, st, kp);
-  else hipLaunchKernelGGL((eval_base_kernel<MRBO_D, 4>), g, b, sm, st, kp);
+  if (rpl == 1) launch_evalb_one<1>(g, b, sm, st, kp);
+  else if (rpl == 2) launch_evalb_one<2>(g, b, sm, st, kp);
+  else if (rpl == 4) launch_evalb_one<4>(g, b, sm, st, kp);
+  else launch_evalb_one<8>(g, b, sm, st, kp);
 }
 
 }  // namespace mrbo

@@ -54,8 +54,9 @@ struct Lay {
   static constexpr int REDN = ((REDN_A > REDN_B ? REDN_A : REDN_B) + 1) & ~1;
   // lane-uniform LDS area (doubles)
   static constexpr int U_X = 0;                          // eval point            D
-  static constexpr int U_XB = U_X + 8;                   // best multistart point D
-  static constexpr int U_XF = U_XB + 8;                  // fantasy points        FMAX*D
+  static constexpr int DE = (D + 1) & ~1;               // D rounded up to an even count
+  static constexpr int U_XB = U_X + (DE > 8 ? DE : 8);   // best multistart point D
+  static constexpr int U_XF = U_XB + (DE > 8 ? DE : 8);  // fantasy points        FMAX*D
   static constexpr int U_YF = U_XF + FMAX * D;           // fantasy observations  FMAX
   static constexpr int U_GF = U_YF + FMAX;               // sampled gradients     FMAX*D
   static constexpr int U_DINV = U_GF + FMAX * D;         // Dinv row-major        FMAX*FMAX
@@ -221,8 +222,23 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 
 // acc[c] += Σ_{j < nrows} L(j) v[c](j) with L(j) = lbase[j · JSTRIDE] (zero-padded past N).
 // Blocks run in the order 0, 2, 1, 3 (two swaps yield blocks p and p+2 together).
+// Column chunks of at most 8 (the generated asm statements cover K ≤ 9; d > 8 runs 2-3 chunks,
+// each re-reading this lane's L0⁻¹ entries)
+template <int K>
+__device__ __forceinline__ double (&head8(double (&a)[K]))[8] { return *reinterpret_cast<double(*)[8]>(&a[0]); }
+template <int K>
+__device__ __forceinline__ double (&tail8(double (&a)[K]))[K - 8] { return *reinterpret_cast<double(*)[K - 8]>(&a[8]); }
+template <int K>
+__device__ __forceinline__ const double (&head8(const double (&a)[K]))[8] {
+  return *reinterpret_cast<const double(*)[8]>(&a[0]);
+}
+template <int K>
+__device__ __forceinline__ const double (&tail8(const double (&a)[K]))[K - 8] {
+  return *reinterpret_cast<const double(*)[K - 8]>(&a[8]);
+}
+
 template <int K, int JSTRIDE>
-__device__ __forceinline__ void bcast_product(double (&acc)[K], const double (&v)[K], const double* lbase, int nrows) {
+__device__ __forceinline__ void bcast_product_k(double (&acc)[K], const double (&v)[K], const double* lbase, int nrows) {
   const unsigned a0 = lds_addr(lbase);
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
@@ -238,11 +254,21 @@ __device__ __forceinline__ void bcast_product(double (&acc)[K], const double (&v
   }
 }
 
+template <int K, int JSTRIDE>
+__device__ __forceinline__ void bcast_product(double (&acc)[K], const double (&v)[K], const double* lbase, int nrows) {
+  if constexpr (K > 9) {
+    bcast_product<8, JSTRIDE>(head8(acc), head8(v), lbase, nrows);
+    bcast_product<K - 8, JSTRIDE>(tail8(acc), tail8(v), lbase, nrows);
+  } else {
+    bcast_product_k<K, JSTRIDE>(acc, v, lbase, nrows);
+  }
+}
+
 // The same product with this lane's L entries from global memory (L2-resident image):
 // step n of the block at lb[n·64].  All 64 steps of both row blocks of a pass are loaded into
 // registers before their FMAs (the image is zero-padded, so the loads need no bounds).
 template <int K>
-__device__ __forceinline__ void gl_bcast_product(double (&acc)[K], const double (&v)[K], const double* lb, int nrows) {
+__device__ __forceinline__ void gl_bcast_product_k(double (&acc)[K], const double (&v)[K], const double* lb, int nrows) {
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     if (16 * p >= nrows) break;
@@ -266,6 +292,16 @@ __device__ __forceinline__ void gl_bcast_product(double (&acc)[K], const double 
       BcastRegAsm<K, 0>::run(acc, bp2, l[2]);
       BcastRegAsm<K, 8>::run(acc, bp2, l[3]);
     }
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void gl_bcast_product(double (&acc)[K], const double (&v)[K], const double* lb, int nrows) {
+  if constexpr (K > 9) {
+    gl_bcast_product<8>(head8(acc), head8(v), lb, nrows);
+    gl_bcast_product<K - 8>(tail8(acc), tail8(v), lb, nrows);
+  } else {
+    gl_bcast_product_k<K>(acc, v, lb, nrows);
   }
 }
 
@@ -577,32 +613,41 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   if (all_cols) {
   {
     const int ncol = D;
-    if (lane < nf * ncol) {
-      const int r = lane / ncol, c = 1 + lane % ncol;
+    // entry t = (r, c) per lane; d > 10 has more entries than lanes: lane, lane + 64, …
+    for (int t = lane; t < (FMAX * D <= WAVE ? WAVE : FMAX * D); t += WAVE) {
+      if (t >= nf * ncol) break;
+      const int r = t / ncol, c = 1 + t % ncol;
       double y = red[Ly::R_MF + D + r * D + (c - 1)];
       for (int q = 0; q <= r; ++q) y = fma(U[Ly::U_DINV + r * FMAX + q], B[(Ly::FR0 + q) * BS + c], y);
       U[Ly::U_YFV + r * D1 + c] = y;
+      if constexpr (FMAX * D <= WAVE) break;
     }
   }
   wave_sync();
   // ---- Gram (incl. fantasy rows) and ∇μ  (lanes own entries; G00 and μ above)
   {
-    const int ng = Ly::NG;
-    if (lane > 0 && lane < ng) {
-      int a = 0, rem = lane;
+    auto gram_entry = [&](int t) {
+      int a = 0, rem = t;
 #pragma unroll
       for (int aa = 0; aa < D1; ++aa) if (a == aa && rem >= D1 - aa) { rem -= D1 - aa; a = aa + 1; }
       const int b = a + rem;
-      double g = (mode == EV_GSTART) ? W.GTAB[kst * Ly::NG + lane] : red[Ly::R_G + lane - 1];
+      double g = (mode == EV_GSTART) ? W.GTAB[kst * Ly::NG + t] : red[Ly::R_G + t - 1];
       for (int r = 0; r < nf; ++r) g = fma(U[Ly::U_YFV + r * D1 + a], U[Ly::U_YFV + r * D1 + b], g);
       U[Ly::U_G + a * D1 + b] = g;
       U[Ly::U_G + b * D1 + a] = g;
-    }
-    if (lane >= 49 && lane < 48 + D1) {
-      const int c = lane - 48;
+    };
+    auto gmu_entry = [&](int c) {   // c = 1..D
       double mu = red[Ly::R_MF + c - 1];
       for (int r = 0; r < nf; ++r) mu = fma(U[Ly::U_CF + (S + 1) * FMAX + r], B[(Ly::FR0 + r) * BS + c], mu);
       U[Ly::U_GMU + c - 1] = mu;
+    };
+    if constexpr (Ly::NG <= 49) {   // d ≤ 8: Gram entries on lanes 1..NG-1, ∇μ on lanes 49..48+d
+      if (lane > 0 && lane < Ly::NG) gram_entry(lane);
+      if (lane >= 49 && lane < 48 + D1) gmu_entry(lane - 48);
+    } else {                        // wider: both as lane-strided loops
+      for (int t = lane; t < Ly::NG; t += WAVE)
+        if (t > 0) gram_entry(t);
+      if (lane >= 1 && lane <= D) gmu_entry(lane);
     }
   }
   wave_sync();
@@ -776,11 +821,13 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   // w_f[q] = Σ_{r ≥ q} Dinv[r][q] Yf[r][0]  (and P_f)
   {
     const int ncol = rich ? D1 : 1;
-    if (lane < nf * ncol) {
-      const int q = lane / ncol, c = lane % ncol;
+    for (int e = lane; e < (FMAX * D1 <= WAVE ? WAVE : FMAX * D1); e += WAVE) {   // d > 9: lane-strided
+      if (e >= nf * ncol) break;
+      const int q = e / ncol, c = e % ncol;
       double t = 0.0;
       for (int r = q; r < nf; ++r) t = fma(U[Ly::U_DINV + r * FMAX + q], U[Ly::U_YFV + r * D1 + c], t);
       if (c == 0) U[Ly::U_WF + q] = t; else U[Ly::U_PF + q * D + c - 1] = t;
+      if constexpr (FMAX * D1 <= WAVE) break;
     }
   }
   if (mode == EV_DRAW) { wave_sync(); STAMP(W, 5); return; }
@@ -825,15 +872,16 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   }
   wave_sync();
   STAMP(W, 6);
-  if (lane < Ly::NH) {
-    int a = 0, rem = lane;
+  for (int he = lane; he < (Ly::NH <= WAVE ? WAVE : Ly::NH); he += WAVE) {   // d > 10: lane-strided
+    if (he >= Ly::NH) break;
+    int a = 0, rem = he;
 #pragma unroll
     for (int aa = 0; aa < D; ++aa) if (a == aa && rem >= D - aa) { rem -= D - aa; a = aa + 1; }
     const int b = a + rem;
     const double gma = U[Ly::U_GMU + a], gmb = U[Ly::U_GMU + b];
     const double gsa = U[Ly::U_GSIG + a], gsb = U[Ly::U_GSIG + b];
     const double rdiag = red[Ly::NH];
-    double hv = red[lane] + ((a == b) ? rdiag : 0.0);
+    double hv = red[he] + ((a == b) ? rdiag : 0.0);
     // fantasy data points ([x − X_r, g1, g2] from phase 1)
     for (int r = 0; r < nf; ++r) {
       const double* hf = U + Ly::U_HF + r * (D + 2);
@@ -851,6 +899,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     }
     U[Ly::U_H + a * D + b] = hv;
     U[Ly::U_H + b * D + a] = hv;
+    if constexpr (Ly::NH <= WAVE) break;
   }
   wave_sync();
   STAMP(W, 7);
@@ -1400,7 +1449,7 @@ __device__ __forceinline__ void stage_start_tables(const KParams& kp, double* sm
       wave_reduce<16>(gv, red + 16 * ch, lane);
     }
     wave_sync();
-    if (lane < Ly::NG) smem[tb.gtab + (long long)k * Ly::NG + lane] = red[lane];
+    for (int t = lane; t < Ly::NG; t += WAVE) smem[tb.gtab + (long long)k * Ly::NG + t] = red[t];
     wave_sync();
   }
   __syncthreads();
@@ -2104,12 +2153,14 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
 // ================================================================================
 // Kernels
 // ================================================================================
-// launch bounds: 2 waves per SIMD (256 VGPRs each) up to N = 128; the N ≤ 256 variant runs one
-// wave per SIMD, whose 512-entry register file (256 VGPRs + 256 AGPRs) holds the four-row state
-template <int RPL>
+// launch bounds: 2 waves per SIMD (256 VGPRs each) up to N = 128 at d ≤ 8; the N > 128 layouts
+// and d > 8 run one wave per SIMD, whose 512-entry register file (256 VGPRs + 256 AGPRs) holds the
+// multi-row / wide state (N ≤ 512 and d ≤ 16 compile, with scratch spills: coverage, not speed)
+template <int D, int RPL>
 struct KBounds {
-  static constexpr int threads = RPL > 2 ? 256 : 512;
-  static constexpr int waves_per_simd = RPL > 2 ? MRBO_WAVES_PER_SIMD_GL : MRBO_WAVES_PER_SIMD;
+  static constexpr bool WIDE = (RPL > 2) || (D > 8);
+  static constexpr int threads = WIDE ? 256 : 512;
+  static constexpr int waves_per_simd = WIDE ? MRBO_WAVES_PER_SIMD_GL : MRBO_WAVES_PER_SIMD;
 };
 
 template <int D, int RPL>
@@ -2154,7 +2205,7 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
 // which frees registers in the whole trajectory (VGPR spills 94 -> 33 at d = 6).  SPEC = 0
 // reads both from the launch parameters.
 template <int D, int RPL, int SPEC>
-__global__ void __launch_bounds__(KBounds<RPL>::threads, KBounds<RPL>::waves_per_simd) rollout_kernel(KParams kp_in) {
+__global__ void __launch_bounds__((KBounds<D, RPL>::threads), (KBounds<D, RPL>::waves_per_simd)) rollout_kernel(KParams kp_in) {
   KParams kp = kp_in;   // a local copy: the fixed fields below propagate as constants
   if constexpr (SPEC == 1) {
     kp.kernel = KERNEL_MATERN52;
@@ -2269,12 +2320,12 @@ __global__ void __launch_bounds__(WAVE) start_tables_kernel(KParams kp) {
     wave_reduce<16>(gv, red + 16 * ch, lane);
   }
   __syncthreads();
-  if (lane < Ly::NG) kp.gtab_g[(long long)k * Ly::NG + lane] = red[lane];
+  for (int t = lane; t < Ly::NG; t += WAVE) kp.gtab_g[(long long)k * Ly::NG + t] = red[t];
 }
 
 // eval(s, x, θ) on the base surrogate for P points (fixture / primitive parity path)
 template <int D, int RPL>
-__global__ void __launch_bounds__(KBounds<RPL>::threads, KBounds<RPL>::waves_per_simd) eval_base_kernel(KParams kp) {
+__global__ void __launch_bounds__((KBounds<D, RPL>::threads), (KBounds<D, RPL>::waves_per_simd)) eval_base_kernel(KParams kp) {
   using Ly = Lay<D, RPL>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   for (int q = threadIdx.x; q < (int)Ly::LINV_DOUBLES; q += blockDim.x) smem[q] = kp.Linv[q];

@@ -215,11 +215,14 @@ def test_other_kernels_replay_vs_oracle(gpu, oracle, kernel, kid):
 
 
 @pytest.mark.parametrize("d,N,h", [(1, 12, 2), (3, 24, 2), (4, 40, 3), (5, 30, 2), (7, 48, 2), (8, 64, 3), (3, 96, 2),
-                                   (6, 128, 4), (3, 150, 2), (5, 200, 5), (8, 256, 3)])
+                                   (6, 128, 4), (3, 150, 2), (5, 200, 5), (8, 256, 3),
+                                   (9, 20, 2), (10, 24, 3), (12, 60, 2), (16, 24, 2), (16, 100, 2),
+                                   (4, 300, 2), (6, 384, 2), (8, 512, 2)])
 def test_dimensions_and_sizes_replay_vs_oracle(gpu, oracle, d, N, h):
-    """d = 1..8 and N up to 256 on Ackley(d): one data row per lane (N ≤ 64, L0⁻¹ square in
-    LDS), two (N ≤ 128, three square 64×64 blocks in LDS), four (N ≤ 256, L0⁻¹ in global memory);
-    ragged N.  The
+    """d = 1..16 and N up to 512 on Ackley(d): one data row per lane (N ≤ 64, L0⁻¹ square in
+    LDS), two (N ≤ 128, three square 64×64 blocks in LDS), four or eight (N ≤ 256 / 512, L0⁻¹ in
+    global memory); d > 8 up to N = 128 (the reference's 10-D / 16-D experiments run budgets of
+    15, experiments/archived/dimensions-timing/nonmyopic_bayesopt/metadata.txt); ragged N.  The
     lengthscale tracks the design spacing (0.6 · width · N^(-1/d)) so that K is dense: with ℓ = 1
     on Ackley's 65-wide box K ≈ I and the triangular products would multiply zeros."""
     ell = 0.6 * 65.536 * N ** (-1.0 / d)

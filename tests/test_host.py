@@ -40,22 +40,24 @@ def test_library_dual_uniform_bit_identical_to_oracle(oracle):
         assert dual_uniform(1906, t, j, k) == oracle.dual_uniform(1906, t, j, k)
 
 
-def test_plan_create_rejects_unsupported_shapes():
-    """Argument errors come back as negative codes with a message (no exception inside C)."""
+@pytest.mark.parametrize("d,N,msg", [(17, 4, b"d=17"), (9, 129, b"N=129"), (4, 513, b"N=513")])
+def test_plan_create_rejects_unsupported_shapes(d, N, msg):
+    """Argument errors come back as negative codes with a message (no exception inside C), before
+    any device call: d ≤ 16, N ≤ 512, and N ≤ 128 when d > 8 are compiled."""
     from mrbo import _lib
     L = _lib.load()
     dp = ctypes.POINTER(ctypes.c_double)
-    X = np.zeros((9, 4), order="F")
-    Lm = np.eye(4, order="F")
-    c = np.zeros(4)
-    sd = _lib.SurrogateDesc(9, 4, 0, 1.0, 1e-6, 0.0, X.ctypes.data_as(dp), Lm.ctypes.data_as(dp), 4,
+    X = np.zeros((d, N), order="F")
+    Lm = np.eye(N, order="F")
+    c = np.zeros(N)
+    sd = _lib.SurrogateDesc(d, N, 0, 1.0, 1e-6, 0.0, X.ctypes.data_as(dp), Lm.ctypes.data_as(dp), N,
                             c.ctypes.data_as(dp), c.ctypes.data_as(dp))
-    lb = np.zeros(9)
+    lb = np.zeros(d)
     pd = _lib.ParamsDesc(3, 8, 2, 18, 0, 0.0, lb.ctypes.data_as(dp), lb.ctypes.data_as(dp), 50, 20, 1e-3, 1e-3,
                          1e-8, 1e-4, 1e-8, 1906, 0, 0)
     h = ctypes.c_void_p()
     rc = L.mrbo_plan_create(ctypes.byref(sd), ctypes.byref(pd), 0, ctypes.byref(h))
-    assert rc == -2 and b"d=9" in L.mrbo_last_error()
+    assert rc == -2 and msg in L.mrbo_last_error()
 
 
 def test_kronecker_matches_oracle(oracle):
