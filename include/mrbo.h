@@ -40,7 +40,8 @@ extern "C" {
 typedef enum {
   MRBO_OK = 0,
   MRBO_ERR_ARG = -1,      /* invalid argument (dimension, size, null pointer)            */
-  MRBO_ERR_UNSUPPORTED = -2, /* shape outside the compiled kernels (d > 8, N > 256, h > 5) */
+  MRBO_ERR_UNSUPPORTED = -2, /* shape outside the compiled kernels: d > 16, N > 512,
+                                d > 8 with N > 128, h > 5 (gp_fit: N > 256) */
   MRBO_ERR_HIP = -3,      /* HIP runtime error                                          */
   MRBO_ERR_NOMEM = -4
 } mrbo_err_t;

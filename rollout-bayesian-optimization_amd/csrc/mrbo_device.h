@@ -270,6 +270,38 @@ __device__ __attribute__((noinline)) double xexp(double x) { return exp(x); }
 __device__ __attribute__((noinline)) double xerfc(double x) { return erfc(x); }
 #endif
 
+// √s and 1/√s (s > 0) from one hardware reciprocal square root and two Newton–Raphson steps
+// y ← y(1.5 − ½s·y²): ~1 ulp, and a much shorter dependent chain than a correctly rounded
+// sqrt followed by an IEEE division (Cholesky pivots of the Newton step and of gp_draw).
+__device__ __forceinline__ void sqrt_rsqrt(double s, double& r, double& ir) {
+  const double h = 0.5 * s;
+  double y = __builtin_amdgcn_rsq(s);
+  y = fma(y, fma(-h * y, y, 0.5), y);
+  y = fma(y, fma(-h * y, y, 0.5), y);
+  ir = y;
+  r = s * y;
+}
+
+// √s for s ≥ 0 (sums of squares) from sqrt_rsqrt: ~8 dependent operations instead of the IEEE
+// expansion's ~14, within 2 ulp.  s ≤ 1e-290 (zero, subnormal) gives 0 and NaN stays NaN; the
+// Matérn-5/2 forms and the certificates absorb a subnormal's root exactly (1 + 1e-145 = 1).
+__device__ __forceinline__ double fast_sqrt0(double s) {
+  double r, ir;
+  sqrt_rsqrt(s, r, ir);
+  return s > 1e-290 ? r : s * 0.0;
+}
+
+// σ = √var and 1/σ of a posterior variance: sqrt_rsqrt where var is a normal positive number,
+// the IEEE root and division otherwise (σ = 0 → 1/σ = inf, var < 0 or NaN → NaN, as Julia)
+__device__ __forceinline__ void sig_isig(double var, double& sig, double& isig) {
+  if (var > 1e-290 && var < 1e290) {
+    sqrt_rsqrt(var, sig, isig);
+  } else {
+    sig = sqrt(var);
+    isig = 1.0 / sig;
+  }
+}
+
 // ---- radial kernels (radial_basis_functions.jl:60-96; derivatives in closed form) -------
 // kind ids = mrbo_kernel_t (include/mrbo.h)
 enum { KERNEL_MATERN52 = 0, KERNEL_MATERN32 = 1, KERNEL_MATERN12 = 2, KERNEL_SE = 3, KERNEL_PERIODIC = 4 };
@@ -312,7 +344,7 @@ __device__ __forceinline__ void rad_eval(const Radial& k, double rho2, double& p
     g2 = c * c * e;
     return;
   }
-  const double rho = sqrt(rho2);
+  const double rho = (k.kind == 0) ? fast_sqrt0(rho2) : sqrt(rho2);
   const double s = c * rho, e = xexp(-s);
   if (k.kind == 0) {
     const double c23 = c * c * (1.0 / 3.0);
@@ -356,7 +388,7 @@ __device__ __forceinline__ void rad_eval2(const Radial& k, double rho2a, double 
     return;
   }
   const double c = k.cK, c23 = c * c * (1.0 / 3.0);
-  const double sa = c * sqrt(rho2a), sb = c * sqrt(rho2b);
+  const double sa = c * fast_sqrt0(rho2a), sb = c * fast_sqrt0(rho2b);
   const Exp2 e = xexp2(-sa, -sb);
   psia = fma(sa, fma(sa, 1.0 / 3.0, 1.0), 1.0) * e.a;
   g1a = -c23 * (1.0 + sa) * e.a;
@@ -444,7 +476,7 @@ struct EIp {
 __device__ __forceinline__ double rule_gth(int rule, double gmu, double sig) { return rule == 2 ? sig : gmu; }
 enum { RULE_EI = 0, RULE_POI = 1, RULE_LCB = 2 };
 __device__ __forceinline__ EIp rule_partials(int rule, double mu, double sig, double theta, double fmin,
-                                             double sigma_tol) {
+                                             double sigma_tol, double isig) {
   EIp e;
   if (rule == RULE_LCB) {
     e.g = theta * sig - mu;
@@ -459,7 +491,6 @@ __device__ __forceinline__ EIp rule_partials(int rule, double mu, double sig, do
     return e;
   }
   const double imp = fmin - mu - theta;
-  const double isig = 1.0 / sig;
   const double z = imp * isig;
   const PhiPair pp = ei_pp(z);
   const double phi = pp.phi, Phi = pp.Phi;
@@ -483,6 +514,10 @@ __device__ __forceinline__ EIp rule_partials(int rule, double mu, double sig, do
   e.gmuth = pis;
   e.gsigth = z * pis;
   return e;
+}
+__device__ __forceinline__ EIp rule_partials(int rule, double mu, double sig, double theta, double fmin,
+                                             double sigma_tol) {
+  return rule_partials(rule, mu, sig, theta, fmin, sigma_tol, 1.0 / sig);
 }
 // first partials only, at (μ', σ') -- the perturbation "second-order" coefficients (Q7, Q8)
 __device__ __forceinline__ void rule_first(int rule, double mu, double sig, double theta, double fmin, double sigma_tol,
@@ -538,18 +573,6 @@ __host__ __device__ __forceinline__ double dual_uniform(unsigned long long seed,
   key = splitmix64(key ^ (unsigned long long)traj);
   key = splitmix64(key ^ (((unsigned long long)(unsigned)j << 32) | (unsigned)k));
   return (double)(key >> 11) * (1.0 / 9007199254740992.0);
-}
-
-// √s and 1/√s (s > 0) from one hardware reciprocal square root and two Newton–Raphson steps
-// y ← y(1.5 − ½s·y²): ~1 ulp, and a much shorter dependent chain than a correctly rounded
-// sqrt followed by an IEEE division (Cholesky pivots of the Newton step and of gp_draw).
-__device__ __forceinline__ void sqrt_rsqrt(double s, double& r, double& ir) {
-  const double h = 0.5 * s;
-  double y = __builtin_amdgcn_rsq(s);
-  y = fma(y, fma(-h * y, y, 0.5), y);
-  y = fma(y, fma(-h * y, y, 0.5), y);
-  ir = y;
-  r = s * y;
 }
 
 // value of a double in lane k (wave-uniform k)

@@ -112,7 +112,8 @@ struct Lay {
 enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, SC_GSIG = 6, SC_GMUMU = 7,
        SC_GSIGSIG = 8, SC_GMUTH = 9, SC_GSIGTH = 10, SC_FMIN = 11, SC_ST = 12, SC_CABS = 13,
        // NonUniformCost (kp.cost): the rule value g before weighting, c(x), max_a |∂_a c(x)|
-       SC_ARAW = 14, SC_COSTC = 15, SC_GCMAX = 16 };
+       SC_ARAW = 14, SC_COSTC = 15, SC_GCMAX = 16,
+       SC_ISIG = 17 };   // 1/σ
 
 // ∂_lane c(x) by unrolled select (lane < D; a runtime index would put gc in scratch)
 template <int D>
@@ -655,14 +656,15 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   STAMP(W, 3);
 
   // ---- σ, EI partials (all lanes, wave-uniform values)
-  double sig_f;
+  double isig_f;
   EIp e_f;
   if (do_val) {
   const double mu = mu_v;
   const double var = kp.psi0 - g00_v;
-  const double sig = sqrt(var);
+  double sig, isig;
+  sig_isig(var, sig, isig);
   const double fmin = U[Ly::U_FMIN + S + 1];
-  const EIp e = rule_partials(kp.rule, mu, sig, kp.theta, fmin, kp.sigma_tol);
+  const EIp e = rule_partials(kp.rule, mu, sig, kp.theta, fmin, kp.sigma_tol, isig);
   double alpha = e.g;
   if (kp.cost) {   // cost-weighted rule f = α/c(x) (NonUniformCost, cost_functions.jl:5-20)
     double gc[D];
@@ -679,6 +681,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   }
   if (lane == 0) {
     U[Ly::U_SC + SC_SIG] = sig;
+    U[Ly::U_SC + SC_ISIG] = isig;
     U[Ly::U_SC + SC_VAR] = var;
     U[Ly::U_SC + SC_ALPHA] = alpha;
     U[Ly::U_SC + SC_GMU] = e.gmu;
@@ -690,17 +693,17 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     U[Ly::U_SC + SC_FMIN] = fmin;
   }
   if (mode == EV_VALUE) { wave_sync(); STAMP(W, 4); return; }
-  sig_f = sig;
+  isig_f = isig;
   e_f = e;
   } else {   // GRADC: σ and the EI partials of the VALUE pass at this point
-    sig_f = U[Ly::U_SC + SC_SIG];
+    isig_f = U[Ly::U_SC + SC_ISIG];
     e_f.gmu = U[Ly::U_SC + SC_GMU];
     e_f.gsig = U[Ly::U_SC + SC_GSIG];
     e_f.gmuth = U[Ly::U_SC + SC_GMUTH];
     e_f.gsigth = U[Ly::U_SC + SC_GSIGTH];
   }
   if (lane < D) {
-    const double gs = -U[Ly::U_G + (1 + lane) * D1] * (1.0 / sig_f);  // ∇σ = -(∇kx·w)/σ
+    const double gs = -U[Ly::U_G + (1 + lane) * D1] * isig_f;  // ∇σ = -(∇kx·w)/σ
     const double gm = U[Ly::U_GMU + lane];
     U[Ly::U_GSIG + lane] = gs;
     double gal = e_f.gmu * gm + e_f.gsig * gs;                         // ∇αx :567
@@ -711,7 +714,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       const double gca = lane_pick<D>(gc, lane);
       const double c = U[Ly::U_SC + SC_COSTC], araw = U[Ly::U_SC + SC_ARAW];
       gal = gal / c - (araw / (c * c)) * gca;
-      mix = mix / c - rule_gth(kp.rule, e_f.gmu, sig_f) * gca / (c * c);
+      mix = mix / c - rule_gth(kp.rule, e_f.gmu, U[Ly::U_SC + SC_SIG]) * gca / (c * c);
     }
     U[Ly::U_GAL + lane] = gal;
     U[Ly::U_MIX + lane] = mix;
@@ -726,7 +729,6 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     for (int s = 0; s < RPL; ++s) acc[s][0] = W.G12[3 * (lane + WAVE * s) + 2];
   }
   wave_sync();   // U_SC / gradients of the front part visible to all lanes
-  const double sig = U[Ly::U_SC + SC_SIG];
   EIp e;
   e.gmu = U[Ly::U_SC + SC_GMU];
   e.gsig = U[Ly::U_SC + SC_GSIG];
@@ -835,7 +837,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
 
   // ---- 6. Hessian  Hα = gμμ∇μ∇μ' + gσσ∇σ∇σ' − (gσ/σ)(∇σ∇σ' + ∇kx·Dw) + Σ_j coef_j Hk_j
   // Σ_i coef_i ∇²k(x − X_i) with ∇²k = g2·r rᵀ + g1·I (g1, g2 kept from phase 1)
-  const double gsig_over = (e.gsig == 0.0) ? 0.0 : e.gsig * (1.0 / sig);
+  const double gsig_over = (e.gsig == 0.0) ? 0.0 : e.gsig * U[Ly::U_SC + SC_ISIG];
   {
     double nv[RPL][D], ca[RPL], tb[RPL];
 #pragma unroll
@@ -1188,8 +1190,8 @@ __device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const K
   using Ly = Lay<D, RPL>;
   const double* U = W.U;
   const double gm = U[Ly::U_SC + SC_GMU], gs = U[Ly::U_SC + SC_GSIG];
-  const double cabs = U[Ly::U_SC + SC_CABS], sig = U[Ly::U_SC + SC_SIG];   // unconditional loads
-  double bound = fabs(gm) * kp.gcert_mu * cabs + fabs(gs) * kp.gcert_sig / sig;
+  const double cabs = U[Ly::U_SC + SC_CABS], isig = U[Ly::U_SC + SC_ISIG];   // unconditional loads
+  double bound = fabs(gm) * kp.gcert_mu * cabs + fabs(gs) * kp.gcert_sig * isig;
   bool zero = (gm == 0.0) & (gs == 0.0);
   if (kp.cost) {   // f = α/c: |∂f| ≤ B/c + |α| max|∇c|/c²; gμ = gσ = 0 certifies only where α = 0
     const double araw = U[Ly::U_SC + SC_ARAW], c = U[Ly::U_SC + SC_COSTC];
@@ -1213,7 +1215,7 @@ __device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const K
 // With a cost model (f = α/c, araw = α at x) every bound B on |∂α| becomes B/c + |α| max|∇c|/c².
 template <int D, int RPL, bool ROWS_KEPT = false>
 __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParams& kp, int S, double gm, double gs,
-                                                double sig, double araw = 0.0) {
+                                                double sig, double isig, double araw = 0.0) {
   using Ly = Lay<D, RPL>;
   constexpr int NR = Ly::NR;
   const double* U = W.U;
@@ -1235,7 +1237,7 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParam
   // cheap μ part (Σ|c|·max|ψ'| ≥ the row sum) it may already pass -- same decisions as the
   // full test, without the row pass
   const double q = fmax(kp.psi0 - sig * sig, 0.0);
-  const double bsig = fabs(gs) * kp.gcert_d2 * sqrt(q) / sig, thr = 0.25 * kp.g_tol;
+  const double bsig = fabs(gs) * kp.gcert_d2 * fast_sqrt0(q) * isig, thr = 0.25 * kp.g_tol;
   if (!(bsig * isc + add <= thr)) return false;
   if ((fabs(gm) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + bsig) * isc + add <= thr) return true;
   double x[D];
@@ -1251,7 +1253,7 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParam
     if constexpr (ROWS_KEPT) g1 = W.G12[3 * (lane + WAVE * s)];
     else rad_eval(W.rad, rho2, psi, g1, g2);
     const double cb = W.C[(long long)(S + 1) * NR + lane + WAVE * s];
-    v[0] += W.valid[s] ? fabs(cb) * fabs(g1) * sqrt(rho2) : 0.0;
+    v[0] += W.valid[s] ? fabs(cb) * fabs(g1) * fast_sqrt0(rho2) : 0.0;
   }
   if (lane < nf) {
     double rho2 = 0.0;
@@ -1260,7 +1262,7 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParam
     double psi, g1, g2;
     if constexpr (ROWS_KEPT) g1 = U[Ly::U_HF + lane * (D + 2) + D];
     else rad_eval(W.rad, rho2, psi, g1, g2);
-    v[0] += fabs(U[Ly::U_CF + (S + 1) * FMAX + lane]) * fabs(g1) * sqrt(rho2);
+    v[0] += fabs(U[Ly::U_CF + (S + 1) * FMAX + lane]) * fabs(g1) * fast_sqrt0(rho2);
   }
   wave_sync();
   wave_reduce<1>(v, W.red, lane);
@@ -1293,7 +1295,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
   wave_sync();
   // a batched start whose cheap certificate failed: the tight one at x_start (gμ, gσ, σ of the
   // batched value) before any gradient work
-  if (have_f0 && kp.gcert_sig > 0.0 && tight_certified<D, RPL>(W, kp, S, gm0, gs0, sig0, a0)) {
+  if (have_f0 && kp.gcert_sig > 0.0 && tight_certified<D, RPL>(W, kp, S, gm0, gs0, sig0, 1.0 / sig0, a0)) {
     wave_sync();
     return f0;
   }
@@ -1365,7 +1367,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
     if (grad_certified<D, RPL>(W, kp)) break;     // ‖∇α‖ ≤ g_tol guaranteed: stationary
     if (kp.gcert_sig > 0.0 &&
         tight_certified<D, RPL, true>(W, kp, S, U[Ly::U_SC + SC_GMU], U[Ly::U_SC + SC_GSIG], U[Ly::U_SC + SC_SIG],
-                                      kp.cost ? U[Ly::U_SC + SC_ARAW] : 0.0))
+                                      U[Ly::U_SC + SC_ISIG], kp.cost ? U[Ly::U_SC + SC_ARAW] : 0.0))
       break;
     STAMP(W, 12);
     phase = P_GRAD;
@@ -1620,8 +1622,9 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
     }
   }
   const double var = kp.psi0 - g00;
-  const double sig = sqrt(var);
-  const EIp e = rule_partials(kp.rule, mu, sig, kp.theta, U[Ly::U_FMIN + S + 1], kp.sigma_tol);
+  double sig, isig;
+  sig_isig(var, sig, isig);
+  const EIp e = rule_partials(kp.rule, mu, sig, kp.theta, U[Ly::U_FMIN + S + 1], kp.sigma_tol, isig);
   double fval = e.g, cval = 1.0, gcm = 0.0;
   if (kp.cost) {   // cost-weighted rule at the start point (see grad_certified)
     double gc[D];
@@ -1632,7 +1635,7 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   }
   bool cert = (e.gmu == 0.0 && e.gsig == 0.0) && (!kp.cost || e.g == 0.0);
   if (!cert && kp.gcert_sig > 0.0) {
-    double b = fabs(e.gmu) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + fabs(e.gsig) * kp.gcert_sig / sig;
+    double b = fabs(e.gmu) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + fabs(e.gsig) * kp.gcert_sig * isig;
     if (kp.cost) b = b * (1.0 / cval) + fabs(e.g) * gcm / (cval * cval);
     cert = b <= 0.25 * kp.g_tol;
   }
@@ -1853,11 +1856,10 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
   }
   const double cq = U[Ly::U_CF + (S + 1) * FMAX + q];
   const double wq = U[Ly::U_WF + q];
-  const double sig = U[Ly::U_SC + SC_SIG];
   const double gmu = U[Ly::U_SC + SC_GMU], gsig = U[Ly::U_SC + SC_GSIG];
   const double kxdc = -(wq * udc + udw * cq);
   const double dmu = dkx * cq + kxdc;
-  const double isig = 1.0 / sig;
+  const double isig = U[Ly::U_SC + SC_ISIG];
   const double dsig = wq * (udw - dkx) * isig;
   double dgm, dgs;
   rule_first(kp.rule, dmu, dsig, kp.theta, U[Ly::U_SC + SC_FMIN], kp.sigma_tol, dgm, dgs);

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Extract the reference's recorded BO gap curves into tests/golden/bo_ref_gaps.json.
+
+Data only: the per-trial `gaps` rows the reference's experiment drivers wrote (create_csv /
+write_to_csv, utils.jl:155-172; gap = (initial_best − observed_best)/(initial_best − f*), utils.jl
+`gap`), for the cases tools/bo_compare.py runs against the MI355X BO loop (mrbo/bayesopt.py):
+
+  myopic_<fn>_ei     experiments/myopic/<fn>/ei_gaps.csv (myopic_bayesopt.jl: EI multistart
+                     solve, 64 starts, 5 initial points, budget 100, 60 trials, optimize!)
+  rollout_h<h>_<fn>  experiments/archived/nonmyopic-shortrun-gaps-and-time/nonmyopic_bayesopt/
+                     <fn>/rollout_h<h>_gaps.csv (an earlier nonmyopic_bayesopt.jl: rollout
+                     acquisition, 8 starts, batch 8, 100 MC samples, 50 SGD iterations, budget 20,
+                     60 trials, optimize!; header columns 0..20)
+
+Each case keeps the header (the budget labels) and the trial rows (the −1.0 placeholder row of
+create_csv dropped).  Run here, where /root/reference exists; the JSON travels with the repo.
+usage: python tests/golden/make_bo_ref.py [--reference /root/reference]
+"""
+import argparse
+import csv
+import json
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+CASES = {
+    "myopic_braninhoo_ei": "experiments/myopic/braninhoo/ei_gaps.csv",
+    "myopic_hartmann6d_ei": "experiments/myopic/hartmann6d/ei_gaps.csv",
+    "rollout_h0_braninhoo": "experiments/archived/nonmyopic-shortrun-gaps-and-time/nonmyopic_bayesopt/braninhoo/rollout_h0_gaps.csv",
+    "rollout_h1_braninhoo": "experiments/archived/nonmyopic-shortrun-gaps-and-time/nonmyopic_bayesopt/braninhoo/rollout_h1_gaps.csv",
+    "rollout_h0_gramacylee": "experiments/archived/nonmyopic-shortrun-gaps-and-time/nonmyopic_bayesopt/gramacylee/rollout_h0_gaps.csv",
+    "rollout_h1_gramacylee": "experiments/archived/nonmyopic-shortrun-gaps-and-time/nonmyopic_bayesopt/gramacylee/rollout_h1_gaps.csv",
+}
+
+
+def read_gaps(path):
+    rows = list(csv.reader(open(path)))
+    header = rows[0][1:]
+    trials = []
+    for r in rows[1:]:
+        v = [float(x) for x in r]
+        if all(x == -1.0 for x in v):          # create_csv's placeholder row
+            continue
+        trials.append(v[-len(header):])        # rows carry the budget values (some a leading trial id)
+    return header, trials
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reference", default="/root/reference")
+    a = ap.parse_args()
+    out = {}
+    for key, rel in CASES.items():
+        header, trials = read_gaps(os.path.join(a.reference, rel))
+        out[key] = {"source": rel, "budget_labels": header, "gaps": trials}
+    with open(os.path.join(HERE, "bo_ref_gaps.json"), "w") as f:
+        json.dump(out, f, separators=(",", ":"))
+    for k, v in out.items():
+        print(k, len(v["gaps"]), "trials x", len(v["budget_labels"]))
+
+
+if __name__ == "__main__":
+    main()
