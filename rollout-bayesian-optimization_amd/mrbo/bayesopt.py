@@ -29,7 +29,7 @@ import numpy as np
 from . import testfns as T
 from .decision_rules import EI, LCB, POI
 from .kernels import Matern52
-from .optimizers import StandardSGA
+from .optimizers import Adam, StandardSGA
 from .rollout import simulate_trajectory_mc_batch
 from .surrogates import FantasySurrogate, Surrogate
 from .trajectory import Trajectory, TrajectoryParameters
@@ -76,16 +76,36 @@ def write_metadata(directory, budget, trials, starts):
 
 
 # ---- one acquisition solve -------------------------------------------------------------------
+class BoxAdam:
+    """Adam (optimizers.jl:25-74) on the box-normalised coordinates u = (x − lb)/(ub − lb), projected
+    onto the box after every step: a step of ≈ η box widths per coordinate whatever the scale of
+    the objective (StandardSGA's fixed η either stalls or throws restarts out of the box when the
+    acquisition's gradient is large, e.g. Branin's).  Build-defined: the reference's rollout solver
+    is undefined (experiments/adaptive_bayesopt.jl:490)."""
+
+    def __init__(self, lbs, ubs, η=0.02):
+        self.lbs, self.ubs = np.asarray(lbs, float), np.asarray(ubs, float)
+        self.w = self.ubs - self.lbs
+        self.adam = Adam(η=η)
+
+    def update(self, x, grad_f):
+        u = (x - self.lbs) / self.w
+        self.adam.update(u, np.asarray(grad_f, float) * self.w)
+        x[:] = np.clip(self.lbs + self.w * u, self.lbs, self.ubs)
+        return x
+
+
 def rollout_solve(sur, lbs, ubs, horizon, mc_samples, batch_size, starts, sgd_iterations, theta, eta=0.5,
-                  device=0):
-    """xnext from the rollout acquisition: SGA restarts from a Sobol batch, best final ETO mean."""
+                  device=0, solver="sga"):
+    """xnext from the rollout acquisition: restarts from a Sobol batch (StandardSGA with step `eta`,
+    or BoxAdam with `eta` box widths per step), best final ETO mean."""
     lbs, ubs = np.asarray(lbs, float), np.asarray(ubs, float)
     batch = generate_batch(batch_size, lbs, ubs)
     tp = TrajectoryParameters(start=batch[:, 0], hypers=[theta], horizon=horizon, mc_iterations=mc_samples,
                               use_low_discrepancy_sequence=True, spatial_lowerbounds=lbs, spatial_upperbounds=ubs)
     es = ExperimentSetup(tp, number_of_starts=starts)
     traj = Trajectory(sur, FantasySurrogate(sur, horizon), start=batch[:, 0], hypers=[theta], horizon=horizon)
-    opts = [StandardSGA(η=eta) for _ in range(batch.shape[1])]
+    opts = [StandardSGA(η=eta) if solver == "sga" else BoxAdam(lbs, ubs, η=eta) for _ in range(batch.shape[1])]
     x, _ = stochastic_solve_batch(opts, sur, tp, es, batch, T=traj, iterations=sgd_iterations, device=device)
     x = np.clip(x, lbs[:, None], ubs[:, None])
     etos = simulate_trajectory_mc_batch(traj, tp, x, es.get_starts(), with_gradient=False, device=device).etos(
@@ -98,20 +118,27 @@ def rollout_solve(sur, lbs, ubs, horizon, mc_samples, batch_size, starts, sgd_it
 
 # ---- the experiment loop (nonmyopic_bayesopt.jl:120-300) -------------------------------------
 def run(function_name, output_dir, budget=15, trials=60, starts=16, horizon=0, mc_samples=200, batch_size=8,
-        sgd_iterations=50, optimize=False, seed=1906, device=0, log=print):
+        sgd_iterations=50, optimize=False, seed=1906, device=0, log=print, rules=("ei", "poi", "lcb"), eta=0.5,
+        initial_observations=INITIAL_OBSERVATIONS, solver="sga", fmini_over_capacity=True):
+    """The experiment loop; `rules` selects a subset of the reference's three acquisitions (all by
+    default, as nonmyopic_bayesopt.jl), `eta` the StandardSGA step of the build-defined solver,
+    `initial_observations` the initial design size (5 in the current script, :131), `solver` "sga"
+    (StandardSGA, η = eta) or "adam" (BoxAdam, eta box widths per step); fmini_over_capacity=False
+    turns the reference's Q3 off (fmini over the observed points, not the zero-padded buffer)."""
     testfn = TESTFNS[function_name]()
     lbs, ubs = testfn.get_bounds()
     directory = os.path.join(output_dir, function_name)
     os.makedirs(directory, exist_ok=True)
-    acquisitions = [f"rollout_{horizon}_ei", f"rollout_{horizon}_poi", f"rollout_{horizon}_lcb"]
-    dr_hypers = [0.0, 0.0, 2.0]
-    rules = [EI(), POI(), LCB()]
+    table = {"ei": (EI(), 0.0), "poi": (POI(), 0.0), "lcb": (LCB(), 2.0)}
+    acquisitions = [f"rollout_{horizon}_{r}" for r in rules]
+    dr_hypers = [table[r][1] for r in rules]
+    rules = [table[r][0] for r in rules]
     for metric in METRICS:
         for acq in acquisitions:
             create_csv(os.path.join(directory, f"{acq}_{metric}"), budget)
     write_metadata(directory, budget, trials, starts)
     rng = np.random.default_rng(seed)
-    initial_samples = [lbs[:, None] + (ubs - lbs)[:, None] * rng.random((testfn.dim, INITIAL_OBSERVATIONS))
+    initial_samples = [lbs[:, None] + (ubs - lbs)[:, None] * rng.random((testfn.dim, initial_observations))
                        for _ in range(trials)]
     true_minimum = float(testfn.f(np.asarray(testfn.xopt[0], dtype=np.float64)))
     results = {}
@@ -120,14 +147,15 @@ def run(function_name, output_dir, budget=15, trials=60, starts=16, horizon=0, m
         for trial in range(trials):
             Xinit = initial_samples[trial]
             yinit = testfn(Xinit)
-            sur = Surrogate(Matern52(), Xinit, yinit, capacity=budget + INITIAL_OBSERVATIONS, decision_rule=rule,
+            sur = Surrogate(Matern52(), Xinit, yinit, capacity=budget + initial_observations, decision_rule=rule,
                             σn2=1e-6)
+            sur.fmini_over_capacity = fmini_over_capacity
             initial_best = float(np.min(yinit))
             times, gaps, allocs, regrets, minobs = (np.zeros(budget) for _ in range(5))
             for b in range(budget):
                 t0 = time.perf_counter()
                 xnext, _ = rollout_solve(sur, lbs, ubs, horizon, mc_samples, batch_size, starts, sgd_iterations,
-                                         theta, device=device)
+                                         theta, eta=eta, device=device, solver=solver)
                 times[b] = time.perf_counter() - t0
                 observed_best = float(np.min(sur.get_active_observations()))
                 regrets[b] = simple_regret(true_minimum, observed_best)
@@ -137,6 +165,7 @@ def run(function_name, output_dir, budget=15, trials=60, starts=16, horizon=0, m
                     from .mle import optimize as mle_optimize
                     mle_optimize(sur, KERNEL_LBS, KERNEL_UBS)
                 minobs[b] = float(np.min(sur.get_active_observations()))
+            log(f"{acq} trial {trial + 1}/{trials}: gap {gaps[-1]:.4f}, {times.sum():.2f} s of solves")
             for metric, data in zip(METRICS, (times, gaps, allocs, regrets, minobs)):
                 write_to_csv(os.path.join(directory, f"{acq}_{metric}"), data)
             results[(acq, trial)] = dict(times=times, gaps=gaps, simple_regret=regrets, minimum_observations=minobs,

@@ -73,8 +73,14 @@ class Surrogate:
     def set_decision_rule(self, g):
         self.g = g
 
+    # Q3 as the reference has it; False (build option, not the reference) takes the minimum over
+    # the observed points only -- a diagnostic of the quirk's effect on positive objectives
+    fmini_over_capacity = True
+
     def fmini(self):
         """minimum(get_observations(base)) over the zero-padded capacity buffer (rollout.jl:109, Q3)."""
+        if not self.fmini_over_capacity:
+            return float(np.min(self.y[:self.observed]))
         return float(np.min(self.y))
 
     def reset(self, X, y):

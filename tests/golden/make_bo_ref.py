@@ -13,7 +13,7 @@ write_to_csv, utils.jl:155-172; gap = (initial_best − observed_best)/(initial_
                      60 trials, optimize!; header columns 0..20)
 
 Each case keeps the header (the budget labels) and the trial rows (the −1.0 placeholder row of
-create_csv dropped).  Run here, where /root/reference exists; the JSON travels with the repo.
+create_csv dropped), and the same of the matching `times` file (seconds per acquisition solve).  Run here, where /root/reference exists; the JSON travels with the repo.
 usage: python tests/golden/make_bo_ref.py [--reference /root/reference]
 """
 import argparse
@@ -41,7 +41,9 @@ def read_gaps(path):
         v = [float(x) for x in r]
         if all(x == -1.0 for x in v):          # create_csv's placeholder row
             continue
-        trials.append(v[-len(header):])        # rows carry the budget values (some a leading trial id)
+        # rows of the current write_to_csv carry the budget values only; the archived ones a
+        # leading trial id, and their times rows the whole preallocated container (zeros after)
+        trials.append(v[1:1 + len(header)] if len(v) > len(header) else v)
     return header, trials
 
 
@@ -52,7 +54,10 @@ def main():
     out = {}
     for key, rel in CASES.items():
         header, trials = read_gaps(os.path.join(a.reference, rel))
-        out[key] = {"source": rel, "budget_labels": header, "gaps": trials}
+        trel = rel.replace("_gaps.csv", "_times.csv")
+        theader, times = read_gaps(os.path.join(a.reference, trel))
+        out[key] = {"source": rel, "budget_labels": header, "gaps": trials, "times_source": trel,
+                    "times_labels": theader, "times": times}
     with open(os.path.join(HERE, "bo_ref_gaps.json"), "w") as f:
         json.dump(out, f, separators=(",", ":"))
     for k, v in out.items():

@@ -51,3 +51,44 @@ def test_bayesopt_end_to_end(gpu, tmp_path, horizon, optimize):
             assert np.all(r["gaps"] <= 1.0 + 1e-12) and np.all(r["gaps"] >= 0.0)
             assert np.all(r["simple_regret"] >= 0.0)
     assert os.path.exists(d / "metadata.txt")
+
+
+def test_reference_bo_fixture_and_comparison_helpers():
+    """tests/golden/bo_ref_gaps.json (the reference's recorded gap curves, make_bo_ref.py) and the
+    label conventions / statistics of tools/bo_compare.py."""
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bo_compare as B
+    ref = B.load_reference()
+    assert set(B.SETTINGS) <= set(ref)
+    for key, case in ref.items():
+        g = np.array(case["gaps"])
+        assert g.shape[0] >= 59 and g.shape[1] == len(case["budget_labels"])
+        assert np.all((g >= 0.0) & (g <= 1.0 + 1e-12))                   # gap ∈ [0, 1]
+        assert np.all(np.diff(g, axis=1) >= -1e-12)                      # running minimum: gaps never fall
+        for lab in B.SETTINGS[key]["labels"]:
+            assert B.ref_column(case, lab).shape == (g.shape[0],)
+    # the archived rollout files start at label 0 (no BO observation yet): gap 0
+    assert np.all(B.ref_column(ref["rollout_h1_braninhoo"], "0") == 0.0)
+    # our columns: label k = after k observations; the last from the final minimum observation
+    res = [dict(gaps=np.array([0.0, 0.5]), minimum_observations=np.array([1.0, 0.5]), initial_best=2.0)]
+    cols = B.our_gap_columns(res, 0.0, 2)
+    np.testing.assert_allclose(cols, [[0.0, 0.5, 0.75]])
+    assert B.our_column(cols, "2", myopic=False)[0] == 0.75 and B.our_column(cols, "2", myopic=True)[0] == 0.5
+    c = B.compare([0.1, 0.2, 0.3], [0.1, 0.2, 0.3, 0.4])
+    assert abs(c["ours_mean"] - 0.2) < 1e-15 and c["n_ref"] == 4 and 0.0 < c["mannwhitney_p"] <= 1.0
+
+
+def test_box_adam_steps_in_box_widths():
+    """BoxAdam: the first Adam step moves every coordinate by η box widths (sign of the gradient),
+    whatever the gradient's scale, and the iterate stays in the box."""
+    from mrbo.bayesopt import BoxAdam
+    lbs, ubs = np.array([-5.0, 0.0]), np.array([10.0, 15.0])
+    opt = BoxAdam(lbs, ubs, η=0.1)
+    x = np.array([0.0, 7.5])
+    opt.update(x, np.array([1e4, -1e-3]))
+    np.testing.assert_allclose(x, [0.0 + 1.5, 7.5 - 1.5], rtol=1e-6)
+    for _ in range(100):
+        opt.update(x, np.array([1e4, -1e-3]))
+    assert np.all(x >= lbs) and np.all(x <= ubs) and x[0] == 10.0 and x[1] == 0.0

@@ -1,0 +1,155 @@
+#!/usr/bin/env python3
+"""Statistical comparison of the MI355X BO loop (mrbo/bayesopt.py) with the reference's recorded
+BO runs (parity of BO trajectories is unpinned -- Julia's RNG, Optim.jl and the
+reference's undefined rollout solver cannot be reproduced -- so the evidence is distributional).
+
+For every case of tests/golden/bo_ref_gaps.json (extracted by tests/golden/make_bo_ref.py from
+the reference's experiment CSVs) this runs the loop on the GPU with the reference's recorded
+settings and compares the per-trial `gaps` (utils.jl `gap`, recorded before conditioning, as
+nonmyopic_bayesopt.jl:273-281) at the compared budget labels: means with standard errors, the
+two-sided Mann–Whitney U and Kolmogorov–Smirnov p-values, and the seconds per acquisition solve
+beside the reference's recorded ones (earlier code versions on unstated hardware).
+
+  myopic_<fn>_ei     vs. the rollout acquisition at horizon 0 (MC expected improvement, SGA
+                     from a 64-point batch, as the myopic driver's 64 starts) -- the myopic
+                     driver's EI multistart is a different solver of the same acquisition
+  rollout_h<h>_<fn>  vs. the rollout acquisition at horizon h, the archived run's settings
+                     (1 initial point, 8 starts, batch 8, 100 MC samples, 50 SGD iterations)
+
+usage: python tools/bo_compare.py [--trials 20] [--cases a,b] [--out gpurun_out/bo_compare.jsonl]
+One JSON line per case (stdout and --out); progress on stderr.
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "rollout-bayesian-optimization_amd"), ROOT]
+
+FIXTURE = os.path.join(ROOT, "tests", "golden", "bo_ref_gaps.json")
+
+# per case: our run() settings and the budget labels compared (the reference's column labels)
+SETTINGS = {
+    "myopic_braninhoo_ei": dict(fn="braninhoo", horizon=0, budget=30, initial=5, starts=16, batch=64,
+                                labels=["10", "20", "30"]),
+    "myopic_hartmann6d_ei": dict(fn="hartmann6d", horizon=0, budget=30, initial=5, starts=16, batch=64,
+                                 labels=["10", "20", "30"]),
+    "rollout_h0_braninhoo": dict(fn="braninhoo", horizon=0, budget=20, initial=1, starts=8, batch=8, labels=["5", "10", "20"]),
+    "rollout_h1_braninhoo": dict(fn="braninhoo", horizon=1, budget=20, initial=1, starts=8, batch=8, labels=["5", "10", "20"]),
+    "rollout_h0_gramacylee": dict(fn="gramacylee", horizon=0, budget=20, initial=1, starts=8, batch=8, labels=["5", "10", "20"]),
+    "rollout_h1_gramacylee": dict(fn="gramacylee", horizon=1, budget=20, initial=1, starts=8, batch=8, labels=["5", "10", "20"]),
+}
+
+
+def load_reference(path=FIXTURE):
+    with open(path) as f:
+        return json.load(f)
+
+
+def our_gap_columns(res, true_minimum, budget):
+    """Per-trial gaps at labels 0..budget: label k = after k BO observations, i.e. run()'s
+    gaps[k] (recorded before conditioning at step k+1) for k < budget, and the gap of the final
+    minimum observation for k = budget.  Returns (trials, budget+1)."""
+    rows = []
+    for r in res:
+        g = list(r["gaps"])
+        ib = r["initial_best"]
+        g.append((ib - r["minimum_observations"][-1]) / (ib - true_minimum))
+        rows.append(g)
+    return np.array(rows)
+
+
+def ref_column(case, label):
+    """Reference gaps at a budget label, with the label convention of its file: the myopic files
+    label budget steps 1..B (gap before conditioning at step b = after b-1 observations); the
+    archived rollout files label 0..B (after k observations)."""
+    labels = case["budget_labels"]
+    return np.array([row[labels.index(label)] for row in case["gaps"]])
+
+
+def our_column(gcols, label, myopic):
+    k = int(label) - 1 if myopic else int(label)
+    return gcols[:, k]
+
+
+def compare(a, b):
+    """ours (a) vs reference (b): means, standard errors, Mann–Whitney U and KS p-values"""
+    from scipy.stats import ks_2samp, mannwhitneyu
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    se = lambda x: float(x.std(ddof=1) / np.sqrt(x.size)) if x.size > 1 else float("nan")
+    out = {"ours_mean": float(a.mean()), "ours_se": se(a), "ref_mean": float(b.mean()), "ref_se": se(b),
+           "n_ours": int(a.size), "n_ref": int(b.size)}
+    out["mannwhitney_p"] = float(mannwhitneyu(a, b, alternative="two-sided").pvalue)
+    out["ks_p"] = float(ks_2samp(a, b).pvalue)
+    return out
+
+
+def run_case(key, case, trials, seed, log, solver="sga", eta=0.5, q3=True):
+    from mrbo import bayesopt
+    s = SETTINGS[key]
+    testfn = bayesopt.TESTFNS[s["fn"]]()
+    true_minimum = float(testfn.f(np.asarray(testfn.xopt[0], dtype=np.float64)))
+    with tempfile.TemporaryDirectory() as tmp:
+        t0 = time.perf_counter()
+        res = bayesopt.run(s["fn"], tmp, budget=s["budget"], trials=trials, starts=s["starts"], horizon=s["horizon"],
+                           mc_samples=100, batch_size=s["batch"], sgd_iterations=50, optimize=True, seed=seed,
+                           rules=("ei",), initial_observations=s["initial"], solver=solver, eta=eta,
+                           fmini_over_capacity=q3,
+                           log=lambda *m: log(f"[{key}] " + " ".join(map(str, m))))
+        wall = time.perf_counter() - t0
+    trials_res = []
+    for t in range(trials):
+        r = res[(f"rollout_{s['horizon']}_ei", t)]
+        y = r["y"]
+        r = dict(r, initial_best=float(np.min(y[:s["initial"]])))
+        trials_res.append(r)
+    gcols = our_gap_columns(trials_res, true_minimum, s["budget"])
+    myopic = key.startswith("myopic")
+    per_label = {lab: compare(our_column(gcols, lab, myopic), ref_column(case, lab)) for lab in s["labels"]}
+    our_times = np.concatenate([r["times"] for r in trials_res])
+    ref_times = np.array(case["times"], float)[:, :s["budget"]].ravel()
+    ref_times = ref_times[ref_times >= 0]
+    return {"case": key, "reference": case["source"], "settings": dict(s, trials=trials, mc_samples=100,
+                                                                        sgd_iterations=50, optimize=True, solver=solver,
+                                                                        eta=eta, seed=seed, q3_fmini_over_capacity=q3),
+            "gaps": per_label, "ours_mean_curve": gcols.mean(axis=0).tolist(),
+            "seconds_per_solve": {"ours_median": float(np.median(our_times)), "ref_median": float(np.median(ref_times)),
+                                  "ref_note": "reference times from earlier code versions on unstated hardware"},
+            "wall_s": wall}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trials", type=int, default=20)
+    ap.add_argument("--seed", type=int, default=1906)
+    ap.add_argument("--cases", default=",".join(SETTINGS))
+    ap.add_argument("--out", default="")
+    ap.add_argument("--solver", default="sga", choices=["sga", "adam"],
+                    help="outer solver of the build-defined rollout acquisition (mrbo/bayesopt.py)")
+    ap.add_argument("--eta", type=float, default=0.0, help="step (default 0.5 for sga, 0.02 box widths for adam)")
+    ap.add_argument("--no-q3", action="store_true",
+                    help="diagnostic: fmini over the observed points instead of the zero-padded buffer (Q3 off)")
+    a = ap.parse_args()
+    ref = load_reference()
+    log = lambda m: print(m, file=sys.stderr, flush=True)
+    for key in a.cases.split(","):
+        eta = a.eta or (0.5 if a.solver == "sga" else 0.02)
+        row = run_case(key, ref[key], a.trials, a.seed, log, solver=a.solver, eta=eta, q3=not a.no_q3)
+        line = json.dumps(row)
+        print(line, flush=True)
+        if a.out:
+            with open(a.out, "a") as f:
+                f.write(line + "\n")
+        g = row["gaps"][SETTINGS[key]["labels"][-1]]
+        log(f"{key} [{a.solver}{'' if not a.no_q3 else ', Q3 off'}]: final gap ours {g['ours_mean']:.3f}±{g['ours_se']:.3f} ref {g['ref_mean']:.3f}±{g['ref_se']:.3f} "
+            f"MW p={g['mannwhitney_p']:.3f}; s/solve ours {row['seconds_per_solve']['ours_median']:.3f} "
+            f"ref {row['seconds_per_solve']['ref_median']:.2f}")
+
+
+if __name__ == "__main__":
+    main()
