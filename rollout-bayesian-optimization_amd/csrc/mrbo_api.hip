@@ -683,7 +683,7 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
   const double *dX = nullptr, *dy = nullptr;
   if (sg.in(s->X, (size_t)d * N, &dX) || sg.in(s->y, (size_t)N, &dy)) return fail(MRBO_ERR_NOMEM, "staging X, y");
   GpFitParams q{d, N, s->kernel, s->sigma_n2, dX, dy, nt, dth, s->period, dll_, dgr, (int*)dst, dL, dc, nullptr};
-  if (!gpfit_in_regs(q)) {   // the register kernel (N ≤ 64, no factor outputs) needs no workspace
+  if (!gpfit_in_regs(q) && !gpfit_in_lds(q)) {   // the register (N ≤ 64) and LDS (N ≤ 128) kernels need none
     if (hipMalloc(&q.work, sizeof(double) * 3 * NN * P) != hipSuccess) return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
     sg.bufs.push_back(q.work);
   }

@@ -55,5 +55,9 @@ void launch_gpfit(int P, hipStream_t st, const GpFitParams& q);
 inline bool gpfit_in_regs(const GpFitParams& q) {
   return q.N <= 64 && q.d <= 16 && !q.L_out && !q.c_out;
 }
+// 64 < N ≤ 128 (and N ≤ 64 with factor outputs): gpfit_lds_kernel, no global workspace
+inline bool gpfit_in_lds(const GpFitParams& q) {
+  return q.N <= 128 && q.d <= 16 && !gpfit_in_regs(q);
+}
 
 }  // namespace mrbo

@@ -17,7 +17,8 @@
 // readlane broadcasts; V = L⁻¹ by columns (lane j = column j) and K⁻¹ = VᵀV with the same DPP
 // broadcasts; tr(K⁻¹δK) and cᵀδKc from K⁻¹.  K and δK are evaluated once per pair j ≤ i.  The
 // reference's operations (chol, then triangular solves); summation orders differ (tolerance).
-// Otherwise (N ≤ 256, or when L / c are requested) gpfit_kernel: one workgroup per candidate;
+// 64 < N ≤ 128, or N ≤ 64 with L / c requested: gpfit_lds_kernel (below; everything in LDS).
+// Otherwise (N ≤ 256) gpfit_kernel: one workgroup per candidate;
 // N³/3 (Cholesky) + N³/2 (Z = L⁻¹δK per θ component) + N³/6 (L⁻¹) FMAs on a global workspace
 // (3·N² doubles per candidate, L2-resident at N ≤ 256).  Column-parallel steps map one thread
 // to one column; the right-looking Cholesky updates the trailing triangle with all 256 threads
@@ -508,6 +509,250 @@ __global__ void __launch_bounds__(64 * GR_WAVES) gpfit_reg_kernel(GpFitParams q,
 #endif
 }
 
+// ---- 64 < N ≤ 128: one workgroup per candidate, the factor and its inverse in LDS ----------
+// S (128 × 129 doubles, column-major r + LD·c, odd LD: row and column walks conflict free) holds
+// K → L in its lower triangle and V = L⁻¹ transposed in its strict upper triangle (V[i][j], i > j,
+// at j + LD·i); L's diagonal in ld_, V's (1/L_ii) in dv.  Four waves:
+//   K pairs (all) → right-looking Cholesky, thread (row i, parity) updating S[i][j] for j ≡ parity
+//   (one barrier per column, no global workspace) → V = L⁻¹ by columns (waves 0-1, lane = column)
+//   beside c = L'\(L\y) by column-
+//   oriented substitutions (wave 2, two rows per lane, readlane broadcasts) → tr(K⁻¹δK_t) and
+//   cᵀδK_t c over the pairs j < i with K⁻¹_ij = Σ_{m ≥ i} V_mi V_mj (δK_ii = 0), δK on the fly.
+// N³/3 + N³/6 + N³/6 FMAs instead of the workspace kernel's N³/3 + N³/2·nt + N³/6.
+constexpr int GL_N = 128, GL_LD = 129, GL_THREADS = 256;
+
+template <int NT>
+__global__ void __launch_bounds__(GL_THREADS) gpfit_lds_kernel(GpFitParams q, int P) {
+  extern __shared__ __attribute__((aligned(16))) double gsm[];
+  double* S = gsm;                      // GL_N × GL_LD
+  double* XS = S + GL_N * GL_LD;        // X[u][i] at u·GL_N + i (u < d ≤ 16)
+  double* ld_ = XS + 16 * GL_N;         // L_ii
+  double* dv = ld_ + GL_N;              // 1/L_ii
+  double* cv = dv + GL_N;               // y, then c
+  __shared__ double part[GL_THREADS / 64][2 * NT + 2];
+  __shared__ int fail;
+  const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (p >= P) return;   // whole workgroups
+#ifdef MRBO_GPFIT_STAMPS
+  unsigned long long gl_ts[6], gl_t0 = __builtin_amdgcn_s_memtime();
+#define GL_STAMP(k) gl_ts[k] = __builtin_amdgcn_s_memtime()
+#else
+#define GL_STAMP(k) ((void)0)
+#endif
+  const int N = q.N, d = q.d;
+  double ell, per;
+  cand_theta(q, p, ell, per);
+  if (tid == 0) fail = 0;
+  for (int idx = tid; idx < d * N; idx += GL_THREADS) {
+    const int u = idx % d, i = idx / d;
+    XS[u * GL_N + i] = q.X[idx];
+  }
+  for (int i = tid; i < N; i += GL_THREADS) cv[i] = q.y[i];
+  __syncthreads();
+  // K (eval_KXX :161-178, ψ(0) + σn2 on the diagonal) over the pairs j ≤ i, lower triangle
+  const int npair = N * (N + 1) / 2;
+  for (int qq = tid; qq < npair; qq += GL_THREADS) {
+    int i = (int)((sqrt(8.0 * qq + 1.0) - 1.0) * 0.5);
+    i += ((i + 1) * (i + 2) / 2 <= qq) ? 1 : 0;   // exact row of the triangle index
+    i -= (i * (i + 1) / 2 > qq) ? 1 : 0;
+    const int j = qq - i * (i + 1) / 2;
+    double r2 = 0.0;
+    for (int u = 0; u < d; ++u) { const double r = XS[u * GL_N + i] - XS[u * GL_N + j]; r2 = fma(r, r, r2); }
+    double psi, dps[2];
+    psi_dtheta(q.kernel, ell, per, (i == j) ? 0.0 : sqrt(r2), psi, dps);
+    S[i + GL_LD * j] = (i == j) ? psi + q.sn2 : psi;
+  }
+  __syncthreads();
+  GL_STAMP(0);
+  // right-looking Cholesky (PosDefException → status 1), ONE barrier per column: column k is final
+  // (unscaled) when step k starts, every thread scales the entries it reads by 1/L_kk itself, and
+  // thread (row i, parity 0) writes its scaled L_ik one step later, when no thread reads column k
+  // any more.  The pivot entry keeps K's value; L_kk goes to ld_.  Thread (row i, parity) updates
+  // S[i][j] for j ≡ parity, in batches of 8 whose 16 loads issue before the FMAs and stores.
+  {
+    const int i = tid & (GL_N - 1), par = tid >> 7;
+    double lprev = 0.0;
+    for (int k = 0; k < N; ++k) {
+      const double piv = S[k + GL_LD * k];
+      if (!(piv > 0.0)) {   // every thread reads the same pivot: a uniform exit
+        if (tid == 0) fail = 1;
+        break;
+      }
+      double lkk, rl;
+      sqrt_rsqrt(piv, lkk, rl);
+      if (tid == 0) { ld_[k] = lkk; dv[k] = rl; }
+      if (k > 0 && par == 0 && i > k - 1 && i < N) S[i + GL_LD * (k - 1)] = lprev;   // scaled L_i,k-1
+      if (i > k && i < N) {
+        const double lik = S[i + GL_LD * k] * rl;
+        lprev = lik;
+        for (int jb = k + 1 + par; jb <= i; jb += 16) {
+          double lv[8], av[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int j = min(jb + 2 * u, i);
+            lv[u] = S[j + GL_LD * k];
+            av[u] = S[i + GL_LD * j];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) av[u] = fma(-lik, lv[u] * rl, av[u]);
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (jb + 2 * u <= i) S[i + GL_LD * (jb + 2 * u)] = av[u];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  GL_STAMP(1);
+  if (fail) {
+    if (tid == 0) {
+      q.ll[p] = NAN;
+      for (int t = 0; t < NT; ++t) q.grad[(size_t)p * NT + t] = NAN;
+      q.status[p] = 1;
+    }
+    return;
+  }
+  if (w < 2) {
+    // V = L⁻¹, column j = tid: V_jj = 1/L_jj, V_ij = −(Σ_{k=j}^{i−1} L_ik V_kj)/L_ii, rows ascending.
+    // Lane j runs its own k range j..i−1 (no masks: L_ik is read at per-lane addresses), in
+    // batches of 8 whose 16 loads issue before the FMAs; k = j contributes L_ij/L_jj.
+    const int j = tid;
+    const double djj = dv[j];
+    for (int i = 64 * w + 1; i < N; ++i) {
+      if (i <= j) continue;
+      double sc[4] = {S[i + GL_LD * j] * djj, 0.0, 0.0, 0.0};
+      int k = j + 1;
+      for (; k + 8 <= i; k += 8) {
+        double lv[8], vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          lv[u] = S[i + GL_LD * (k + u)];
+          vv[u] = S[j + GL_LD * (k + u)];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sc[u & 3] = fma(lv[u], vv[u], sc[u & 3]);
+      }
+      for (; k < i; ++k) sc[0] = fma(S[i + GL_LD * k], S[j + GL_LD * k], sc[0]);
+      if (j < N) S[j + GL_LD * i] = -((sc[0] + sc[1]) + (sc[2] + sc[3])) * dv[i];
+    }
+    GL_STAMP(2);
+  } else if (w == 2) {
+    // c = L'\(L\y): column-oriented substitutions, rows lane and lane + 64 in registers, the
+    // solved entry broadcast by readlane
+    double r[2];
+    r[0] = (lane < N) ? cv[lane] : 0.0;
+    r[1] = (lane + 64 < N) ? cv[lane + 64] : 0.0;
+    for (int k = 0; k < N; ++k) {
+      const double zk = readlane_d(r[k >> 6], k & 63) * dv[k];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int i = lane + 64 * s2;
+        if (i == k) r[s2] = zk;
+        else if (i > k && i < N) r[s2] = fma(-S[i + GL_LD * k], zk, r[s2]);
+      }
+    }
+    for (int k = N - 1; k >= 0; --k) {
+      const double ck = readlane_d(r[k >> 6], k & 63) * dv[k];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int i = lane + 64 * s2;
+        if (i == k) r[s2] = ck;
+        else if (i < k) r[s2] = fma(-S[k + GL_LD * i], ck, r[s2]);
+      }
+    }
+    double yc = 0.0, lg = 0.0;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int i = lane + 64 * s2;
+      if (i < N) {
+        yc = fma(q.y[i], r[s2], yc);
+        lg += log(ld_[i]);
+      }
+    }
+    if (lane < N) cv[lane] = r[0];
+    if (lane + 64 < N) cv[lane + 64] = r[1];
+    yc = gr_sum(yc);
+    lg = gr_sum(lg);
+    if (lane == 0) { part[0][2 * NT] = yc; part[0][2 * NT + 1] = lg; }
+    GL_STAMP(3);
+  }
+  __syncthreads();
+  GL_STAMP(4);
+  // traces over the pairs j < i: wave w takes rows i ≡ w (mod 4), lanes over j in chunks of 64
+  double tr[NT], cgc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) tr[t] = cgc[t] = 0.0;
+  for (int i = 1 + w; i < N; i += GL_THREADS / 64) {
+    const double ci = cv[i];
+    for (int jb = 0; jb < i; jb += 64) {
+      const int j = jb + lane;
+      if (j >= i) break;
+      // K⁻¹_ij = V_ii V_ij + Σ_{m > i} V_mi V_mj
+      double kc[4] = {dv[i] * S[j + GL_LD * i], 0.0, 0.0, 0.0};
+      for (int mb = i + 1; mb < N; mb += 8) {
+        double av[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int m = min(mb + u, N - 1);
+          double x = S[i + GL_LD * m];
+          bv[u] = S[j + GL_LD * m];
+          asm volatile("" : "+v"(x), "+v"(bv[u]));
+          av[u] = (mb + u < N) ? x : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) kc[u & 3] = fma(av[u], bv[u], kc[u & 3]);
+      }
+      const double kij = (kc[0] + kc[1]) + (kc[2] + kc[3]);
+      double r2 = 0.0;
+      for (int u = 0; u < d; ++u) { const double r = XS[u * GL_N + i] - XS[u * GL_N + j]; r2 = fma(r, r, r2); }
+      double psi, dps[2];
+      psi_dtheta(q.kernel, ell, per, sqrt(r2), psi, dps);
+      const double cc = ci * cv[j];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        tr[t] = fma(kij, dps[t], tr[t]);
+        cgc[t] = fma(cc, dps[t], cgc[t]);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const double trs = gr_sum(tr[t]), cgs = gr_sum(cgc[t]);
+    if (lane == 0) { part[w][t] = trs; part[w][NT + t] = cgs; }
+  }
+  __syncthreads();
+  if (tid == 0) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {   // both triangles: 2·Σ_{j<i}
+      const double trs = (part[0][t] + part[1][t]) + (part[2][t] + part[3][t]);
+      const double cgs = (part[0][NT + t] + part[1][NT + t]) + (part[2][NT + t] + part[3][NT + t]);
+      q.grad[(size_t)p * NT + t] = cgs - trs;
+    }
+    q.ll[p] = -0.5 * part[0][2 * NT] - part[0][2 * NT + 1] - 0.5 * N * log(2.0 * 3.141592653589793);
+    q.status[p] = 0;
+  }
+  GL_STAMP(5);
+#ifdef MRBO_GPFIT_STAMPS
+  if (p == 0 && (tid == 0 || tid == 128))
+    printf("gpfit_lds cycles (thread %d): K %llu  chol %llu  V %llu  c %llu  wait %llu  traces %llu\n", tid,
+           gl_ts[0] - gl_t0, gl_ts[1] - gl_ts[0], gl_ts[2] - gl_ts[1], gl_ts[3] - gl_ts[1], gl_ts[4] - gl_ts[1],
+           gl_ts[5] - gl_ts[4]);
+#endif
+#undef GL_STAMP
+  if (q.L_out) {
+    double* Lo = q.L_out + (size_t)N * N * p;
+    for (int idx = tid; idx < N * N; idx += GL_THREADS) {
+      const int i = idx % N, j = idx / N;
+      Lo[idx] = (i > j) ? S[i + GL_LD * j] : ((i == j) ? ld_[i] : 0.0);
+    }
+  }
+  if (q.c_out)
+    for (int i = tid; i < N; i += GL_THREADS) q.c_out[(size_t)N * p + i] = cv[i];
+}
+
+size_t gpfit_lds_bytes() { return sizeof(double) * ((size_t)GL_N * GL_LD + 16 * GL_N + 3 * GL_N); }
+
 size_t gpfit_reg_lds(int nt) { return sizeof(double) * ((size_t)(1 + nt) * 64 * GR_LD + 64 + 16 * 64); }
 
 void launch_gpfit(int P, hipStream_t st, const GpFitParams& q) {
@@ -516,6 +761,13 @@ void launch_gpfit(int P, hipStream_t st, const GpFitParams& q) {
       hipLaunchKernelGGL(gpfit_reg_kernel<2>, dim3(P), dim3(64 * GR_WAVES), gpfit_reg_lds(2), st, q, P);
     else
       hipLaunchKernelGGL(gpfit_reg_kernel<1>, dim3(P), dim3(64 * GR_WAVES), gpfit_reg_lds(1), st, q, P);
+    return;
+  }
+  if (gpfit_in_lds(q)) {
+    if (q.nt == 2)
+      hipLaunchKernelGGL(gpfit_lds_kernel<2>, dim3(P), dim3(GL_THREADS), gpfit_lds_bytes(), st, q, P);
+    else
+      hipLaunchKernelGGL(gpfit_lds_kernel<1>, dim3(P), dim3(GL_THREADS), gpfit_lds_bytes(), st, q, P);
     return;
   }
   hipLaunchKernelGGL(gpfit_kernel, dim3(P), dim3(GPFIT_THREADS), 0, st, q);
