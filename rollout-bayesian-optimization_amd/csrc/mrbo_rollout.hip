@@ -306,13 +306,19 @@ __device__ __forceinline__ void gl_bcast_product(double (&acc)[K], const double 
   }
 }
 
+template <int D, int RPL>
+__device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL>& W, const KParams& kp);
+
 // ================================================================================
 // eval(fs, x, θ; fantasy_index = S)  -- radial_basis_surrogates.jl:482-581
 //   x is read from U[U_X].  Results land in U (lane-uniform) and `lr` (per lane).
 // ================================================================================
+// back_after (GRAD / GRADC / GSTART of the Newton iteration): the projected-gradient test runs
+// here and, when the step continues, the BACK part (backward product, Hα) follows in the same
+// call with the forward state still in registers.  Returns 1 when that BACK part ran.
 template <int D, int RPL>
-__device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, int S, int mode, LaneRes<D, RPL>& lr,
-                                         int kst = 0) {
+__device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, int S, int mode, LaneRes<D, RPL>& lr,
+                                        int kst = 0, bool back_after = false) {
   using Ly = Lay<D, RPL>;
   constexpr int D1 = Ly::D1, BS = Ly::BS, NR = Ly::NR;
   // Opaque copy of the lane index: keeps the per-lane LDS/global addresses derived from it
@@ -692,7 +698,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
     U[Ly::U_SC + SC_GSIGTH] = e.gsigth;
     U[Ly::U_SC + SC_FMIN] = fmin;
   }
-  if (mode == EV_VALUE) { wave_sync(); STAMP(W, 4); return; }
+  if (mode == EV_VALUE) { wave_sync(); STAMP(W, 4); return 0; }
   isig_f = isig;
   e_f = e;
   } else {   // GRADC: σ and the EI partials of the VALUE pass at this point
@@ -722,7 +728,12 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   if (mode == EV_GRAD || mode == EV_GRADC || mode == EV_GSTART) {   // a BACK evaluation may follow
     wave_sync();
     STAMP(W, 4);
-    return;
+    if (!back_after) return 0;
+    // the Newton iteration's P_GRAD decision (newton below): g = −∇α, stop when stationary
+    if (lane < D) U[Ly::U_NG + lane] = -U[Ly::U_GAL + lane];
+    wave_sync();
+    if (!newton_pg_ok<D, RPL>(W, kp)) return 0;
+    STAMP(W, 12);
   }
   } else {   // EV_BACK: resume at the point of the preceding GRAD evaluation
 #pragma unroll
@@ -832,7 +843,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
       if constexpr (FMAX * D1 <= WAVE) break;
     }
   }
-  if (mode == EV_DRAW) { wave_sync(); STAMP(W, 5); return; }
+  if (mode == EV_DRAW) { wave_sync(); STAMP(W, 5); return 0; }
   STAMP(W, 5);
 
   // ---- 6. Hessian  Hα = gμμ∇μ∇μ' + gσσ∇σ∇σ' − (gσ/σ)(∇σ∇σ' + ∇kx·Dw) + Σ_j coef_j Hk_j
@@ -905,6 +916,7 @@ __device__ __forceinline__ void evaluate(WaveCtx<D, RPL>& W, const KParams& kp, 
   }
   wave_sync();
   STAMP(W, 7);
+  return 1;
 }
 
 // ================================================================================
@@ -1287,6 +1299,11 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
   double* U = W.U;
   const int lane = W.ln();
   enum { P_VAL = 0, P_TRIAL = 1, P_GRAD = 2, P_HESS = 3 };
+#ifdef MRBO_NO_FUSE_BACK
+  constexpr bool FUSE_BACK = false;
+#else
+  constexpr bool FUSE_BACK = true;   // GRAD + BACK in one evaluation call (evaluate back_after)
+#endif
   if (lane < D) {
     const double xa = clampd(W.XS[(long long)k * D + lane], U[Ly::U_LB + lane], U[Ly::U_UB + lane]);
     U[Ly::U_NX + lane] = xa;
@@ -1306,10 +1323,15 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
   int phase = have_f0 ? P_GRAD : P_VAL, mode = have_f0 ? (Ly::SQ ? EV_GSTART : EV_GRAD) : EV_VALUE, it = 0, ls = 0;
   double f = have_f0 ? f0 : 0.0, ft = 0.0, t = 1.0, dec = 0.0;
   for (;;) {
-    evaluate<D, RPL>(W, kp, S, mode, lr, k);
+    const int back = evaluate<D, RPL>(W, kp, S, mode, lr, k, FUSE_BACK && phase == P_GRAD);
     if (mode == EV_VALUE) ++nevals.value;
     else if (mode == EV_GRADC || mode == EV_GRAD || mode == EV_GSTART) ++nevals.grad;
     else ++nevals.hess;
+    if (FUSE_BACK && phase == P_GRAD) {   // the projected-gradient test ran inside the evaluation
+      if (!back) break;                   // stationary
+      ++nevals.hess;                      // the BACK part (Hα) ran in the same call
+      phase = P_HESS;
+    }
     if (phase == P_HESS) {                 // Hα at x ready: step
       STAMP(W, 12);
       const bool go = newton_direction<D, RPL>(W, kp);
