@@ -65,6 +65,7 @@ struct mrbo_plan {
   int wpg = 4, blocks = 0;
   size_t smem = 0;
   int spec = 0;             // 1: rollout_kernel<D, RPL, 1> (Matérn-5/2 + EI fixed)
+  int fx = 0;               // 1: the FMAX = 4 kernel units (h ≤ 3, d ≤ 8)
   int xs_lds = 0;           // rollout launches stage xstarts in LDS (≤ 8 KB)
   int batch = 0;            // batched start-point values (start tables in LDS)
   int ewpg = 4, eblocks = 0;
@@ -78,59 +79,55 @@ namespace {
 double g_gpfit_ms = -1.0;   // kernel time of the last mrbo_gp_fit (HIP events around the launch)
 
 // ---- kernel dispatch: one translation unit per input dimension (mrbo_kernels.hip) -------
-bool get_kset(int d, int rpl, KernelSet& ks) {
-#define CASE_(DD) \
-  case DD: return kset_d##DD(rpl, ks);
-#define CASE(DD) CASE_(DD)
-  switch (d) {
+// fx = 1 selects the FMAX = 4 units (horizon ≤ 3, d ≤ 8), fx = 0 the FMAX = 6 ones
 #ifdef MRBO_ONLY_D
-    CASE(MRBO_ONLY_D)
+#define MRBO_APPLY(X, a) X(a)   // expands MRBO_ONLY_D before X pastes it
+#define MRBO_FOR_D(X) MRBO_APPLY(X, MRBO_ONLY_D)
+#if MRBO_ONLY_D <= 8
+#define MRBO_FOR_DF4(X) MRBO_APPLY(X, MRBO_ONLY_D)
 #else
-    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
+#define MRBO_FOR_DF4(X)
 #endif
-    default: return false;
-  }
-#undef CASE
-#undef CASE_
+#else
+#define MRBO_FOR_D(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
+#define MRBO_FOR_DF4(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
+#endif
+
+bool get_kset(int d, int rpl, int fx, KernelSet& ks) {
+#define K6(DD) case DD: return kset_d##DD(rpl, ks);
+#define K4(DD) case DD: return kset_d##DD##_f4(rpl, ks);
+  if (fx) { switch (d) { MRBO_FOR_DF4(K4) default: return false; } }
+  switch (d) { MRBO_FOR_D(K6) default: return false; }
+#undef K6
+#undef K4
 }
 
 // start tables of the packed layouts (rpl 2 / 4), before a rollout launch with kp.batch
-void launch_tables(int d, int rpl, int nstarts, hipStream_t st, const KParams& kp) {
-#define CASE_(DD) \
-  case DD: launch_tables_d##DD(rpl, nstarts, st, kp); break;
-#define CASE(DD) CASE_(DD)
-#ifdef MRBO_ONLY_D
-  switch (d) { CASE(MRBO_ONLY_D) }
-#else
-  switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) }
-#endif
-#undef CASE
-#undef CASE_
+void launch_tables(int d, int rpl, int fx, int nstarts, hipStream_t st, const KParams& kp) {
+#define K6(DD) case DD: launch_tables_d##DD(rpl, nstarts, st, kp); return;
+#define K4(DD) case DD: launch_tables_d##DD##_f4(rpl, nstarts, st, kp); return;
+  if (fx) { switch (d) { MRBO_FOR_DF4(K4) default: return; } }
+  switch (d) { MRBO_FOR_D(K6) default: return; }
+#undef K6
+#undef K4
 }
 
-void launch_rollout(int d, int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
-#define CASE_(DD) \
-  case DD: launch_rollout_d##DD(rpl, spec, g, b, sm, st, kp); break;
-#define CASE(DD) CASE_(DD)
-#ifdef MRBO_ONLY_D
-  switch (d) { CASE(MRBO_ONLY_D) }
-#else
-  switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) }
-#endif
-#undef CASE
-#undef CASE_
+void launch_rollout(int d, int rpl, int fx, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
+#define K6(DD) case DD: launch_rollout_d##DD(rpl, spec, g, b, sm, st, kp); return;
+#define K4(DD) case DD: launch_rollout_d##DD##_f4(rpl, spec, g, b, sm, st, kp); return;
+  if (fx) { switch (d) { MRBO_FOR_DF4(K4) default: return; } }
+  switch (d) { MRBO_FOR_D(K6) default: return; }
+#undef K6
+#undef K4
 }
-void launch_evalb(int d, int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
-#define CASE_(DD) \
-  case DD: launch_evalb_d##DD(rpl, g, b, sm, st, kp); break;
-#define CASE(DD) CASE_(DD)
-#ifdef MRBO_ONLY_D
-  switch (d) { CASE(MRBO_ONLY_D) }
-#else
-  switch (d) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) }
-#endif
-#undef CASE
-#undef CASE_
+
+void launch_evalb(int d, int rpl, int fx, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
+#define K6(DD) case DD: launch_evalb_d##DD(rpl, g, b, sm, st, kp); return;
+#define K4(DD) case DD: launch_evalb_d##DD##_f4(rpl, g, b, sm, st, kp); return;
+  if (fx) { switch (d) { MRBO_FOR_DF4(K4) default: return; } }
+  switch (d) { MRBO_FOR_D(K6) default: return; }
+#undef K6
+#undef K4
 }
 
 // choose waves per workgroup maximising resident waves per CU (LDS + register limits)
@@ -393,7 +390,8 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) { delete P; return fail(MRBO_ERR_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e)); }
   KernelSet ks;
-  if (!get_kset(d, P->RPL, ks)) {
+  P->fx = (p->h <= F4_HMAX && d <= F4_DMAX) ? 1 : 0;
+  if (!get_kset(d, P->RPL, P->fx, ks)) {
     delete P;
     return fail(MRBO_ERR_UNSUPPORTED, "d=%d (rows per lane %d) not compiled into this library", d, P->RPL);
   }
@@ -561,10 +559,10 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
   if (P->batch && P->RPL > 1) {   // packed layouts: global start tables for this launch's xstarts
     kp.kxb_g = P->dkxb;
     kp.gtab_g = P->dgtab;
-    launch_tables(d, P->RPL, P->p.nstarts, st, kp);
+    launch_tables(d, P->RPL, P->fx, P->p.nstarts, st, kp);
     HIP_TRY(hipGetLastError());
   }
-  launch_rollout(d, P->RPL, P->spec, dim3(P->blocks), dim3(P->wpg * WAVE), P->smem, st, kp);
+  launch_rollout(d, P->RPL, P->fx, P->spec, dim3(P->blocks), dim3(P->wpg * WAVE), P->smem, st, kp);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(P->ev1, st));
   P->timed = true;
@@ -650,7 +648,7 @@ int mrbo_eval_base(mrbo_plan_t* P, int32_t npts, const double* xs, double* out, 
   kp.pts = dxs;
   kp.pts_out = dout;
   HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * 4, st));
-  launch_evalb(d, P->RPL, dim3(P->eblocks), dim3(P->ewpg * WAVE), P->esmem, st, kp);
+  launch_evalb(d, P->RPL, P->fx, dim3(P->eblocks), dim3(P->ewpg * WAVE), P->esmem, st, kp);
   HIP_TRY(hipGetLastError());
   if (flags & MRBO_FLAG_HOST_POINTERS) {
     HIP_TRY(hipStreamSynchronize(st));

@@ -215,6 +215,18 @@ __device__ __forceinline__ void wave_reduce(double (&v)[K], double* red, int lan
   if ((lane & ((64 >> S) - 1)) == 0) red[idx] = v[0];
 }
 
+// Sum over the 64 lanes in EVERY lane, no LDS round trip: the butterfly of wave_reduce<1>
+// (each step adds the partner's value; a + b == b + a, so all lanes hold the same bits, those
+// wave_reduce<1> stores for lane 0).
+__device__ __forceinline__ double wave_allreduce1(double v) {
+  v = fold_all<32>(v);
+  v = fold_all<16>(v);
+  v = fold_all<8>(v);
+  v = fold_all<4>(v);
+  v = fold_all<2>(v);
+  return fold_all<1>(v);
+}
+
 // ---- transcendentals behind leaf calls ---------------------------------------------------
 // The fp64 exp/erfc expansions carry tens of 64-bit polynomial constants; inlined into the
 // Newton/horizon loops, LICM hoists their materialisation out of the loops and the kernel

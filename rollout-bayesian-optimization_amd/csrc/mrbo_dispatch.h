@@ -32,6 +32,18 @@ MRBO_DECLARE_D(5) MRBO_DECLARE_D(6) MRBO_DECLARE_D(7) MRBO_DECLARE_D(8)
 MRBO_DECLARE_D(9) MRBO_DECLARE_D(10) MRBO_DECLARE_D(11) MRBO_DECLARE_D(12)
 MRBO_DECLARE_D(13) MRBO_DECLARE_D(14) MRBO_DECLARE_D(15) MRBO_DECLARE_D(16)
 #undef MRBO_DECLARE_D
+// the same entry points of the FMAX = 4 units (h ≤ 3, d ≤ 8): fewer fantasy rows per wave in
+// LDS and registers
+#define MRBO_DECLARE_DF4(DD)                                                                    \
+  bool kset_d##DD##_f4(int rpl, KernelSet& ks);                                                 \
+  void launch_rollout_d##DD##_f4(int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp); \
+  void launch_evalb_d##DD##_f4(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp); \
+  void launch_tables_d##DD##_f4(int rpl, int nstarts, hipStream_t st, const KParams& kp);
+MRBO_DECLARE_DF4(1) MRBO_DECLARE_DF4(2) MRBO_DECLARE_DF4(3) MRBO_DECLARE_DF4(4)
+MRBO_DECLARE_DF4(5) MRBO_DECLARE_DF4(6) MRBO_DECLARE_DF4(7) MRBO_DECLARE_DF4(8)
+#undef MRBO_DECLARE_DF4
+constexpr int F4_HMAX = 3;   // horizons served by the FMAX = 4 units
+constexpr int F4_DMAX = 8;
 
 // base-GP fit + marginal likelihood for P lengthscales (mrbo_gpfit.hip)
 struct GpFitParams {

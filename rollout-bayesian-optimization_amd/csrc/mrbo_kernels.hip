@@ -1,5 +1,6 @@
-// mrbo_kernels.hip -- the rollout / eval_base kernels for ONE input dimension d = MRBO_D
-// (compiled once per d, in parallel; mrbo_api.hip dispatches through mrbo_dispatch.h).
+// mrbo_kernels.hip -- the rollout / eval_base kernels for ONE input dimension d = MRBO_D and one
+// fantasy capacity FMAX = MRBO_FMAX (compiled once per d with FMAX = 6, and for d ≤ 8 again
+// with FMAX = 4 for horizons h ≤ 3; mrbo_api.hip dispatches through mrbo_dispatch.h).
 // Rows per lane (RPL) compiled: d ≤ 8: 1, 2, 4, 8 (N ≤ 64, 128, 256, 512); d = 9..16: 1, 2
 // (N ≤ 128).  The compile-time Matérn-5/2 + EI specialisation (SPEC = 1) exists for d ≤ 8 and
 // RPL ≤ 4 -- the configurations of BASELINE.json; everything else runs the generic kernel.
@@ -12,6 +13,12 @@
 
 #define MRBO_CAT_(a, b) a##b
 #define MRBO_CAT(a, b) MRBO_CAT_(a, b)
+// entry points of this unit: <name><d> for FMAX = 6, <name><d>_f<FMAX> otherwise (mrbo_dispatch.h)
+#if MRBO_FMAX == 6
+#define MRBO_SFX(name) MRBO_CAT(name, MRBO_D)
+#else
+#define MRBO_SFX(name) MRBO_CAT(MRBO_CAT(MRBO_CAT(name, MRBO_D), _f), MRBO_FMAX)
+#endif
 
 namespace mrbo {
 
@@ -28,7 +35,7 @@ static KernelSet kset() {
                    Ly::LINV_GLOBAL, KBounds<D, RPL>::threads};
 }
 
-bool MRBO_CAT(kset_d, MRBO_D)(int rpl, KernelSet& ks) {
+bool MRBO_SFX(kset_d)(int rpl, KernelSet& ks) {
   if (rpl == 1) ks = kset<MRBO_D, 1>();
   else if (rpl == 2) ks = kset<MRBO_D, 2>();
 #if MRBO_D <= 8
@@ -53,7 +60,7 @@ static void launch_rollout_spec(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t 
   else launch_one<8, SPEC>(g, b, sm, st, kp);
 }
 
-void MRBO_CAT(launch_rollout_d, MRBO_D)(int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st,
+void MRBO_SFX(launch_rollout_d)(int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st,
                                        const KParams& kp) {
   if (spec) launch_rollout_spec<1>(rpl, g, b, sm, st, kp);
   else launch_rollout_spec<0>(rpl, g, b, sm, st, kp);
@@ -65,7 +72,7 @@ static void launch_tables_one(int nstarts, hipStream_t st, const KParams& kp) {
     hipLaunchKernelGGL((start_tables_kernel<MRBO_D, RPL>), dim3(nstarts), dim3(WAVE), 0, st, kp);
 }
 
-void MRBO_CAT(launch_tables_d, MRBO_D)(int rpl, int nstarts, hipStream_t st, const KParams& kp) {
+void MRBO_SFX(launch_tables_d)(int rpl, int nstarts, hipStream_t st, const KParams& kp) {
   if (rpl == 2) launch_tables_one<2>(nstarts, st, kp);
   else if (rpl == 4) launch_tables_one<4>(nstarts, st, kp);
   else if (rpl == 8) launch_tables_one<8>(nstarts, st, kp);
@@ -76,7 +83,7 @@ static void launch_evalb_one(dim3 g, dim3 b, size_t sm, hipStream_t st, const KP
   if constexpr (has_rpl(MRBO_D, RPL)) hipLaunchKernelGGL((eval_base_kernel<MRBO_D, RPL>), g, b, sm, st, kp);
 }
 
-void MRBO_CAT(launch_evalb_d, MRBO_D)(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
+void MRBO_SFX(launch_evalb_d)(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
   if (rpl == 1) launch_evalb_one<1>(g, b, sm, st, kp);
   else if (rpl == 2) launch_evalb_one<2>(g, b, sm, st, kp);
   else if (rpl == 4) launch_evalb_one<4>(g, b, sm, st, kp);

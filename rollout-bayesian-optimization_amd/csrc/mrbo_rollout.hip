@@ -18,11 +18,18 @@
 #ifndef MRBO_WAVES_PER_SIMD
 #define MRBO_WAVES_PER_SIMD 2
 #endif
+// Everything below is compiled per fantasy capacity FMAX (-DMRBO_FMAX, default 6 = h ≤ 5; the
+// kernel units are also built with FMAX = 4 for h ≤ 3): an inline namespace per FMAX keeps the
+// two builds' kernels and helpers distinct symbols in one library.
+#define MRBO_FNS_CAT_(a, b) a##b
+#define MRBO_FNS_CAT(a, b) MRBO_FNS_CAT_(a, b)
+#define MRBO_FNS MRBO_FNS_CAT(fmax, MRBO_FMAX)
 #ifndef MRBO_WAVES_PER_SIMD_GL   // N ≤ 256 (L2-fed layout): 512 registers per wave at 1
 #define MRBO_WAVES_PER_SIMD_GL 1
 #endif
 
 namespace mrbo {
+inline namespace MRBO_FNS {
 
 template <int D, int RPL>
 struct Lay {
@@ -1276,11 +1283,7 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParam
     else rad_eval(W.rad, rho2, psi, g1, g2);
     v[0] += fabs(U[Ly::U_CF + (S + 1) * FMAX + lane]) * fabs(g1) * fast_sqrt0(rho2);
   }
-  wave_sync();
-  wave_reduce<1>(v, W.red, lane);
-  wave_sync();
-  const double bmu = W.red[0];
-  wave_sync();
+  const double bmu = wave_allreduce1(v[0]);
   return (fabs(gm) * bmu + bsig) * isc + add <= thr;
 }
 
@@ -1691,10 +1694,7 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
     double v[1] = {0.0};
 #pragma unroll
     for (int s = 0; s < RPL; ++s) v[0] += fabs(W.C[(long long)(S + 1) * Ly::NR + lane + WAVE * s]);
-    wave_sync();
-    wave_reduce<1>(v, W.red, lane);
-    wave_sync();
-    double cabs = W.red[0];
+    double cabs = wave_allreduce1(v[0]);
     for (int r = 0; r <= S; ++r) cabs += fabs(U[Ly::U_CF + (S + 1) * FMAX + r]);
     if (lane == 0) U[Ly::U_SC + SC_CABS] = cabs;
     wave_sync();
@@ -2385,4 +2385,5 @@ __global__ void __launch_bounds__((KBounds<D, RPL>::threads), (KBounds<D, RPL>::
   }
 }
 
+}  // namespace MRBO_FNS
 }  // namespace mrbo
