@@ -574,7 +574,8 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
                                               "Hessian assembly", "Newton/draw bookkeeping (outside eval)",
                                               "adjoint pair", "draw+condition", "resolve+adjoint setup",
                                               "Newton accept/convergence", "Newton direction", "Newton trial point",
-                                              "batched start values", "multistart loop (certified starts)"};
+                                              "batched start values", "multistart loop (certified starts)",
+                                              "Newton Gershgorin retry", "Newton substitutions"};
     unsigned long long hs[20];
     HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipMemcpy(hs, dstamps, sizeof(hs), hipMemcpyDeviceToHost));
@@ -583,6 +584,7 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
     for (int k = 0; k < NSTAMP; ++k)
       fprintf(stderr, "[mrbo stamps] %-40s %6.2f%%  %.3e ticks/traj\n", stamp_names[k], 100.0 * hs[k] / tot,
               (double)hs[k] / (double)T);
+    fprintf(stderr, "[mrbo stamps] Gershgorin retries per trajectory: %.3f\n", (double)hs[19] / (double)T);
   }
 #endif
   if (host) {

@@ -91,7 +91,8 @@ struct Lay {
   static constexpr int U_UB = U_LB + D;                  // box upper bounds      D
   static constexpr int U_HF = U_UB + D;                  // fantasy rows: [x - X_r (D), g1, g2]  FMAX×(D+2)
   static constexpr int U_STAMP = U_HF + FMAX * (D + 2);   // cycle accumulators (MRBO_STAMPS) 20
-  static constexpr int U_SIZE = ((U_STAMP + 20) + 1) & ~1;
+  static constexpr int U_KC = U_STAMP + 20;              // launch constants (KC_*), see wave_setup
+  static constexpr int U_SIZE = ((U_KC + 12) + 1) & ~1;
   static constexpr int G12 = 3 * NR;                     // per-lane [g1, g2, Y0] of the base rows
   static constexpr int EC = SQ ? (2 * FMAX + 1) * NR : 0;  // E (FMAX×NR) + C ((FMAX+1)×NR) in LDS
   static constexpr int WAVE_LDS = BROWS * BS + REDN + U_SIZE + G12 + EC;
@@ -121,6 +122,14 @@ enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, 
        // NonUniformCost (kp.cost): the rule value g before weighting, c(x), max_a |∂_a c(x)|
        SC_ARAW = 14, SC_COSTC = 15, SC_GCMAX = 16,
        SC_ISIG = 17 };   // 1/σ
+
+// Launch constants the trajectory code reads in its loops, copied into each wave's lane-uniform
+// LDS at wave_setup: read back with ds_read at the point of use instead of being held in SGPRs
+// for the whole kernel, where they overflowed the 102-SGPR budget and were spilled to VGPR lanes
+// (a v_readlane per reload, on the VALU).  Branch conditions keep the kernel-argument copy.
+enum { KC_PSI0 = 0, KC_D2PSI0 = 1, KC_THETA = 2, KC_SIGTOL = 3, KC_GTOL = 4, KC_GCMU = 5, KC_GCSIG = 6,
+       KC_GCD2 = 7, KC_XTOL = 8, KC_FTOL = 9, KC_HTOL = 10, KC_SN2 = 11 };
+#define KCV(F) (W.U[Lay<D, RPL>::U_KC + KC_##F])
 
 // ∂_lane c(x) by unrolled select (lane < D; a runtime index would put gc in scratch)
 template <int D>
@@ -673,11 +682,11 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
   EIp e_f;
   if (do_val) {
   const double mu = mu_v;
-  const double var = kp.psi0 - g00_v;
+  const double var = KCV(PSI0) - g00_v;
   double sig, isig;
   sig_isig(var, sig, isig);
   const double fmin = U[Ly::U_FMIN + S + 1];
-  const EIp e = rule_partials(kp.rule, mu, sig, kp.theta, fmin, kp.sigma_tol, isig);
+  const EIp e = rule_partials(kp.rule, mu, sig, KCV(THETA), fmin, KCV(SIGTOL), isig);
   double alpha = e.g;
   if (kp.cost) {   // cost-weighted rule f = α/c(x) (NonUniformCost, cost_functions.jl:5-20)
     double gc[D];
@@ -940,7 +949,7 @@ __device__ __forceinline__ int condition(WaveCtx<D, RPL>& W, const KParams& kp, 
   const int nf = S + 1;   // index of the new fantasy row
   const double g00 = U[Ly::U_G];
   const double mu = U[Ly::U_SC + SC_MU];
-  const double l22sq = kp.psi0 + kp.sn2 - g00;   // C - L21·L21 (update_cholesky! :405-418)
+  const double l22sq = KCV(PSI0) + KCV(SN2) - g00;   // C - L21·L21 (update_cholesky! :405-418)
   if (!(l22sq > 0.0)) return 4;                  // PosDefException
   const double inv = 1.0 / sqrt(l22sq);
   const double gam = (yv - mu) / l22sq;          // c_new = [c - γ w; γ]
@@ -986,7 +995,7 @@ __device__ __forceinline__ int draw(WaveCtx<D, RPL>& W, const KParams& kp, const
 #pragma unroll
   for (int j = 0; j < D1; ++j) {
     // Symmetric(σx) uses the upper triangle: σx[j][i] for i ≥ j
-    const double kjj = (j == 0) ? kp.psi0 : -kp.d2psi0;
+    const double kjj = (j == 0) ? KCV(PSI0) : -KCV(D2PSI0);
     double sdiag = kjj - U[Ly::U_G + j * D1 + j];
 #pragma unroll
     for (int k = 0; k < j; ++k) sdiag -= Lc[TRI(j, k)] * Lc[TRI(j, k)];
@@ -1082,7 +1091,7 @@ template <int D, int RPL>
 __device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL>& W, const KParams& kp) {
   bool fr[D];
   double gs[D], box;
-  return newton_free_set<D, RPL>(W, fr, gs, box) > kp.g_tol;
+  return newton_free_set<D, RPL>(W, fr, gs, box) > KCV(GTOL);
 }
 
 // One projected-Newton direction from the state in U (x = U_NX, g = U_NG, H = U_H).
@@ -1094,7 +1103,7 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
   bool fr[D];
   double gs[D], box;
   const double pg = newton_free_set<D, RPL>(W, fr, gs, box);
-  if (!(pg > kp.g_tol)) return false;
+  if (!(pg > KCV(GTOL))) return false;
   // lower triangle of Hα, read unconditionally (a load under a select becomes a branch with a
   // full LDS round trip per element)
   double Hl[D * (D + 1) / 2];
@@ -1116,7 +1125,11 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
   }
   double idg[D];
   bool ok = chol_packed<D>(A, idg);
+  STAMP(W, 13);
   if (!ok) {  // Gershgorin shift over the free block, one retry
+#ifdef MRBO_STAMPS
+    stamp_count(W, 19, 1);   // Gershgorin retries (taken at ~80 % of C3's Newton directions)
+#endif
     double tau = 0.0, hmax = 0.0;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
@@ -1141,6 +1154,7 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
       }
     ok = chol_packed<D>(A, idg);
   }
+  STAMP(W, 17);
   double p[D];
   if (ok) {
     double t1[D];
@@ -1175,6 +1189,7 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
   for (int a = 0; a < D; ++a) pmine = (a == lane) ? p[a] : pmine;
   if (lane < D) U[Ly::U_NP + lane] = (pn > box) ? pmine * sc : pmine;
   wave_sync();
+  STAMP(W, 18);
   return true;
 }
 
@@ -1210,14 +1225,14 @@ __device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const K
   const double* U = W.U;
   const double gm = U[Ly::U_SC + SC_GMU], gs = U[Ly::U_SC + SC_GSIG];
   const double cabs = U[Ly::U_SC + SC_CABS], isig = U[Ly::U_SC + SC_ISIG];   // unconditional loads
-  double bound = fabs(gm) * kp.gcert_mu * cabs + fabs(gs) * kp.gcert_sig * isig;
+  double bound = fabs(gm) * KCV(GCMU) * cabs + fabs(gs) * KCV(GCSIG) * isig;
   bool zero = (gm == 0.0) & (gs == 0.0);
   if (kp.cost) {   // f = α/c: |∂f| ≤ B/c + |α| max|∇c|/c²; gμ = gσ = 0 certifies only where α = 0
     const double araw = U[Ly::U_SC + SC_ARAW], c = U[Ly::U_SC + SC_COSTC];
     bound = bound * (1.0 / c) + fabs(araw) * U[Ly::U_SC + SC_GCMAX] / (c * c);
     zero = zero & (araw == 0.0);
   }
-  return zero | ((kp.gcert_sig > 0.0) & (bound <= 0.25 * kp.g_tol));
+  return zero | ((kp.gcert_sig > 0.0) & (bound <= 0.25 * KCV(GTOL)));
 }
 
 // Tight certificate at x = U[U_X] on surface S, where grad_certified's cheap bound failed
@@ -1255,10 +1270,10 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParam
   // the σ part needs no rows: if it alone exceeds the threshold the test fails, and with the
   // cheap μ part (Σ|c|·max|ψ'| ≥ the row sum) it may already pass -- same decisions as the
   // full test, without the row pass
-  const double q = fmax(kp.psi0 - sig * sig, 0.0);
-  const double bsig = fabs(gs) * kp.gcert_d2 * fast_sqrt0(q) * isig, thr = 0.25 * kp.g_tol;
+  const double q = fmax(KCV(PSI0) - sig * sig, 0.0);
+  const double bsig = fabs(gs) * KCV(GCD2) * fast_sqrt0(q) * isig, thr = 0.25 * KCV(GTOL);
   if (!(bsig * isc + add <= thr)) return false;
-  if ((fabs(gm) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + bsig) * isc + add <= thr) return true;
+  if ((fabs(gm) * KCV(GCMU) * U[Ly::U_SC + SC_CABS] + bsig) * isc + add <= thr) return true;
   double x[D];
 #pragma unroll
   for (int a = 0; a < D; ++a) x[a] = U[Ly::U_X + a];
@@ -1382,7 +1397,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
       wave_sync();
       f = ft;
       ++it;
-      if (dx <= kp.x_tol || df <= kp.f_tol * fabs(f)) break;
+      if (dx <= KCV(XTOL) || df <= KCV(FTOL) * fabs(f)) break;
     } else {
       f = fe;
     }
@@ -1646,10 +1661,10 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
       mu = fma(U[Ly::U_CF + (S + 1) * FMAX + r], pf[r], mu);
     }
   }
-  const double var = kp.psi0 - g00;
+  const double var = KCV(PSI0) - g00;
   double sig, isig;
   sig_isig(var, sig, isig);
-  const EIp e = rule_partials(kp.rule, mu, sig, kp.theta, U[Ly::U_FMIN + S + 1], kp.sigma_tol, isig);
+  const EIp e = rule_partials(kp.rule, mu, sig, KCV(THETA), U[Ly::U_FMIN + S + 1], KCV(SIGTOL), isig);
   double fval = e.g, cval = 1.0, gcm = 0.0;
   if (kp.cost) {   // cost-weighted rule at the start point (see grad_certified)
     double gc[D];
@@ -1660,9 +1675,9 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   }
   bool cert = (e.gmu == 0.0 && e.gsig == 0.0) && (!kp.cost || e.g == 0.0);
   if (!cert && kp.gcert_sig > 0.0) {
-    double b = fabs(e.gmu) * kp.gcert_mu * U[Ly::U_SC + SC_CABS] + fabs(e.gsig) * kp.gcert_sig * isig;
+    double b = fabs(e.gmu) * KCV(GCMU) * U[Ly::U_SC + SC_CABS] + fabs(e.gsig) * KCV(GCSIG) * isig;
     if (kp.cost) b = b * (1.0 / cval) + fabs(e.g) * gcm / (cval * cval);
-    cert = b <= 0.25 * kp.g_tol;
+    cert = b <= 0.25 * KCV(GTOL);
   }
   f_lane = -fval;
   a_lane = e.g;
@@ -1884,7 +1899,7 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
   const double isig = U[Ly::U_SC + SC_ISIG];
   const double dsig = wq * (udw - dkx) * isig;
   double dgm, dgs;
-  rule_first(kp.rule, dmu, dsig, kp.theta, U[Ly::U_SC + SC_FMIN], kp.sigma_tol, dgm, dgs);
+  rule_first(kp.rule, dmu, dsig, KCV(THETA), U[Ly::U_SC + SC_FMIN], KCV(SIGTOL), dgm, dgs);
   // cost-weighted rule: δ∇(α/c) = δ∇α/c − δα ∇c/c², δα = gμ δμ + gσ δσ (build-defined)
   double gcx[D], cc = 1.0, dal = 0.0;
   if (kp.cost) {
@@ -2125,7 +2140,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
             for (int a = 0; a < D; ++a) xd[a] = -U[Ly::U_GF + (j - 1) * D + a] * ybj - U[Ly::U_ACC + j * D + a];
             // det(Hα) == det(Hα'): one LU serves the det test (Q4) and the solve
             const bool nonsing = lu_det_solve<D>(Hm, xd, det, true);
-            bool zero = !(det >= kp.htol);  // det(H) < htol → zeros; a NaN det keeps going (Julia)
+            bool zero = !(det >= KCV(HTOL));  // det(H) < htol → zeros; a NaN det keeps going (Julia)
             if (det != det) zero = false;
             if (zero) {
 #pragma unroll
@@ -2222,6 +2237,22 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
   }
   // zero this wave's LDS so that padded rows read as zeros
   for (int q = W.lane; q < Ly::WAVE_LDS; q += WAVE) wbase[q] = 0.0;
+  wave_sync();
+  if (W.lane == 0) {
+    double* kc = W.U + Ly::U_KC;
+    kc[KC_PSI0] = kp.psi0;
+    kc[KC_D2PSI0] = kp.d2psi0;
+    kc[KC_THETA] = kp.theta;
+    kc[KC_SIGTOL] = kp.sigma_tol;
+    kc[KC_GTOL] = kp.g_tol;
+    kc[KC_GCMU] = kp.gcert_mu;
+    kc[KC_GCSIG] = kp.gcert_sig;
+    kc[KC_GCD2] = kp.gcert_d2;
+    kc[KC_XTOL] = kp.x_tol;
+    kc[KC_FTOL] = kp.f_tol;
+    kc[KC_HTOL] = kp.htol;
+    kc[KC_SN2] = kp.sn2;
+  }
 }
 
 // SPEC = 1: the kernel function and decision rule fixed at compile time to Matérn-5/2 and EI
