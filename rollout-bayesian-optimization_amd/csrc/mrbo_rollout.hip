@@ -1033,6 +1033,8 @@ __device__ __forceinline__ int draw(WaveCtx<D, RPL>& W, const KParams& kp, const
 // Inner solve: deterministic projected Newton on f = -α, surface S.
 // ================================================================================
 // packed lower Cholesky in place; idg receives the reciprocals of the diagonal
+// The first non-positive pivot ends the factorization (wave-uniform branch): the caller discards
+// A then -- the Gershgorin retry refills it -- so the remaining columns would be wasted issue.
 template <int D>
 __device__ __forceinline__ bool chol_packed(double (&A)[D * (D + 1) / 2], double (&idg)[D]) {
 #define TRI(i, j) ((i) * ((i) + 1) / 2 + (j))
@@ -1043,6 +1045,9 @@ __device__ __forceinline__ bool chol_packed(double (&A)[D * (D + 1) / 2], double
 #pragma unroll
     for (int k = 0; k < j; ++k) s -= A[TRI(j, k)] * A[TRI(j, k)];
     ok = ok && (s > 0.0);
+#ifndef MRBO_NO_CHOL_EXIT
+    if (!ok) return false;
+#endif
     double ljj;
     sqrt_rsqrt(s, ljj, idg[j]);
     A[TRI(j, j)] = ljj;
