@@ -65,7 +65,9 @@ typedef enum {
  * the build defines the cost-weighted acquisition f(x) = α(x)/c(x) of the inner policy solve
  * (α, ∇f, Hf, ∂∇f/∂θ and the adjoint perturbations all weighted; parity unpinned, the oracle
  * implements the same definition).  u_a = (x_a − lb_a)/(ub_a − lb_a) over the plan's box:
- *   MRBO_COST_QUADRATIC  c(x) = c0 + Σ_a w_a u_a²        MRBO_COST_LOGLINEAR  c(x) = c0·exp(Σ_a w_a u_a) */
+ *   MRBO_COST_QUADRATIC  c(x) = c0 + Σ_a w_a u_a²        MRBO_COST_LOGLINEAR  c(x) = c0·exp(Σ_a w_a u_a)
+ * mrbo_plan_create refuses (MRBO_ERR_ARG) any model that is not positive on the box: c0 ≤ 0 or
+ * non-finite, a non-finite weight, a negative QUADRATIC weight, or ub ≤ lb in some dimension. */
 typedef enum { MRBO_COST_NONE = 0, MRBO_COST_QUADRATIC = 1, MRBO_COST_LOGLINEAR = 2 } mrbo_cost_t;
 
 /* per-trajectory status bits: the reference's exceptions (SURVEY.md §8b "Errors") */
@@ -178,7 +180,8 @@ int mrbo_eto_reduce(mrbo_plan_t* plan, const double* values, const double* grad_
                     double* eto, uint32_t flags, void* stream);
 
 /* Shard moments for the multi-GPU exchange: moments R×(2+2d+2) = [Σα, M2α, Σ∇x(d), M2∇x(d), Σ∇θ, M2∇θ]
- * over the M_local samples of this rank, M2 = Σ(x − x̄_local)² by two passes.  Ranks all-gather
+ * over the first M_local samples of each restart (the outputs keep the plan's M as the restart
+ * stride; 1 ≤ M_local ≤ M), M2 = Σ(x − x̄_local)² by two passes.  Ranks all-gather
  * (n, Σ, M2) and merge them with Chan's formula (mrbo/parallel.py merge_moments), which gives the
  * two-pass mean / std(n-1) of rollout.jl:328-339 without one-pass cancellation.            */
 int mrbo_partial_moments(mrbo_plan_t* plan, const double* values, const double* grad_x, const double* grad_theta,

@@ -93,10 +93,14 @@ static void run_case(int testfn, int d, int N, int h, int M, int R, double lo, d
   int64_t* ev = malloc(sizeof(int64_t) * 3 * T);
   rbo_params p = {h, M, R, S, 0.0, lbs, ubs, 50, 20, 1e-3, 1e-3, 1e-8, 1e-4, 1e-8, 1906, 0, 0, 1, 1, RBO_RULE_EI,
                   cost, 1.0, w};
+  double* kap = malloc(sizeof(double) * T);
+  p.kappa = kap;
   CHECK(rbo_simulate_mc(&s, &p, x0s, rn, xs, NULL, NULL, values, gx, gt, st, pol, obs, eto, ev) == 0, "mc d=%d", d);
+  p.kappa = NULL;
   int ok = 0;
-  for (int64_t t = 0; t < T; ++t) ok += (st[t] == 0) && isfinite(values[t]);
+  for (int64_t t = 0; t < T; ++t) ok += (st[t] == 0) && isfinite(values[t]) && kap[t] >= 1.0;
   CHECK(ok == T, "mc d=%d: %d of %lld trajectories ok", d, ok, (long long)T);
+  free(kap);
   /* replay the policy points just found: same values */
   if (h > 0) {
     double* rp = malloc(sizeof(double) * d * h * T);

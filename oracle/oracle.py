@@ -37,7 +37,7 @@ class Params(ctypes.Structure):
                 ("htol", ctypes.c_double), ("sigma_tol", ctypes.c_double), ("seed", ctypes.c_uint64),
                 ("sample_offset", ctypes.c_int32), ("samples_total", ctypes.c_int32),
                 ("with_gradient", ctypes.c_int32), ("nthreads", ctypes.c_int32), ("rule", ctypes.c_int32),
-                ("cost", ctypes.c_int32), ("cost_c0", ctypes.c_double), ("cost_w", _dp)]
+                ("cost", ctypes.c_int32), ("cost_c0", ctypes.c_double), ("cost_w", _dp), ("kappa", _dp)]
 
 
 def build():
@@ -194,11 +194,13 @@ def eval_base(osur, xs, theta=0.0, sigma_tol=1e-8, rule="EI", cost=None, lbs=Non
 def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=None, replay_x=None,
                 max_iters=50, max_ls=20, x_tol=1e-3, f_tol=1e-3, g_tol=1e-8, htol=1e-4, sigma_tol=1e-8,
                 seed=1906, with_gradient=True, nthreads=0, want_policy=True, sample_offset=0,
-                samples_total=0, rule="EI", ghq=None, cost=None):
+                samples_total=0, rule="EI", ghq=None, cost=None, want_kappa=False):
     """Run the oracle's simulate_trajectory_mc for every restart column of x0s (d×R).
     ghq=(nodes, weights), each M×(h+1): the Gauss–Hermite estimator (rbo_simulate_ghq) instead
     of the rnstream draws (rnstream is then only used for its M).
-    cost=(kind, c0, w): NonUniformCost weighting of the inner-solve rule (rbo_oracle.h RBO_COST_*)."""
+    cost=(kind, c0, w): NonUniformCost weighting of the inner-solve rule (rbo_oracle.h RBO_COST_*).
+    want_kappa: also return "kappa" (M×R), each trajectory's largest cond₁ of the acquisition
+    Hessians its adjoint solved with (rbo_params.kappa; 1 when none)."""
     x0s, xstarts = _f64(x0s), _f64(xstarts)
     lbs, ubs = _f64(lbs), _f64(ubs)
     d, R = x0s.shape
@@ -220,6 +222,8 @@ def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=
     prm = Params(h, M, R, xstarts.shape[1], theta, _p(lbs), _p(ubs), max_iters, max_ls, x_tol, f_tol, g_tol,
                  htol, sigma_tol, seed, sample_offset, samples_total, 1 if with_gradient else 0, nthreads,
                  RULES[rule], ck, c0, _p(cw))
+    kappa = np.zeros((M, R), order="F") if want_kappa else None
+    prm.kappa = _p(kappa)
     values = np.zeros((M, R), order="F")
     grad_x = np.zeros((d, M, R), order="F")
     grad_t = np.zeros((1, M, R), order="F")
@@ -242,4 +246,4 @@ def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=
                                    evals.ctypes.data_as(_lp))
     assert rc == 0, rc
     return dict(values=values, grad_x=grad_x, grad_theta=grad_t, status=status, policy_x=policy, obs=obs,
-                eto=eto, evals=evals)
+                eto=eto, evals=evals, kappa=kappa)

@@ -390,6 +390,22 @@ static void lu_solve(const double* LU, const int* piv, int n, double* b) {
   for (int i = 0; i < n; ++i) { double s = b[i]; for (int k = 0; k < i; ++k) s -= LU[i + n * k] * b[k]; b[i] = s; }
   for (int i = n - 1; i >= 0; --i) { double s = b[i]; for (int k = i + 1; k < n; ++k) s -= LU[i + n * k] * b[k]; b[i] = s / LU[i + n * i]; }
 }
+/* cond₁(A) = ‖A‖₁‖A⁻¹‖₁ from A (n×n) and its LU factors, by n unit solves (diagnostic only:
+ * the parity tests scale the adjoint-gradient tolerance by it) */
+static double cond1(const double* A, const double* LU, const int* piv, int n) {
+  double na = 0, ni = 0, e[16];
+  for (int j = 0; j < n; ++j) {
+    double s = 0;
+    for (int i = 0; i < n; ++i) s += fabs(A[i + n * j]);
+    na = fmax(na, s);
+    for (int i = 0; i < n; ++i) e[i] = (i == j) ? 1.0 : 0.0;
+    lu_solve(LU, piv, n, e);
+    s = 0;
+    for (int i = 0; i < n; ++i) s += fabs(e[i]);
+    ni = fmax(ni, s);
+  }
+  return na * ni;
+}
 
 /* ------------------------------------------------------------------------------------
  * FantasySurrogate (radial_basis_surrogates.jl:320-481)
@@ -621,8 +637,10 @@ static void fsur_eval(const fsur_t* fs, const double* x, double theta, double si
 }
 
 /* gp_draw(fs, x, θ; stdnormal, with_gradient=true, fantasy_index) :588-611; sx.dσ :530-539 */
+/* kappa (diagnostic, may be NULL): raised to ‖Dk(0)‖₁‖σx⁻¹‖₁, the cancellation condition of the
+ * draw covariance σx = Dk(0) − G (its rounding error is relative to Dk(0), not to σx) */
 static int fsur_draw(const fsur_t* fs, const double* x, double theta, double sigma_tol, int fi, const double* z,
-                     double* y_out, double* grad_out, sx_t* sx, scratch_t* sc) {
+                     double* y_out, double* grad_out, sx_t* sx, scratch_t* sc, double* kappa) {
   const int d = fs->d, cap = fs->cap, n = fs->N + fi + 1, D1 = d + 1;
   fsur_eval(fs, x, theta, sigma_tol, fi, 0, sx, sc);
   /* kxX = [kx'; ∇kx]  ((d+1)×n);  σx = Dk(0) - kxX*(L'\(L\kxX')) */
@@ -646,6 +664,18 @@ static int fsur_draw(const fsur_t* fs, const double* x, double theta, double sig
   /* Symmetric(σx) reads the upper triangle */
   for (int b = 0; b < D1; ++b) for (int a = b + 1; a < D1; ++a) Sig[a + D1 * b] = Sig[b + D1 * a];
   if (chol_small(Sig, D1, Ls)) return RBO_ST_DRAW_NOT_PD;
+  if (kappa) {
+    double ni = 0, e[17];
+    for (int j = 0; j < D1; ++j) {   /* column j of σx⁻¹ = Ls'\(Ls\e_j) */
+      for (int i = 0; i < D1; ++i) e[i] = (i == j) ? 1.0 : 0.0;
+      for (int i = 0; i < D1; ++i) { double t = e[i]; for (int k = 0; k < i; ++k) t -= Ls[i + D1 * k] * e[k]; e[i] = t / Ls[i + D1 * i]; }
+      for (int i = D1 - 1; i >= 0; --i) { double t = e[i]; for (int k = i + 1; k < D1; ++k) t -= Ls[k + D1 * i] * e[k]; e[i] = t / Ls[i + D1 * i]; }
+      double sc1 = 0;
+      for (int i = 0; i < D1; ++i) sc1 += fabs(e[i]);
+      ni = fmax(ni, sc1);
+    }
+    *kappa = fmax(*kappa, fmax(fabs(psi0), fabs(d2psi0)) * ni);
+  }
   double dmu[17];
   dmu[0] = sx->mu;
   for (int a = 0; a < d; ++a) dmu[a + 1] = sx->gmu[a];
@@ -950,7 +980,8 @@ typedef struct {
 } traj_in;
 
 static int run_trajectory(const traj_in* in, int r, int m, const double* x0, fsur_t* fs, scratch_t* sc,
-                          double* value, double* gx, double* gth, double* pol, double* obs_out, int64_t* evals) {
+                          double* value, double* gx, double* gth, double* pol, double* obs_out, int64_t* evals,
+                          double* kappa) {
   const rbo_params* p = in->p;
   const int d = fs->d, h = p->h, M = p->M, D1 = d + 1;
   double obs[64] = {0}, grads[64 * 16], z[17], xnext[16];
@@ -986,7 +1017,7 @@ static int run_trajectory(const traj_in* in, int r, int m, const double* x0, fsu
       for (int a = 0; a < d; ++a) grads[a + d * k] = wk * (sx.gmu[a] + SQRT2 * sx.gsig[a] * tk);
     } else {
       for (int a = 0; a < D1; ++a) z[a] = in->rnstream[(int64_t)m + (int64_t)M * a + (int64_t)M * D1 * k];
-      st |= fsur_draw(fs, xk, p->theta, p->sigma_tol, k - 1, z, &obs[k], grads + d * k, &sx, sc);
+      st |= fsur_draw(fs, xk, p->theta, p->sigma_tol, k - 1, z, &obs[k], grads + d * k, &sx, sc, kappa);
     }
     if (st) break;
     st |= fsur_condition(fs, xk, obs[k], sc->tmp);
@@ -1070,7 +1101,14 @@ static int run_trajectory(const traj_in* in, int r, int m, const double* x0, fsu
         double HT[256];
         for (int b = 0; b < d; ++b) for (int a = 0; a < d; ++a) HT[a + d * b] = sxj->Halpha[b + d * a];
         if (lu_small(HT, d, piv)) { st |= RBO_ST_SINGULAR; }
-        else lu_solve(HT, piv, d, xd);
+        else {
+          lu_solve(HT, piv, d, xd);
+          if (kappa) {
+            double A[256];
+            for (int b = 0; b < d; ++b) for (int a = 0; a < d; ++a) A[a + d * b] = sxj->Halpha[b + d * a];
+            *kappa = fmax(*kappa, cond1(A, HT, piv, d));
+          }
+        }
       }
       for (int a = 0; a < d; ++a) xbars[j][a] = xd[a];
     }
@@ -1137,8 +1175,10 @@ static int simulate_impl(const rbo_surrogate* s, const rbo_params* p, const doub
     for (int64_t tr = 0; tr < T; ++tr) {
       const int r = (int)(tr / M), m = (int)(tr % M);
       int64_t ev[3] = {0, 0, 0};
+      double* kap = p->kappa ? p->kappa + tr : NULL;
+      if (kap) *kap = 1.0;
       const int st = run_trajectory(&in, r, m, x0s + (int64_t)d * r, &fs, &sc, values + tr, grad_x + (int64_t)d * tr,
-                                    grad_theta + tr, policy_x, obs ? obs + (int64_t)(h + 1) * tr : NULL, ev);
+                                    grad_theta + tr, policy_x, obs ? obs + (int64_t)(h + 1) * tr : NULL, ev, kap);
       status[tr] = st;
       if (evals) for (int k = 0; k < 3; ++k) evals[3 * tr + k] = ev[k];
     }

@@ -74,6 +74,11 @@ typedef struct {
   int32_t cost;            /* RBO_COST_*: NonUniformCost weighting of the inner-solve rule */
   double cost_c0;          /* cost family parameters (see RBO_COST_*)            */
   const double* cost_w;    /* d weights, or NULL when cost == RBO_COST_NONE      */
+  double* kappa;           /* diagnostic output M×R, or NULL: per trajectory the largest of
+                              cond₁(H_j) = ‖H_j‖₁‖H_j⁻¹‖₁ over the adjoint solves H_j'\x̄ and
+                              ‖Dk(0)‖₁‖σx⁻¹‖₁ over the draws (the cancellation condition of the
+                              draw covariance σx = Dk(0) − G); the parity tests scale the
+                              gradient tolerance by it                                        */
 } rbo_params;
 
 /* NonUniformCost (cost_functions.jl:5-20) as closed-form families.  The reference's cost is an

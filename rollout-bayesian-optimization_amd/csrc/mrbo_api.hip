@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/mrbo.h"
+#define MRBO_API_TU
 #include "mrbo_dispatch.h"
 #include "sobol_table.h"
 
@@ -79,21 +80,23 @@ namespace {
 double g_gpfit_ms = -1.0;   // kernel time of the last mrbo_gp_fit (HIP events around the launch)
 
 // ---- kernel dispatch: one translation unit per input dimension (mrbo_kernels.hip) -------
-// fx = 1 selects the FMAX = 4 units (horizon ≤ 3, d ≤ 8), fx = 0 the FMAX = 6 ones
-#ifdef MRBO_ONLY_D
-#define MRBO_APPLY(X, a) X(a)   // expands MRBO_ONLY_D before X pastes it
-#define MRBO_FOR_D(X) MRBO_APPLY(X, MRBO_ONLY_D)
-#if MRBO_ONLY_D <= 8
-#define MRBO_FOR_DF4(X) MRBO_APPLY(X, MRBO_ONLY_D)
-#else
-#define MRBO_FOR_DF4(X)
-#endif
-#else
+// fx = 1 selects the FMAX = 4 units (horizon ≤ 3, d ≤ 8), fx = 0 the FMAX = 6 ones.  The units'
+// entry points are weak references here (mrbo_dispatch.h): null when the unit is not linked in.
 #define MRBO_FOR_D(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 #define MRBO_FOR_DF4(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
-#endif
+
+// is the unit (d, fx) linked into this library?
+bool unit_present(int d, int fx) {
+#define K6(DD) case DD: return kset_d##DD != nullptr;
+#define K4(DD) case DD: return kset_d##DD##_f4 != nullptr;
+  if (fx) { switch (d) { MRBO_FOR_DF4(K4) default: return false; } }
+  switch (d) { MRBO_FOR_D(K6) default: return false; }
+#undef K6
+#undef K4
+}
 
 bool get_kset(int d, int rpl, int fx, KernelSet& ks) {
+  if (!unit_present(d, fx)) return false;
 #define K6(DD) case DD: return kset_d##DD(rpl, ks);
 #define K4(DD) case DD: return kset_d##DD##_f4(rpl, ks);
   if (fx) { switch (d) { MRBO_FOR_DF4(K4) default: return false; } }
@@ -102,6 +105,7 @@ bool get_kset(int d, int rpl, int fx, KernelSet& ks) {
 #undef K4
 }
 
+// the launchers below are reached only through a plan whose unit get_kset found
 // start tables of the packed layouts (rpl 2 / 4), before a rollout launch with kp.batch
 void launch_tables(int d, int rpl, int fx, int nstarts, hipStream_t st, const KParams& kp) {
 #define K6(DD) case DD: launch_tables_d##DD(rpl, nstarts, st, kp); return;
@@ -150,14 +154,15 @@ int pick_grid(const void* fn, size_t fixed_bytes, size_t wave_bytes, int ncu, in
 // comp 0: values, 1..d: grad_x[a], d+1: grad_theta.  Two passes (mean, then centred squares)
 // in both modes.  mode 0: ETO (mean, std n-1) -> eto; mode 1: shard moments (Σx, M2 = Σ(x − x̄)²)
 // -> moments, merged across ranks by Chan's formula (mrbo/parallel.py).
+// M samples of each restart are reduced; Ms is the restart stride of the outputs (the plan's M)
 __global__ void __launch_bounds__(256) reduce_kernel(const double* values, const double* grad_x,
-                                                     const double* grad_theta, int M, int d, int mode,
+                                                     const double* grad_theta, int M, int Ms, int d, int mode,
                                                      double* out) {
   __shared__ double sh[256];
   const int r = blockIdx.x, comp = blockIdx.y, tid = threadIdx.x;
   const int W = 2 + 2 * d + 2;
   auto elem = [&](int m) -> double {
-    const long long idx = (long long)m + (long long)M * r;
+    const long long idx = (long long)m + (long long)Ms * r;
     if (comp == 0) return values[idx];
     if (comp <= d) return grad_x ? grad_x[idx * d + (comp - 1)] : 0.0;
     return grad_theta ? grad_theta[idx] : 0.0;
@@ -280,8 +285,8 @@ static int reduce_common(mrbo_plan_t* P, const double* values, const double* gra
                          int M, double* out, int mode, uint32_t flags, void* stream) {
   if (!P || !values || !out) return fail(MRBO_ERR_ARG, "null argument");
   hipStream_t st = (hipStream_t)stream;
-  const int d = P->d, R = P->p.R;
-  const size_t T = (size_t)M * R, W = 2 + 2 * d + 2;
+  const int d = P->d, R = P->p.R, Ms = P->p.M;
+  const size_t T = (size_t)Ms * R, W = 2 + 2 * d + 2;
   Stage sg;
   const double *dv = values, *dg = grad_x, *dt = grad_theta;
   double* dout = out;
@@ -290,7 +295,7 @@ static int reduce_common(mrbo_plan_t* P, const double* values, const double* gra
         sg.out(W * R, out, &dout))
       return fail(MRBO_ERR_NOMEM, "staging allocation failed");
   }
-  hipLaunchKernelGGL(reduce_kernel, dim3(R, d + 2), dim3(256), 0, st, dv, dg, dt, M, d, mode, dout);
+  hipLaunchKernelGGL(reduce_kernel, dim3(R, d + 2), dim3(256), 0, st, dv, dg, dt, M, Ms, d, mode, dout);
   HIP_TRY(hipGetLastError());
   if (flags & MRBO_FLAG_HOST_POINTERS) {
     HIP_TRY(hipStreamSynchronize(st));
@@ -327,6 +332,17 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   if (p->cost < MRBO_COST_NONE || p->cost > MRBO_COST_LOGLINEAR) return fail(MRBO_ERR_ARG, "cost model %d", p->cost);
   if (p->cost != MRBO_COST_NONE && !p->cost_w) return fail(MRBO_ERR_ARG, "cost model without weights");
   if (p->cost != MRBO_COST_NONE && d > MAXD) return fail(MRBO_ERR_UNSUPPORTED, "cost model at d=%d > %d", d, MAXD);
+  if (p->cost != MRBO_COST_NONE) {
+    // c(x) must stay positive and finite on the box: α/c and the certificates' bound·(1/c) flip
+    // sign otherwise (a negative bound would falsely certify a stationary point)
+    if (!(p->cost_c0 > 0.0) || !std::isfinite(p->cost_c0)) return fail(MRBO_ERR_ARG, "cost_c0=%g must be > 0", p->cost_c0);
+    for (int a = 0; a < d; ++a) {
+      if (!std::isfinite(p->cost_w[a])) return fail(MRBO_ERR_ARG, "cost weight %d is not finite", a);
+      if (p->cost == MRBO_COST_QUADRATIC && p->cost_w[a] < 0.0)
+        return fail(MRBO_ERR_ARG, "quadratic cost weight %d = %g < 0", a, p->cost_w[a]);
+      if (!(p->ubs[a] > p->lbs[a])) return fail(MRBO_ERR_ARG, "cost model needs ub > lb (dimension %d)", a);
+    }
+  }
   if (s->kernel == MRBO_KERNEL_PERIODIC && !(s->period > 0.0)) return fail(MRBO_ERR_ARG, "period %g", s->period);
   const int ldL = s->ldL > 0 ? s->ldL : N;
 
@@ -390,7 +406,8 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) { delete P; return fail(MRBO_ERR_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e)); }
   KernelSet ks;
-  P->fx = (p->h <= F4_HMAX && d <= F4_DMAX) ? 1 : 0;
+  // the FMAX = 4 unit when the horizon allows it and the library carries it
+  P->fx = (p->h <= F4_HMAX && d <= F4_DMAX && unit_present(d, 1)) ? 1 : 0;
   if (!get_kset(d, P->RPL, P->fx, ks)) {
     delete P;
     return fail(MRBO_ERR_UNSUPPORTED, "d=%d (rows per lane %d) not compiled into this library", d, P->RPL);
@@ -627,6 +644,8 @@ int mrbo_eto_reduce(mrbo_plan_t* P, const double* values, const double* grad_x, 
 
 int mrbo_partial_moments(mrbo_plan_t* P, const double* values, const double* grad_x, const double* grad_theta,
                          int32_t M_local, double* moments, uint32_t flags, void* stream) {
+  // the launch's outputs are laid out with the plan's M as the restart stride: M_local < M
+  // reduces the first M_local samples of every restart
   if (P && (M_local < 1 || M_local > P->p.M)) return fail(MRBO_ERR_ARG, "M_local=%d outside [1, %d]", M_local, P->p.M);
   return reduce_common(P, values, grad_x, grad_theta, M_local, moments, 1, flags, stream);
 }

@@ -1,0 +1,216 @@
+r"""Shared GPU-test helpers: plans and launches through libmrbo.so (mrbo.engine), the problem
+arrays of the BASELINE configurations, and the GPU-vs-oracle parity comparison (SURVEY.md §8c
+T2/T3) used by tests/test_gpu.py and tests/test_gpu_parity.py.
+
+The Julia reference cannot run here (no julia, no golden vectors in the reference), so parity
+against it is unpinned; the oracle (oracle/rbo_oracle.c, a line-by-line C restatement pinned by
+the NumPy goldens, scipy's Sobol and finite differences) stands in.
+Per trajectory t, with normwise relative errors
+   e_val(t)  = |Δ value| / max(|value|, 1e-12)
+   e_grad(t) = ‖Δ ∇x‖∞ / max(‖∇x‖∞, 1e-11·max_t ‖∇x‖∞)
+  T2 replay (the oracle replays the GPU's own policy points x_1..x_h; every trajectory):
+     e_val ≤ 1e-9;  e_grad ≤ tol(t) = max(1e-9, n·u·κ(t)), u = 2^-53, n = N + h the largest data
+     size, κ(t) the oracle's conditioning of that trajectory (rbo_params.kappa): the largest of
+     cond₁(H_j) over the adjoint solves H_j'\x̄ and ‖Dk(0)‖₁‖σx⁻¹‖₁ over the draws.  The two
+     sides sum the n-term products of the draw covariance σx = Dk(0) − G and of Hα in different
+     orders (rounding ≤ n·u relative to Dk(0) and ‖Hα‖); the draw's Cholesky and the adjoint solves
+     amplify that by κ.  No trajectory is exempt.
+  T3 end to end (both sides run the inner Newton solve):
+     flips (an x_1..x_h differing by > 1e-6·(1+|x|))                  ≤ 0.1 % of trajectories
+     identical paths (policy equal to 1e-12 relative): the T2 bounds, and equal Newton work
+     ETO: no flips → normwise 1e-9 relative per block (mean value, std value, mean ∇x);
+     flips → each mean within 3·σ/√M of the oracle's (σ the oracle's std)
+  Non-vacuity (every case; a case that only exercises the forward rollout says so with
+  kind="forward"): ≥ 25 % non-zero values, ≥ 1 % trajectories whose best observation is a
+  fantasy step (t ≥ 1, the adjoint's Case #3, rollout.jl:251-276) and adjoint perturbation pairs
+  on the GPU (> 0).  Forward cases still need non-zero values and Newton work.
+Trajectories between the two path thresholds end the Newton solve (stopped by x_tol = 1e-3, not
+at a stationary point) at iterates that differ by rounding-level drift; they are counted, and the
+replay covers their arithmetic.  The statistics of every case go to $MRBO_PARITY_REPORT (JSON).
+"""
+import os
+
+import numpy as np
+
+def _plan(g, M=None, R=None, h=None, nstarts=None, kernel=0, theta=0.0, **opts):
+    from mrbo.engine import RolloutPlan
+    M = M or g["rnstream"].shape[0]
+    R = R or g["x0s"].shape[1]
+    h = int(g["h"]) if h is None else h
+    return RolloutPlan(g["X"], g["L"], g["c"], g["y"], kernel, float(g.get("ell", 1.0)), 1e-6, float(g["fmini"]), h, M, R,
+                       nstarts or g["xstarts"].shape[1], g["lbs"], g["ubs"], theta, period=g.get("period", 1.0),
+                       **opts)
+
+
+def _run(plan, g, dual=None, replay=None, want_policy=True, with_gradient=True, rn=None, x0s=None):
+    import torch
+    from mrbo.engine import from_device, to_device
+    dev = "cuda:0"
+    out = plan.alloc_outputs(with_gradient=with_gradient, want_policy=want_policy, want_obs=True)
+    plan.simulate(to_device(g["x0s"] if x0s is None else x0s, dev),
+                  to_device(g["rnstream"] if rn is None else rn, dev),
+                  to_device(g["xstarts"], dev), out,
+                  dual_y_dx=None if dual is None else to_device(dual, dev),
+                  replay_x=None if replay is None else to_device(replay, dev))
+    eto = plan.eto(out)
+    torch.cuda.synchronize()
+    d, M, R, h = plan.d, plan.M, plan.R, plan.h
+    res = dict(values=from_device(out["values"], (M, R)), status=from_device(out["status"], (M, R)),
+               obs=from_device(out["obs"], (h + 1, M, R)), eto=from_device(eto, (2 + 2 * d + 2, R)),
+               evals=from_device(out["evals"], (5, M, R)))
+    if with_gradient:
+        res["grad_x"] = from_device(out["grad_x"], (d, M, R))
+        res["grad_theta"] = from_device(out["grad_theta"], (1, M, R))
+    if want_policy:
+        res["policy_x"] = from_device(out["policy_x"], (d, h + 1, M, R))
+    return res
+
+
+def _osur(oracle, g, kernel="matern52"):
+    return oracle.OracleSurrogate(g["X"], g["L"], g["c"], g["y"], kernel=kernel, ell=float(g.get("ell", 1.0)),
+                                  fmini=float(g["fmini"]), period=float(g.get("period", 1.0)))
+
+
+def _assert_grads_close(a, b, rtol=1e-6):
+    if b.size == 0:
+        return
+    scale = max(np.abs(b).max(), 1e-300)
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=1e-9 * scale)
+
+
+def _problem_arrays(name, M, R, kernel=None, testfn=None, d=None, N=None, h=None, ell=None):
+    from mrbo import configs
+    from mrbo.kernels import Matern12, Matern32, Matern52, Periodic, SquaredExponential
+    if testfn is not None:
+        cfg = configs.Config(f"T{testfn}{d}", testfn, d, h, M, R, N, 1)
+        pb = configs.Problem(cfg)
+    else:
+        pb = configs.problem(name, M=M, R=R)
+    s = pb.surrogate
+    if kernel is not None:
+        # Periodic: a period beyond twice the box diagonal (Branin: 21) and an effective
+        # lengthscale ℓp/2π ≈ 1 below the design spacing keep K well conditioned
+        s.set_kernel({"matern32": Matern32(), "matern12": Matern12(), "se": SquaredExponential(),
+                      "periodic": Periodic([0.125, 50.0])}[kernel])
+    if ell is not None:
+        s.set_kernel(Matern52([ell]))
+    n = s.observed
+    return dict(X=s.X[:, :n], L=s.L[:n, :n], c=s.c[:n], y=s.y[:n], fmini=s.fmini(), lbs=pb.lbs, ubs=pb.ubs,
+                x0s=pb.x0s, rnstream=pb.tp.rnstream_sequence, xstarts=pb.es.get_starts(), h=pb.cfg.h,
+                ell=s.ψ.lengthscale, period=s.ψ.period)
+
+
+FLIP_MAX = 1e-3
+GRAD_ATOL_SCALE = 1e-11
+_REPORT = {}
+
+
+def _threads():
+    try:
+        return min(16, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return 8
+
+
+def _errs(r, o, gscale):
+    """per-trajectory normwise relative errors (e_val, e_grad), flat over (m, r)"""
+    ev = np.abs(r["values"] - o["values"]) / np.maximum(np.abs(o["values"]), 1e-12)
+    dg = np.abs(r["grad_x"] - o["grad_x"]).max(axis=0)
+    ng = np.maximum(np.abs(o["grad_x"]).max(axis=0), GRAD_ATOL_SCALE * gscale)
+    return ev.ravel(order="F"), (dg / ng).ravel(order="F")
+
+
+def _summ(e, tol=None):
+    if e.size == 0:
+        return dict(max=0.0, p999=0.0, over_1e9=0, over_1e8=0, over_tol=0, max_over_tol=0.0)
+    out = dict(max=float(e.max()), p999=float(np.quantile(e, 0.999)), over_1e9=int((e > 1e-9).sum()),
+               over_1e8=int((e > 1e-8).sum()))
+    if tol is not None:
+        out.update(over_tol=int((e > tol).sum()), max_over_tol=float((e / tol).max()))
+    return out
+
+
+def _blocknorm(a, b):
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def grad_tolerance(kappa, n):
+    """T2 per-trajectory gradient bound max(1e-9, n·u·κ) (module docstring)"""
+    return np.maximum(1e-9, n * 2.0 ** -53 * np.asarray(kappa, dtype=np.float64))
+
+
+def _coverage(r, o):
+    """what a case exercises: non-zero values, t ≥ 1 (best observation at a fantasy step), adjoint
+    pairs and Newton work on the GPU, non-zero gradients"""
+    v = o["values"].ravel(order="F")
+    tb = np.argmin(o["obs"], axis=0).ravel(order="F")
+    ev = r["evals"].reshape(5, -1, order="F")
+    nzg = np.abs(o["grad_x"]).max(axis=0).ravel(order="F") > 0
+    return dict(nonzero_values=float((v > 0).mean()), t_ge_1=float(((tb >= 1) & (v > 0)).mean()),
+                nonzero_grads=float(nzg.mean()), gpu_pairs=int(ev[4].sum()), gpu_rich=int(ev[3].sum()),
+                gpu_grad_evals=int(ev[0].sum()), gpu_hessians=int(ev[2].sum()))
+
+
+def _compare(key, g, r, o, o_replay, M, kind="full"):
+    """The T2 / T3 assertions above and the non-vacuity guard; records the measured statistics
+    under `key`."""
+    assert kind in ("full", "forward")
+    assert (r["status"] == 0).all() and (o["status"] == 0).all() and (o_replay["status"] == 0).all()
+    dx = np.abs(r["policy_x"] - o["policy_x"]) / (1 + np.abs(o["policy_x"]))
+    dxt = dx.max(axis=(0, 1)).ravel(order="F")
+    flip, exact = dxt > 1e-6, dxt <= 1e-12
+    gscale = max(float(np.abs(o["grad_x"]).max()), 1e-300)
+    ev2, eg2 = _errs(r, o_replay, gscale)
+    ev3, eg3 = _errs(r, o, gscale)
+    d, N = g["X"].shape
+    tol = grad_tolerance(o_replay["kappa"].ravel(order="F"), N + int(g["h"]))
+    evals_r = r["evals"][:3].reshape(3, -1, order="F")
+    evals_o = o["evals"].reshape(3, -1, order="F")
+    e_r, e_o = r["eto"], o["eto"]
+    cov = _coverage(r, o)
+    stats = dict(kind=kind, coverage=cov, trajectories=int(dxt.size), flips=int(flip.sum()),
+                 drift=int((~flip & ~exact).sum()), identical=int(exact.sum()), flip_fraction=float(flip.mean()),
+                 kappa_max=float(o_replay["kappa"].max()), grad_tol_max=float(tol.max()),
+                 replay_value=_summ(ev2), replay_grad=_summ(eg2, tol),
+                 identical_value=_summ(ev3[exact]), identical_grad=_summ(eg3[exact], tol[exact]),
+                 work_equal_identical=bool(np.array_equal(evals_r[:, exact], evals_o[:, exact])),
+                 eto_mean_value_rel=_blocknorm(e_r[0], e_o[0]), eto_std_value_rel=_blocknorm(e_r[1], e_o[1]),
+                 eto_mean_grad_rel=_blocknorm(e_r[2:2 + d], e_o[2:2 + d]))
+    sd_o = np.concatenate([e_o[1:2], e_o[2 + d:2 + 2 * d]])
+    dev = np.abs(np.concatenate([e_r[0:1], e_r[2:2 + d]]) - np.concatenate([e_o[0:1], e_o[2:2 + d]]))
+    stats["eto_mean_max_in_se"] = float(np.max(dev / np.maximum(sd_o / np.sqrt(M), 1e-300)))
+    _REPORT[key] = stats
+    # non-vacuity
+    assert cov["nonzero_values"] >= 0.25 and cov["gpu_grad_evals"] > 0, stats
+    if kind == "full":
+        assert cov["t_ge_1"] >= 0.01 and cov["gpu_pairs"] > 0, stats
+    # T2
+    assert stats["replay_value"]["max"] <= 1e-9, stats
+    assert stats["replay_grad"]["over_tol"] == 0, stats
+    # T3
+    assert stats["flip_fraction"] <= FLIP_MAX, stats
+    assert stats["identical_value"]["max"] <= 1e-9, stats
+    assert stats["identical_grad"]["over_tol"] == 0, stats
+    assert stats["work_equal_identical"], stats
+    if not flip.any():
+        assert max(stats["eto_mean_value_rel"], stats["eto_std_value_rel"], stats["eto_mean_grad_rel"]) <= 1e-9, stats
+    else:
+        assert np.all(dev <= 3 * sd_o / np.sqrt(M) + 1e-14), stats
+    return stats
+
+
+def _end_to_end(oracle, key, g, M, cost=None, plan_opts=None, kind="full", htol=1e-4):
+    opts = dict(plan_opts or {})
+    if htol != 1e-4:
+        opts["htol"] = htol
+    r = _run(_plan(g, **opts), g)
+    nt = _threads()
+    kw = dict(nthreads=nt, cost=cost, htol=htol)
+    o = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
+                           **kw)
+    rp = np.asfortranarray(r["policy_x"][:, 1:])
+    o2 = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
+                            replay_x=rp, want_policy=False, want_kappa=True, **kw)
+    return _compare(key, g, r, o, o2, M, kind=kind)
+
+

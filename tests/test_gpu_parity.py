@@ -4,20 +4,8 @@ The Julia reference cannot run here (no julia, no golden vectors in the referenc
 against it is unpinned; the oracle (oracle/rbo_oracle.c, a line-by-line C restatement pinned by
 the NumPy goldens, scipy's Sobol and finite differences) stands in, and these tests hold the GPU
 to it EXHAUSTIVELY at the headline size and per full restart of the other configurations.
-Per trajectory t, with normwise relative errors
-   e_val(t)  = |Δ value| / max(|value|, 1e-12)
-   e_grad(t) = ‖Δ ∇x‖∞ / max(‖∇x‖∞, 1e-11·max_t ‖∇x‖∞)
-  T2 replay (the oracle replays the GPU's own policy points x_1..x_h; every trajectory):
-     e_val ≤ 1e-9 for all; e_grad ≤ 1e-9 for ≥ 99.9 %, ≤ 1e-7 for all (the adjoint solves with
-     the acquisition Hessians: their conditioning amplifies summation-order rounding)
-  T3 end to end (both sides run the inner Newton solve):
-     flips (an x_1..x_h differing by > 1e-6·(1+|x|))                  ≤ 0.1 % of trajectories
-     identical paths (policy equal to 1e-12 relative): the T2 bounds, and equal Newton work
-     ETO: no flips → normwise 1e-9 relative per block (mean value, std value, mean ∇x);
-     flips → each mean within 3·σ/√M of the oracle's (σ the oracle's std)
-Trajectories between the two path thresholds end the Newton solve (stopped by x_tol = 1e-3, not
-at a stationary point) at iterates that differ by rounding-level drift; they are counted, and the
-replay covers their arithmetic.  The statistics of every case go to $MRBO_PARITY_REPORT (JSON).
+The tolerances, the non-vacuity guard and the statistics recorded per case are defined in
+tests/parity.py; $MRBO_PARITY_REPORT names the JSON file the statistics of every case go to.
 """
 import json
 import os
@@ -28,14 +16,9 @@ import numpy as np
 import pytest
 
 from conftest import ROOT
-from test_gpu import _osur, _plan, _problem_arrays, _run
+from parity import _REPORT, _end_to_end, _plan, _problem_arrays, _run
 
 pytestmark = pytest.mark.gpu
-
-FLIP_MAX = 1e-3
-GRAD_ATOL_SCALE = 1e-11
-_REPORT = {}
-
 
 @pytest.fixture(scope="module", autouse=True)
 def _parity_report():
@@ -44,83 +27,6 @@ def _parity_report():
     if path and _REPORT:
         with open(path, "w") as f:
             json.dump(_REPORT, f, indent=1, sort_keys=True)
-
-
-def _threads():
-    try:
-        return min(16, len(os.sched_getaffinity(0)))
-    except AttributeError:
-        return 8
-
-
-def _errs(r, o, gscale):
-    """per-trajectory normwise relative errors (e_val, e_grad), flat over (m, r)"""
-    ev = np.abs(r["values"] - o["values"]) / np.maximum(np.abs(o["values"]), 1e-12)
-    dg = np.abs(r["grad_x"] - o["grad_x"]).max(axis=0)
-    ng = np.maximum(np.abs(o["grad_x"]).max(axis=0), GRAD_ATOL_SCALE * gscale)
-    return ev.ravel(order="F"), (dg / ng).ravel(order="F")
-
-
-def _summ(e):
-    if e.size == 0:
-        return dict(max=0.0, p999=0.0, over_1e9=0, over_1e8=0)
-    return dict(max=float(e.max()), p999=float(np.quantile(e, 0.999)), over_1e9=int((e > 1e-9).sum()),
-                over_1e8=int((e > 1e-8).sum()))
-
-
-def _blocknorm(a, b):
-    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
-
-
-def _compare(key, g, r, o, o_replay, M):
-    """The T2 / T3 assertions above; records the measured statistics under `key`."""
-    assert (r["status"] == 0).all() and (o["status"] == 0).all() and (o_replay["status"] == 0).all()
-    dx = np.abs(r["policy_x"] - o["policy_x"]) / (1 + np.abs(o["policy_x"]))
-    dxt = dx.max(axis=(0, 1)).ravel(order="F")
-    flip, exact = dxt > 1e-6, dxt <= 1e-12
-    gscale = max(float(np.abs(o["grad_x"]).max()), 1e-300)
-    ev2, eg2 = _errs(r, o_replay, gscale)
-    ev3, eg3 = _errs(r, o, gscale)
-    evals_r = r["evals"][:3].reshape(3, -1, order="F")
-    evals_o = o["evals"].reshape(3, -1, order="F")
-    d = g["X"].shape[0]
-    e_r, e_o = r["eto"], o["eto"]
-    stats = dict(trajectories=int(dxt.size), flips=int(flip.sum()), drift=int((~flip & ~exact).sum()),
-                 identical=int(exact.sum()), flip_fraction=float(flip.mean()),
-                 replay_value=_summ(ev2), replay_grad=_summ(eg2),
-                 identical_value=_summ(ev3[exact]), identical_grad=_summ(eg3[exact]),
-                 work_equal_identical=bool(np.array_equal(evals_r[:, exact], evals_o[:, exact])),
-                 eto_mean_value_rel=_blocknorm(e_r[0], e_o[0]), eto_std_value_rel=_blocknorm(e_r[1], e_o[1]),
-                 eto_mean_grad_rel=_blocknorm(e_r[2:2 + d], e_o[2:2 + d]))
-    sd_o = np.concatenate([e_o[1:2], e_o[2 + d:2 + 2 * d]])
-    dev = np.abs(np.concatenate([e_r[0:1], e_r[2:2 + d]]) - np.concatenate([e_o[0:1], e_o[2:2 + d]]))
-    stats["eto_mean_max_in_se"] = float(np.max(dev / np.maximum(sd_o / np.sqrt(M), 1e-300)))
-    _REPORT[key] = stats
-    # T2
-    assert stats["replay_value"]["max"] <= 1e-9, stats
-    assert stats["replay_grad"]["over_1e9"] <= 1e-3 * dxt.size and stats["replay_grad"]["max"] <= 1e-7, stats
-    # T3
-    assert stats["flip_fraction"] <= FLIP_MAX, stats
-    assert stats["identical_value"]["max"] <= 1e-9, stats
-    assert stats["identical_grad"]["over_1e9"] <= 1e-3 * dxt.size and stats["identical_grad"]["max"] <= 1e-7, stats
-    assert stats["work_equal_identical"], stats
-    if not flip.any():
-        assert max(stats["eto_mean_value_rel"], stats["eto_std_value_rel"], stats["eto_mean_grad_rel"]) <= 1e-9, stats
-    else:
-        assert np.all(dev <= 3 * sd_o / np.sqrt(M) + 1e-14), stats
-    return stats
-
-
-def _end_to_end(oracle, key, g, M, cost=None, plan_opts=None):
-    r = _run(_plan(g, **(plan_opts or {})), g)
-    nt = _threads()
-    kw = dict(nthreads=nt, cost=cost)
-    o = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
-                           **kw)
-    rp = np.asfortranarray(r["policy_x"][:, 1:])
-    o2 = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
-                            replay_x=rp, want_policy=False, **kw)
-    return _compare(key, g, r, o, o2, M)
 
 
 def test_full_size_c3_vs_oracle(gpu, oracle):
@@ -140,18 +46,30 @@ def _mle_arrays(name, M, R):
     return _problem_arrays(name, M, R, ell=ell), ell
 
 
-@pytest.mark.parametrize("name,R,ell", [("C4", 1, None), ("C5", 1, None), ("C5", 1, 20.0), ("C3", 4, "mle"),
-                                        ("C4", 1, "mle")])
-def test_full_restart_vs_oracle(gpu, oracle, name, R, ell):
+# (config, restarts, lengthscale, kind, htol).  At ℓ = 1 Hartmann-6 at N = 128 never improves on
+# fmini (every C4 value is 0) and C4's MLE ℓ barely does, so C4 runs at ℓ = 0.5 (94 % non-zero
+# values, the N = 128 resolution and adjoint at scale) and its MLE case is forward-only.  At C5
+# the reference's det(H) < 1e-4 test (Q4, rollout.jl:159-161) zeroes almost every x-dual at
+# d = 8; ℓ = 1 is therefore forward-only, and the Q4-off diagnostic (htol = -∞ on both sides,
+# not the reference's behaviour) runs the d = 8 back-substitution on real x-duals.
+RESTART_CASES = [("C4", 1, 0.5, "full", 1e-4), ("C4", 1, "mle", "forward", 1e-4), ("C5", 1, None, "forward", 1e-4),
+                 ("C5", 1, 20.0, "full", 1e-4), ("C5", 1, 20.0, "full", -np.inf), ("C3", 4, "mle", "full", 1e-4)]
+
+
+@pytest.mark.parametrize("name,R,ell,kind,htol", RESTART_CASES)
+def test_full_restart_vs_oracle(gpu, oracle, name, R, ell, kind, htol):
     """One full restart (1 024 MC samples) of C4 and C5, C5 also at a lengthscale at its design
     spacing (ℓ = 20: its MLE within the reference's bounds stays at ℓ = 1, the likelihood being
     flat there), and C3 / C4 at their MLE lengthscales -- surfaces where the Newton solve and the
-    adjoint do real work."""
+    adjoint do real work (see RESTART_CASES)."""
     if ell == "mle":
         g, ell_v = _mle_arrays(name, 1024, R)
     else:
         g, ell_v = _problem_arrays(name, 1024, R, ell=ell), (ell or 1.0)
-    _end_to_end(oracle, f"{name} restart (1024 x {R}, l={ell_v:.4g})", g, 1024)
+    q4 = "" if htol == 1e-4 else ", Q4 off"
+    st = _end_to_end(oracle, f"{name} restart (1024 x {R}, l={ell_v:.4g}{q4}, {kind})", g, 1024, kind=kind, htol=htol)
+    if htol != 1e-4:    # the diagnostic's purpose: the d = 8 adjoint on non-zero x-duals
+        assert st["coverage"]["nonzero_grads"] >= 0.5, st
 
 
 @pytest.mark.parametrize("name,M,R,ell", [("C2", 64, 4, None), ("C3", 64, 4, None), ("C5", 16, 1, 20.0)])
@@ -198,6 +116,17 @@ def test_device_moments_merge_equals_eto_reduce(gpu):
     np.testing.assert_allclose(e, r["eto"], rtol=1e-12, atol=1e-16)
     with pytest.raises(Exception):     # M_local outside [1, M]
         q.partial_moments(out, M + 5)
+    # M_local < the plan's M: the first M_local samples of every restart (the outputs keep the
+    # plan's M as the restart stride)
+    Mq, ml = hi - lo, 7
+    mom = q.partial_moments(out, ml)
+    torch.cuda.synchronize()
+    mom = mom.cpu().numpy().reshape((width(d), R), order="F")
+    vals = out["values"].cpu().numpy().reshape((Mq, R), order="F")[:ml]
+    gx = out["grad_x"].cpu().numpy().reshape((d, Mq, R), order="F")[:, :ml]
+    np.testing.assert_allclose(mom[0], vals.sum(0), rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(mom[1], ((vals - vals.mean(0)) ** 2).sum(0), rtol=1e-10, atol=1e-300)
+    np.testing.assert_allclose(mom[2:2 + d], gx.sum(1), rtol=1e-10, atol=1e-14)
 
 
 def _bench(args, env):

@@ -60,6 +60,31 @@ def test_plan_create_rejects_unsupported_shapes(d, N, msg):
     assert rc == -2 and msg in L.mrbo_last_error()
 
 
+@pytest.mark.parametrize("kind,c0,w,ub,msg", [
+    (1, 0.0, 1.0, 1.0, b"cost_c0"), (2, -1.0, 1.0, 1.0, b"cost_c0"), (1, float("nan"), 1.0, 1.0, b"cost_c0"),
+    (1, 1.0, -0.5, 1.0, b"quadratic cost weight"), (2, 1.0, float("inf"), 1.0, b"not finite"),
+    (1, 1.0, 1.0, 0.0, b"ub > lb")])
+def test_plan_create_rejects_non_positive_cost_models(kind, c0, w, ub, msg):
+    """NonUniformCost models that are not positive on the box (c0 ≤ 0, negative quadratic weights,
+    non-finite parameters, ub ≤ lb) are refused with MRBO_ERR_ARG before any device call: α/c and
+    the gradient certificates' bound·(1/c) would flip sign and could certify a non-stationary point."""
+    from mrbo import _lib
+    L = _lib.load()
+    dp = ctypes.POINTER(ctypes.c_double)
+    d, N = 2, 4
+    X = np.zeros((d, N), order="F")
+    Lm = np.eye(N, order="F")
+    c = np.zeros(N)
+    sd = _lib.SurrogateDesc(d, N, 0, 1.0, 1e-6, 0.0, X.ctypes.data_as(dp), Lm.ctypes.data_as(dp), N,
+                            c.ctypes.data_as(dp), c.ctypes.data_as(dp))
+    lb, ubs, cw = np.zeros(d), np.full(d, ub), np.full(d, w)
+    pd = _lib.ParamsDesc(2, 8, 2, 18, 0, 0.0, lb.ctypes.data_as(dp), ubs.ctypes.data_as(dp), 50, 20, 1e-3, 1e-3,
+                         1e-8, 1e-4, 1e-8, 1906, 0, 0, kind, c0, cw.ctypes.data_as(dp))
+    h = ctypes.c_void_p()
+    rc = L.mrbo_plan_create(ctypes.byref(sd), ctypes.byref(pd), 0, ctypes.byref(h))
+    assert rc == -1 and msg in L.mrbo_last_error(), (rc, L.mrbo_last_error())
+
+
 def test_kronecker_matches_oracle(oracle):
     from mrbo.utils import kronecker_quasirand
     for d, N, s in [(1, 8, 0), (2, 32, 0), (6, 64, 64), (8, 16, 3)]:
