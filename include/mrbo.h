@@ -191,6 +191,17 @@ int mrbo_partial_moments(mrbo_plan_t* plan, const double* values, const double* 
  * [μ, σ, α, ∇μ(d), ∇σ(d), ∇α(d), Hα(d×d col-major), d2α/dxdθ(d)].                       */
 int mrbo_eval_base(mrbo_plan_t* plan, int32_t P, const double* xs, double* out, uint32_t flags, void* stream);
 
+/* base_solve(s::Surrogate; spatial_lbs, spatial_ubs, xstart, θfixed) rbf_optim.jl:35-66 for each
+ * of n starts (columns of xstarts, d×n; any n ≥ 1) on the plan's BASE surrogate, with the plan's
+ * rule, θ, box and solver options (the build's projected Newton, DESIGN.md §3, as the rollout's
+ * inner solve): xmin d×n = the minimizers, fmin n = the minima of −α, status n (MRBO_ST_* bits
+ * except ALL_NAN), evals MRBO_NCOUNTERS×n or NULL.  One wavefront per start.  The caller takes
+ * multistart_base_solve!'s findmin over the candidates (rbf_optim.jl:103-135: drop minimizers
+ * with a NaN, a NaN minimum wins, else the first minimum) -- mrbo/rbf_optim.py does.  Arrays are
+ * device pointers unless MRBO_FLAG_HOST_POINTERS; launches on `stream` without synchronising. */
+int mrbo_base_solve(mrbo_plan_t* plan, int32_t n, const double* xstarts, double* xmin, double* fmin, int32_t* status,
+                    int64_t* evals, uint32_t flags, void* stream);
+
 /* Base-GP fit at P hyperparameter vectors θ_p = thetas[p·nt .. p·nt+nt−1] (kernel, σn2, X d×N,
  * y N from s; s->L, s->c unused) -- the evaluations behind optimize!'s fg! (r_b_s.jl:810-814):
  * K = Ψ(‖Xi−Xj‖; θ_p)+σn2·I, L = chol(K), c = L'\(L\y), and

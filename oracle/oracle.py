@@ -81,6 +81,8 @@ def lib():
                                                ctypes.c_double, ctypes.c_double, _dp, _dp, _dp, _dp, _dp, _dp]
         L.rbo_simulate_ghq.argtypes = [ctypes.POINTER(Surrogate), ctypes.POINTER(Params), _dp, _dp, _dp, _dp, _dp,
                                        _dp, _dp, _dp, _dp, _ip, _dp, _dp, _dp, _lp]
+        L.rbo_base_solve.argtypes = [ctypes.POINTER(Surrogate), ctypes.POINTER(Params), ctypes.c_int32, _dp, _dp,
+                                     _dp, _ip, _lp]
         _lib = L
     return _lib
 
@@ -247,3 +249,21 @@ def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=
     assert rc == 0, rc
     return dict(values=values, grad_x=grad_x, grad_theta=grad_t, status=status, policy_x=policy, obs=obs,
                 eto=eto, evals=evals, kappa=kappa)
+
+
+def base_solve(osur, xstarts, lbs, ubs, theta=0.0, rule="EI", max_iters=50, max_ls=20, x_tol=1e-3, f_tol=1e-3,
+               g_tol=1e-8, sigma_tol=1e-8):
+    """base_solve(s; xstart) from every column of xstarts (d×n) on the base surrogate (rbo_base_solve):
+    (xmin d×n, fmin n, status n, evals 3×n)."""
+    xstarts, lbs, ubs = _f64(xstarts), _f64(lbs).ravel(), _f64(ubs).ravel()
+    d, n = xstarts.shape
+    prm = Params(0, 1, 1, n, theta, _p(lbs), _p(ubs), max_iters, max_ls, x_tol, f_tol, g_tol, 1e-4, sigma_tol, 0, 0,
+                 0, 0, 1, RULES[rule], 0, 1.0, None)
+    xmin = np.zeros((d, n), order="F")
+    fmin = np.zeros(n)
+    status = np.zeros(n, dtype=np.int32)
+    evals = np.zeros((3, n), dtype=np.int64, order="F")
+    rc = lib().rbo_base_solve(ctypes.byref(osur.s), ctypes.byref(prm), n, _p(xstarts), _p(xmin), _p(fmin),
+                              status.ctypes.data_as(_ip), evals.ctypes.data_as(_lp))
+    assert rc == 0, rc
+    return xmin, fmin, status, evals

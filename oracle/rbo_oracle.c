@@ -767,7 +767,7 @@ static void newton_solve(solve_ctx* cx, const double* xs, double* xout, double* 
   const fsur_t* fs = cx->fs;
   const rbo_params* p = cx->p;
   const int d = fs->d;
-  double x[16], g[16], H[256], xt[16], pdir[16], Hs[256], Lc[256];
+  double x[16] = {0}, g[16], H[256], xt[16], pdir[16], Hs[256], Lc[256];
   sx_t sx;
   int free_[16];
   for (int a = 0; a < d; ++a) x[a] = clampd(xs[a], p->lbs[a], p->ubs[a]);
@@ -1342,6 +1342,41 @@ static int eval_base_impl(const rbo_surrogate* s, int32_t rule, double theta, do
     for (int a = 0; a < d; ++a) { o[3 + a] = sx.gmu[a]; o[3 + d + a] = sx.gsig[a]; o[3 + 2 * d + a] = sx.galpha[a]; }
     for (int q = 0; q < d * d; ++q) o[3 + 3 * d + q] = sx.Halpha[q];
     for (int a = 0; a < d; ++a) o[3 + 3 * d + d * d + a] = sx.mixed[a];
+  }
+  scratch_free(&sc);
+  fsur_free(&fs);
+  return 0;
+}
+
+/* base_solve(s::Surrogate; xstart) rbf_optim.jl:35-66 for every column of xstarts (d×n) on the
+ * base surrogate (fantasy index -1): the build's projected Newton (newton_solve) with p's rule,
+ * θ, box and options; the caller's findmin over the candidates is multistart_base_solve!(s, …)
+ * (:103-135).  evals: optional 3×n [gradient, value, Hessian] counts. */
+int rbo_base_solve(const rbo_surrogate* s, const rbo_params* p, int32_t n, const double* xstarts, double* xmin,
+                   double* fmin, int32_t* status, int64_t* evals) {
+  fsur_t fs;
+  scratch_t sc;
+  if (!s || !p || n < 1 || p->rule < 0 || p->rule > RBO_RULE_LCB) return -1;
+  if (fsur_alloc(&fs, s, 0, p->rule, p)) return -2;
+  scratch_alloc(&sc, fs.cap, s->d);
+  const int d = s->d;
+  double cabs = 0;
+  for (int j = 0; j < s->N; ++j) cabs += fabs(fs.cs[j]);
+  for (int i = 0; i < n; ++i) {
+    solve_ctx cx;
+    memset(&cx, 0, sizeof cx);
+    cx.fs = &fs;
+    cx.p = p;
+    cx.fi = -1;
+    cx.sc = &sc;
+    cx.cabs = cabs;
+    newton_solve(&cx, xstarts + (int64_t)d * i, xmin + (int64_t)d * i, fmin + i);
+    status[i] = cx.st;
+    if (evals) {
+      evals[3 * (int64_t)i + 0] = cx.n_grad;
+      evals[3 * (int64_t)i + 1] = cx.n_value;
+      evals[3 * (int64_t)i + 2] = cx.n_hess;
+    }
   }
   scratch_free(&sc);
   fsur_free(&fs);

@@ -111,6 +111,13 @@ int rbo_eval_base(const rbo_surrogate* s, int32_t rule, double theta, double sig
  * ∇, H and ∂∇/∂θ; p->lbs / p->ubs define u).                                              */
 int rbo_eval_base_p(const rbo_surrogate* s, const rbo_params* p, int32_t P, const double* xs, double* out);
 
+/* base_solve(s::Surrogate; xstart) (rbf_optim.jl:35-66) from each column of xstarts (d×n) on the
+ * base surrogate with p's rule, θ, box and solver options: xmin d×n, fmin n (minima of −α),
+ * status n, evals 3×n [gradient, value, Hessian] (optional).  The findmin of
+ * multistart_base_solve!(s, …) (:103-135) is the caller's. */
+int rbo_base_solve(const rbo_surrogate* s, const rbo_params* p, int32_t n, const double* xstarts, double* xmin,
+                   double* fmin, int32_t* status, int64_t* evals);
+
 /* simulate_trajectory_mc (rollout.jl:279-340) for R restarts x0s (d×R).
  * Outputs (caller-allocated, Julia layout):
  *   values   M×R, grad_x d×M×R, grad_theta 1×M×R, status M×R,

@@ -678,6 +678,54 @@ int mrbo_eval_base(mrbo_plan_t* P, int32_t npts, const double* xs, double* out, 
   return MRBO_OK;
 }
 
+int mrbo_base_solve(mrbo_plan_t* P, int32_t n, const double* xstarts, double* xmin, double* fmin, int32_t* status,
+                    int64_t* evals, uint32_t flags, void* stream) {
+  if (!P || !xstarts || !xmin || !fmin || !status || n < 1) return fail(MRBO_ERR_ARG, "bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipSetDevice(P->device) != hipSuccess) return fail(MRBO_ERR_HIP, "hipSetDevice");
+  const int d = P->d;
+  KParams kp;
+  fill_common(P, kp);
+  // one launch item per start, on the base surrogate; no trajectory, no start tables (the
+  // per-workgroup LDS layout shrinks to L0⁻¹ + the wave areas, within the plan's smem)
+  kp.base_solve = 1;
+  kp.nstarts = n;
+  kp.M = n;
+  kp.R = 1;
+  kp.T = n;
+  kp.with_gradient = 0;
+  kp.xs_lds = 0;
+  kp.batch = 0;
+  Stage sg;
+  const double* dxs = xstarts;
+  double *dx = xmin, *df = fmin;
+  int32_t* dst = status;
+  int64_t* dev = evals;
+  const bool host = flags & MRBO_FLAG_HOST_POINTERS;
+  if (host) {
+    if (sg.in(xstarts, (size_t)d * n, &dxs) || sg.out((size_t)d * n, xmin, &dx) || sg.out((size_t)n, fmin, &df) ||
+        sg.out((size_t)n, status, &dst) || sg.out((size_t)NCOUNT * n, evals, &dev))
+      return fail(MRBO_ERR_NOMEM, "staging allocation failed");
+  }
+  kp.xstarts = dxs;
+  kp.policy = dx;
+  kp.values = df;
+  kp.status = (int*)dst;
+  kp.evals = (long long*)dev;
+  HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * 4, st));
+  const int blocks = std::min(P->blocks, (n + P->wpg - 1) / P->wpg);
+  launch_rollout(d, P->RPL, P->fx, P->spec, dim3(blocks), dim3(P->wpg * WAVE), P->smem, st, kp);
+  HIP_TRY(hipGetLastError());
+  if (host) {
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipMemcpy(xmin, dx, sizeof(double) * d * n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(fmin, df, sizeof(double) * n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(status, dst, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    if (evals) HIP_TRY(hipMemcpy(evals, dev, sizeof(int64_t) * NCOUNT * n, hipMemcpyDeviceToHost));
+  }
+  return MRBO_OK;
+}
+
 int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const double* thetas, double* ll,
                       double* grad, int32_t* status, double* L_out, double* c_out, uint32_t flags, void* stream) {
   if (!s || !thetas || !ll || !grad || !status || np < 1) return fail(MRBO_ERR_ARG, "null argument");

@@ -92,6 +92,10 @@ struct KParams {
   int cost;
   double cost_c0;
   const double* cost_tab;   // device [lb (d), del = ub − lb (d), w (d)]
+  // mrbo_base_solve: item k of the launch = base_solve(s::Surrogate; xstart = column k of
+  // xstarts) on the base surrogate (rbf_optim.jl:35-66); minimizer -> policy (d×T), minimum ->
+  // values (T), no trajectory
+  int base_solve;
 };
 
 

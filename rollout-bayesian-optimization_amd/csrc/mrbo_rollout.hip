@@ -1699,10 +1699,12 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   varneg = __ballot(act && var < 0.0) != 0;
 }
 
-// multistart_base_solve!(fs, …) rbf_optim.jl:68-101 -> U[U_XB]
+// multistart_base_solve!(fs, …) rbf_optim.jl:68-101 -> U[U_XB], over the starts k0 ≤ k < k1.
+// kp.base_solve: one start per launch item, whose (minimizer, minimum) is the output -- the
+// candidate list multistart_base_solve!(s::Surrogate, …) (:103-135) takes its findmin over.
 template <int D, int RPL>
 __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp, int S, Counters& nevals,
-                                          LaneRes<D, RPL>& lr) {
+                                          LaneRes<D, RPL>& lr, int k0, int k1) {
   using Ly = Lay<D, RPL>;
   double* U = W.U;
   const int lane = W.ln();
@@ -1731,12 +1733,16 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
     wave_sync();
   }
   // starts that need a Newton iteration, in index order (all of them without kp.batch)
-  for (int k = 0; k < kp.nstarts; ++k) {
+  for (int k = k0; k < k1; ++k) {
     if ((stopmask >> k) & 1ull) continue;
     const double fo = kp.batch ? newton<D, RPL>(W, kp, S, k, nevals, st, lr, readlane_d(f_lane, k), true,
                                                 readlane_d(gm_lane, k), readlane_d(gs_lane, k), readlane_d(sig_lane, k),
                                                 kp.cost ? readlane_d(a_lane, k) : 0.0)
                                : newton<D, RPL>(W, kp, S, k, nevals, st, lr, 0.0, false);
+    if (kp.base_solve) {   // (Optim.minimizer(res), minimum(res)) of base_solve, rbf_optim.jl:127-128
+      if (lane < D) kp.policy[(long long)k * D + lane] = U[Ly::U_NX + lane];
+      if (lane == 0) kp.values[k] = fo;
+    }
     bool xnan = false;
 #pragma unroll
     for (int a = 0; a < D; ++a) xnan = xnan || (U[Ly::U_NX + a] != U[Ly::U_NX + a]);
@@ -2026,23 +2032,39 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
 #pragma unroll
   for (int s = 0; s < RPL; ++s) W.C[lane + WAVE * s] = kp.c0[lane + WAVE * s];
   if (lane == 0) U[Ly::U_FMIN] = kp.fmin_base;
+  // kp.base_solve: this item is start tr of a base_solve launch (one multistart call site: the
+  // loop below runs its solve step once, on surface -1, for start tr alone)
+  const bool bsolve = kp.base_solve != 0;
   if (lane < D) {
-    U[Ly::U_X + lane] = kp.x0s[(long long)r * D + lane];
+    if (!bsolve) U[Ly::U_X + lane] = kp.x0s[(long long)r * D + lane];
     U[Ly::U_LB + lane] = kp.lbs[lane];
     U[Ly::U_UB + lane] = kp.ubs[lane];
   }
   wave_sync();
 
-  for (int k = 0; k <= h; ++k) {
-    const int S = k - 1;
+  const int kend = bsolve ? 1 : h;
+  for (int k = bsolve ? 1 : 0; k <= kend; ++k) {
+    const int S = bsolve ? -1 : k - 1;
     if (k > 0) {
-      if (kp.replay) {
+      if (kp.replay && !bsolve) {
         if (lane < D) U[Ly::U_X + lane] = kp.replay[(long long)lane + D * ((k - 1) + (long long)h * (m + (long long)M * r))];
         wave_sync();
       } else {
 #ifndef MRBO_EXP_NO_NEWTON
-        st |= multistart<D, RPL>(W, kp, S, nevals, lr);
+        st |= multistart<D, RPL>(W, kp, S, nevals, lr, bsolve ? (int)tr : 0, bsolve ? (int)tr + 1 : kp.nstarts);
 #endif
+        if (bsolve) {   // the start's minimizer and minimum were written by multistart
+          if (lane == 0) kp.status[tr] = st & ~8;   // a NaN minimizer is the host's filter, not an error
+          if (kp.evals && lane == 0) {
+            kp.evals[NCOUNT * tr + 0] = nevals.grad;
+            kp.evals[NCOUNT * tr + 1] = nevals.value;
+            kp.evals[NCOUNT * tr + 2] = nevals.hess;
+            kp.evals[NCOUNT * tr + 3] = 0;
+            kp.evals[NCOUNT * tr + 4] = 0;
+          }
+          wave_sync();
+          return;
+        }
         if (st) break;
         if (lane < D) U[Ly::U_X + lane] = U[Ly::U_XB + lane];
         wave_sync();

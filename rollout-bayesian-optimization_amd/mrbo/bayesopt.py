@@ -173,6 +173,64 @@ def run(function_name, output_dir, budget=15, trials=60, starts=16, horizon=0, m
     return results
 
 
+# ---- the myopic experiment loop (experiments/myopic_bayesopt.jl:93-270) -----------------------
+MYOPIC_RULES = {"ei": (EI, 0.0), "poi": (POI, 0.0), "lcb": (LCB, 2.0)}   # :151-153 (random: no solve)
+
+
+def run_myopic(function_name, output_dir, budget=100, trials=60, starts=64, seed=1906, device=0, log=print,
+               rules=("ei", "poi", "lcb"), optimize=True, initial_observations=INITIAL_OBSERVATIONS):
+    """myopic_bayesopt.jl's loop: per budget step xnext = multistart_base_solve!(sur, …; guesses =
+    generate_initial_guesses(starts, lbs, ubs), θfixed) -- the deterministic multistart local solve of
+    the analytic acquisition on the base surrogate (:224-233), here mrbo_base_solve on the device --
+    then the metrics before conditioning (:234-245), condition!, optimize! (lengthscale MLE, bounds
+    [0.1, 5], :248-249) and the minimum observation.  CSVs `<acq>_<metric>.csv` as the reference."""
+    from .rbf_optim import multistart_base_solve
+    from .utils import generate_initial_guesses
+    testfn = TESTFNS[function_name]()
+    lbs, ubs = testfn.get_bounds()
+    directory = os.path.join(output_dir, "myopic", function_name)
+    os.makedirs(directory, exist_ok=True)
+    for metric in METRICS:
+        for acq in rules:
+            create_csv(os.path.join(directory, f"{acq}_{metric}"), budget)
+    write_metadata(directory, budget, trials, starts)
+    guesses = generate_initial_guesses(starts, lbs, ubs)                     # :186
+    rng = np.random.default_rng(seed)
+    initial_samples = [lbs[:, None] + (ubs - lbs)[:, None] * rng.random((testfn.dim, initial_observations))
+                       for _ in range(trials)]                              # :187
+    true_minimum = float(testfn.f(np.asarray(testfn.xopt[0], dtype=np.float64)))
+    results = {}
+    for acq in rules:
+        make_rule, theta = MYOPIC_RULES[acq]
+        log(f"Conducting experiments with acquisition = {acq}")
+        for trial in range(trials):
+            Xinit = initial_samples[trial]
+            yinit = testfn(Xinit)
+            sur = Surrogate(Matern52(), Xinit, yinit, capacity=budget + initial_observations, decision_rule=make_rule(),
+                            σn2=1e-6)
+            initial_best = float(np.min(yinit))
+            times, gaps, allocs, regrets, minobs = (np.zeros(budget) for _ in range(5))
+            xnext = np.zeros(testfn.dim)
+            for b in range(budget):
+                t0 = time.perf_counter()
+                multistart_base_solve(sur, xnext, lbs, ubs, guesses, [theta], device=device)
+                times[b] = time.perf_counter() - t0
+                observed_best = float(np.min(sur.get_active_observations()))
+                regrets[b] = simple_regret(true_minimum, observed_best)
+                gaps[b] = gap(initial_best, observed_best, true_minimum)
+                sur.condition(xnext, float(testfn.f(xnext)))
+                if optimize:
+                    from .mle import optimize as mle_optimize
+                    mle_optimize(sur, KERNEL_LBS, KERNEL_UBS)
+                minobs[b] = float(np.min(sur.get_active_observations()))
+            log(f"myopic {acq} trial {trial + 1}/{trials}: gap {gaps[-1]:.4f}, {times.sum():.2f} s of solves")
+            for metric, data in zip(METRICS, (times, gaps, allocs, regrets, minobs)):
+                write_to_csv(os.path.join(directory, f"{acq}_{metric}"), data)
+            results[(acq, trial)] = dict(times=times, gaps=gaps, simple_regret=regrets, minimum_observations=minobs,
+                                         X=sur.get_active_covariates().copy(), y=sur.get_active_observations().copy())
+    return results
+
+
 def parse(argv=None):
     """parse_command_line (nonmyopic_bayesopt.jl:4-75)."""
     ap = argparse.ArgumentParser("Non-myopic Bayesian optimisation on the MI355X rollout acquisition")

@@ -17,13 +17,22 @@ Per trajectory t, with normwise relative errors
      amplify that by κ.  No trajectory is exempt.
   T3 end to end (both sides run the inner Newton solve):
      flips (an x_1..x_h differing by > 1e-6·(1+|x|))                  ≤ 0.1 % of trajectories
-     identical paths (policy equal to 1e-12 relative): the T2 bounds, and equal Newton work
+     identical paths (policy equal to Δx(t) ≤ 1e-12 relative): e_val ≤ 1e-9 and
+     e_grad ≤ max(tol(t), 10·κ(t)·Δx(t)) -- the T2 bound plus the first-order effect of the
+     policy points' own rounding difference Δx on the adjoint (‖∂x̄_j/∂x_j‖ ≤ κ·‖∂H/∂x‖/‖H‖, and
+     ‖∂H/∂x‖/‖H‖ ≤ 10 is the kernel's derivative ratio ≈ √5/ℓ at ℓ ≥ 0.5); Newton work per counter
+     (gradient, value, Hessian) summed over them within 1 % of the oracle's.  Per-trajectory
+     equality of the counts is recorded, not asserted: on flat acquisition surfaces the line
+     search of a start that does not win the multistart is rounding-sensitive -- two builds of the
+     ORACLE itself (-ffp-contract=off vs -O3 -march=native) disagree on 56 of 122 identical-path
+     C4 trajectories at ℓ = 0.5 (totals within 0.2 %) and on none at C3 (tests/test_oracle.py)
      ETO: no flips → normwise 1e-9 relative per block (mean value, std value, mean ∇x);
      flips → each mean within 3·σ/√M of the oracle's (σ the oracle's std)
   Non-vacuity (every case; a case that only exercises the forward rollout says so with
   kind="forward"): ≥ 25 % non-zero values, ≥ 1 % trajectories whose best observation is a
   fantasy step (t ≥ 1, the adjoint's Case #3, rollout.jl:251-276) and adjoint perturbation pairs
-  on the GPU (> 0).  Forward cases still need non-zero values and Newton work.
+  on the GPU (> 0).  Forward cases compare the policy paths (the inner Newton solves) and need
+  Newton work on the GPU (gradient evaluations > 0); their values may all be 0.
 Trajectories between the two path thresholds end the Newton solve (stopped by x_tol = 1e-3, not
 at a stationary point) at iterates that differ by rounding-level drift; they are counted, and the
 replay covers their arithmetic.  The statistics of every case go to $MRBO_PARITY_REPORT (JSON).
@@ -163,7 +172,9 @@ def _compare(key, g, r, o, o_replay, M, kind="full"):
     ev2, eg2 = _errs(r, o_replay, gscale)
     ev3, eg3 = _errs(r, o, gscale)
     d, N = g["X"].shape
-    tol = grad_tolerance(o_replay["kappa"].ravel(order="F"), N + int(g["h"]))
+    kap = o_replay["kappa"].ravel(order="F")
+    tol = grad_tolerance(kap, N + int(g["h"]))
+    tol3 = np.maximum(tol, 10.0 * kap * dxt)
     evals_r = r["evals"][:3].reshape(3, -1, order="F")
     evals_o = o["evals"].reshape(3, -1, order="F")
     e_r, e_o = r["eto"], o["eto"]
@@ -172,18 +183,26 @@ def _compare(key, g, r, o, o_replay, M, kind="full"):
                  drift=int((~flip & ~exact).sum()), identical=int(exact.sum()), flip_fraction=float(flip.mean()),
                  kappa_max=float(o_replay["kappa"].max()), grad_tol_max=float(tol.max()),
                  replay_value=_summ(ev2), replay_grad=_summ(eg2, tol),
-                 identical_value=_summ(ev3[exact]), identical_grad=_summ(eg3[exact], tol[exact]),
-                 work_equal_identical=bool(np.array_equal(evals_r[:, exact], evals_o[:, exact])),
+                 identical_value=_summ(ev3[exact]), identical_grad=_summ(eg3[exact], tol3[exact]),
+                 identical_dx_max=float(dxt[exact].max()) if exact.any() else 0.0,
+                 work_unequal_identical=int((evals_r[:, exact] != evals_o[:, exact]).any(axis=0).sum()),
                  eto_mean_value_rel=_blocknorm(e_r[0], e_o[0]), eto_std_value_rel=_blocknorm(e_r[1], e_o[1]),
                  eto_mean_grad_rel=_blocknorm(e_r[2:2 + d], e_o[2:2 + d]))
+    # the identical-path trajectories above the T2 bound: (e_grad, κ, Δx, bound) of the worst ten
+    over = np.flatnonzero(exact & (eg3 > tol))
+    over = over[np.argsort(-eg3[over])][:10]
+    mism = np.flatnonzero(exact & (evals_r != evals_o).any(axis=0))[:6]
+    stats["work_mismatch_examples"] = [[int(i), evals_r[:, i].tolist(), evals_o[:, i].tolist()] for i in mism]
+    stats["work_totals"] = dict(gpu=evals_r[:, exact].sum(axis=1).tolist(), oracle=evals_o[:, exact].sum(axis=1).tolist())
+    stats["identical_over_t2"] = [[float(eg3[i]), float(kap[i]), float(dxt[i]), float(tol3[i])] for i in over]
     sd_o = np.concatenate([e_o[1:2], e_o[2 + d:2 + 2 * d]])
     dev = np.abs(np.concatenate([e_r[0:1], e_r[2:2 + d]]) - np.concatenate([e_o[0:1], e_o[2:2 + d]]))
     stats["eto_mean_max_in_se"] = float(np.max(dev / np.maximum(sd_o / np.sqrt(M), 1e-300)))
     _REPORT[key] = stats
     # non-vacuity
-    assert cov["nonzero_values"] >= 0.25 and cov["gpu_grad_evals"] > 0, stats
+    assert cov["gpu_grad_evals"] > 0, stats
     if kind == "full":
-        assert cov["t_ge_1"] >= 0.01 and cov["gpu_pairs"] > 0, stats
+        assert cov["nonzero_values"] >= 0.25 and cov["t_ge_1"] >= 0.01 and cov["gpu_pairs"] > 0, stats
     # T2
     assert stats["replay_value"]["max"] <= 1e-9, stats
     assert stats["replay_grad"]["over_tol"] == 0, stats
@@ -191,7 +210,8 @@ def _compare(key, g, r, o, o_replay, M, kind="full"):
     assert stats["flip_fraction"] <= FLIP_MAX, stats
     assert stats["identical_value"]["max"] <= 1e-9, stats
     assert stats["identical_grad"]["over_tol"] == 0, stats
-    assert stats["work_equal_identical"], stats
+    tg, to = np.asarray(stats["work_totals"]["gpu"], float), np.asarray(stats["work_totals"]["oracle"], float)
+    assert np.all(np.abs(tg - to) <= 0.01 * np.maximum(to, 1.0)), stats
     if not flip.any():
         assert max(stats["eto_mean_value_rel"], stats["eto_std_value_rel"], stats["eto_mean_grad_rel"]) <= 1e-9, stats
     else:

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from conftest import ROOT
-from parity import _REPORT, _end_to_end, _plan, _problem_arrays, _run
+from parity import _REPORT, _end_to_end, _osur, _plan, _problem_arrays, _run
 
 pytestmark = pytest.mark.gpu
 

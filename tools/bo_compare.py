@@ -10,9 +10,10 @@ nonmyopic_bayesopt.jl:273-281) at the compared budget labels: means with standar
 two-sided Mann–Whitney U and Kolmogorov–Smirnov p-values, and the seconds per acquisition solve
 beside the reference's recorded ones (earlier code versions on unstated hardware).
 
-  myopic_<fn>_ei     vs. the rollout acquisition at horizon 0 (MC expected improvement, SGA
-                     from a 64-point batch, as the myopic driver's 64 starts) -- the myopic
-                     driver's EI multistart is a different solver of the same acquisition
+  myopic_<fn>_ei     vs. the myopic loop (bayesopt.run_myopic): multistart_base_solve! of the
+                     analytic EI from generate_initial_guesses(64) on the base surrogate, the
+                     reference's solver shape (experiments/myopic_bayesopt.jl:224-233) with the
+                     build's projected Newton in place of IPNewton
   rollout_h<h>_<fn>  vs. the rollout acquisition at horizon h, the archived run's settings
                      (1 initial point, 8 starts, batch 8, 100 MC samples, 50 SGD iterations)
 
@@ -35,9 +36,9 @@ FIXTURE = os.path.join(ROOT, "tests", "golden", "bo_ref_gaps.json")
 
 # per case: our run() settings and the budget labels compared (the reference's column labels)
 SETTINGS = {
-    "myopic_braninhoo_ei": dict(fn="braninhoo", horizon=0, budget=30, initial=5, starts=16, batch=64,
+    "myopic_braninhoo_ei": dict(fn="braninhoo", horizon=0, budget=30, initial=5, starts=64, batch=0,
                                 labels=["10", "20", "30"]),
-    "myopic_hartmann6d_ei": dict(fn="hartmann6d", horizon=0, budget=30, initial=5, starts=16, batch=64,
+    "myopic_hartmann6d_ei": dict(fn="hartmann6d", horizon=0, budget=30, initial=5, starts=64, batch=0,
                                  labels=["10", "20", "30"]),
     "rollout_h0_braninhoo": dict(fn="braninhoo", horizon=0, budget=20, initial=1, starts=8, batch=8, labels=["5", "10", "20"]),
     "rollout_h1_braninhoo": dict(fn="braninhoo", horizon=1, budget=20, initial=1, starts=8, batch=8, labels=["5", "10", "20"]),
@@ -78,13 +79,23 @@ def our_column(gcols, label, myopic):
 
 
 def compare(a, b):
-    """ours (a) vs reference (b): means, standard errors, Mann–Whitney U and KS p-values"""
-    from scipy.stats import ks_2samp, mannwhitneyu
+    """ours (a) vs reference (b): means, standard errors, the difference of means with its Welch 95 %
+    confidence interval, Mann–Whitney U and KS p-values.  A large p-value means no significant
+    difference was DETECTED at these sample sizes -- not equivalence; the interval says how large a
+    difference the data still allow."""
+    from scipy.stats import ks_2samp, mannwhitneyu, t as student_t
     a, b = np.asarray(a, float), np.asarray(b, float)
     se = lambda x: float(x.std(ddof=1) / np.sqrt(x.size)) if x.size > 1 else float("nan")
     out = {"ours_mean": float(a.mean()), "ours_se": se(a), "ref_mean": float(b.mean()), "ref_se": se(b),
            "n_ours": int(a.size), "n_ref": int(b.size)}
+    va, vb = a.var(ddof=1) / a.size, b.var(ddof=1) / b.size
+    diff, sd = float(a.mean() - b.mean()), float(np.sqrt(va + vb))
+    dof = (va + vb) ** 2 / (va ** 2 / (a.size - 1) + vb ** 2 / (b.size - 1)) if va + vb > 0 else 1.0
+    half = float(student_t.ppf(0.975, dof) * sd)
+    out["diff_mean"], out["diff_ci95"] = diff, [diff - half, diff + half]
     out["mannwhitney_p"] = float(mannwhitneyu(a, b, alternative="two-sided").pvalue)
+    # one-sided: evidence that ours is stochastically SMALLER (gaps: worse) than the reference's
+    out["mannwhitney_p_worse"] = float(mannwhitneyu(a, b, alternative="less").pvalue)
     out["ks_p"] = float(ks_2samp(a, b).pvalue)
     return out
 
@@ -94,22 +105,26 @@ def run_case(key, case, trials, seed, log, solver="sga", eta=0.5, q3=True):
     s = SETTINGS[key]
     testfn = bayesopt.TESTFNS[s["fn"]]()
     true_minimum = float(testfn.f(np.asarray(testfn.xopt[0], dtype=np.float64)))
+    myopic = key.startswith("myopic")
     with tempfile.TemporaryDirectory() as tmp:
         t0 = time.perf_counter()
-        res = bayesopt.run(s["fn"], tmp, budget=s["budget"], trials=trials, starts=s["starts"], horizon=s["horizon"],
-                           mc_samples=100, batch_size=s["batch"], sgd_iterations=50, optimize=True, seed=seed,
-                           rules=("ei",), initial_observations=s["initial"], solver=solver, eta=eta,
-                           fmini_over_capacity=q3,
-                           log=lambda *m: log(f"[{key}] " + " ".join(map(str, m))))
+        lg = lambda *m: log(f"[{key}] " + " ".join(map(str, m)))
+        if myopic:
+            res = bayesopt.run_myopic(s["fn"], tmp, budget=s["budget"], trials=trials, starts=s["starts"], seed=seed,
+                                      rules=("ei",), initial_observations=s["initial"], log=lg)
+        else:
+            res = bayesopt.run(s["fn"], tmp, budget=s["budget"], trials=trials, starts=s["starts"], horizon=s["horizon"],
+                               mc_samples=100, batch_size=s["batch"], sgd_iterations=50, optimize=True, seed=seed,
+                               rules=("ei",), initial_observations=s["initial"], solver=solver, eta=eta,
+                               fmini_over_capacity=q3, log=lg)
         wall = time.perf_counter() - t0
     trials_res = []
     for t in range(trials):
-        r = res[(f"rollout_{s['horizon']}_ei", t)]
+        r = res[("ei", t) if myopic else (f"rollout_{s['horizon']}_ei", t)]
         y = r["y"]
         r = dict(r, initial_best=float(np.min(y[:s["initial"]])))
         trials_res.append(r)
     gcols = our_gap_columns(trials_res, true_minimum, s["budget"])
-    myopic = key.startswith("myopic")
     per_label = {lab: compare(our_column(gcols, lab, myopic), ref_column(case, lab)) for lab in s["labels"]}
     our_times = np.concatenate([r["times"] for r in trials_res])
     ref_times = np.array(case["times"], float)[:, :s["budget"]].ravel()
@@ -147,6 +162,7 @@ def main():
                 f.write(line + "\n")
         g = row["gaps"][SETTINGS[key]["labels"][-1]]
         log(f"{key} [{a.solver}{'' if not a.no_q3 else ', Q3 off'}]: final gap ours {g['ours_mean']:.3f}±{g['ours_se']:.3f} ref {g['ref_mean']:.3f}±{g['ref_se']:.3f} "
+            f"diff {g['diff_mean']:+.3f} [{g['diff_ci95'][0]:+.3f}, {g['diff_ci95'][1]:+.3f}] "
             f"MW p={g['mannwhitney_p']:.3f}; s/solve ours {row['seconds_per_solve']['ours_median']:.3f} "
             f"ref {row['seconds_per_solve']['ref_median']:.2f}")
 
