@@ -41,7 +41,7 @@ typedef enum {
   MRBO_OK = 0,
   MRBO_ERR_ARG = -1,      /* invalid argument (dimension, size, null pointer)            */
   MRBO_ERR_UNSUPPORTED = -2, /* shape outside the compiled kernels: d > 16, N > 512,
-                                d > 8 with N > 128, h > 5 (gp_fit: N > 256) */
+                                d > 8 with N > 128, h > 5 (gp_fit: N > 512) */
   MRBO_ERR_HIP = -3,      /* HIP runtime error                                          */
   MRBO_ERR_NOMEM = -4
 } mrbo_err_t;
@@ -212,9 +212,11 @@ int mrbo_base_solve(mrbo_plan_t* plan, int32_t n, const double* xstarts, double*
  * takes θ = (ℓ, p) (nt = 2) or (ℓ) with p = s->period (nt = 1: ∂/∂ℓ only).
  * status[p] = 0, or 1 when cholesky throws PosDefException (ll, grad = NaN).  L_out (N×N×P,
  * lower, zeros above) and c_out (N×P) are optional (NULL).  thetas / ll / grad / status / L_out
- * / c_out are device pointers unless MRBO_FLAG_HOST_POINTERS; N ≤ 256.  N ≤ 64 without L_out /
- * c_out runs one wave per candidate with no workspace; otherwise 3·N²·P doubles of workspace are
- * allocated for the call.  Synchronises the stream before returning.                        */
+ * / c_out are device pointers unless MRBO_FLAG_HOST_POINTERS; N ≤ 512 (every N the rollout
+ * accepts).  N ≤ 128 runs without workspace (one wave per candidate at N ≤ 64 without L_out /
+ * c_out, the candidate in LDS up to N = 128); N > 128 runs the 32 × 32-tile kernel on the fp64
+ * matrix cores with (T(T+1) + T)·1024·P doubles of workspace, T = ⌈N/32⌉, allocated for the
+ * call.  Synchronises the stream before returning.                                          */
 int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t P, int32_t nt, const double* thetas, double* ll,
                       double* grad, int32_t* status, double* L_out, double* c_out, uint32_t flags, void* stream);
 /* mrbo_gp_fit_theta with nt = 1: ells[p] = ℓ_p, dll[p] = ∂ll/∂ℓ (Periodic: p = s->period). */

@@ -731,7 +731,7 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
   if (!s || !thetas || !ll || !grad || !status || np < 1) return fail(MRBO_ERR_ARG, "null argument");
   const int d = s->d, N = s->N;
   if (d < 1 || N < 1 || !s->X || !s->y) return fail(MRBO_ERR_ARG, "bad surrogate (d=%d N=%d)", d, N);
-  if (N > 256) return fail(MRBO_ERR_UNSUPPORTED, "N=%d > 256", N);
+  if (N > 512) return fail(MRBO_ERR_UNSUPPORTED, "N=%d > 512", N);
   if (s->kernel < 0 || s->kernel > 4) return fail(MRBO_ERR_UNSUPPORTED, "gp_fit: kernel id %d", s->kernel);
   // θ = (ℓ) for the one-parameter kernels; Periodic takes (ℓ) (period fixed at s->period) or (ℓ, p)
   if (nt < 1 || nt > (s->kernel == 4 ? 2 : 1)) return fail(MRBO_ERR_ARG, "gp_fit: nt=%d for kernel %d", nt, s->kernel);
@@ -751,7 +751,8 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
   if (sg.in(s->X, (size_t)d * N, &dX) || sg.in(s->y, (size_t)N, &dy)) return fail(MRBO_ERR_NOMEM, "staging X, y");
   GpFitParams q{d, N, s->kernel, s->sigma_n2, dX, dy, nt, dth, s->period, dll_, dgr, (int*)dst, dL, dc, nullptr};
   if (!gpfit_in_regs(q) && !gpfit_in_lds(q)) {   // the register (N ≤ 64) and LDS (N ≤ 128) kernels need none
-    if (hipMalloc(&q.work, sizeof(double) * 3 * NN * P) != hipSuccess) return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
+    if (hipMalloc(&q.work, sizeof(double) * gpfit_tile_work_doubles(N) * P) != hipSuccess)
+      return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
     sg.bufs.push_back(q.work);
   }
   static hipEvent_t gev[2] = {nullptr, nullptr};

@@ -69,8 +69,10 @@ struct GpFitParams {
   int* status;           // P: 0, or 1 = PosDefException
   double* L_out;         // optional N×N×P
   double* c_out;         // optional N×P
-  double* work;          // 3·N²·P (gpfit_kernel only)
+  double* work;          // gpfit_tile_work_doubles(N)·P (the tile kernel only)
 };
+// 128 < N ≤ 512 (or factor outputs at N > 128): gpfit_tile_kernel's workspace per candidate
+size_t gpfit_tile_work_doubles(int N);
 void launch_gpfit(int P, hipStream_t st, const GpFitParams& q);
 // N ≤ 64, d ≤ 16 and no factor / coefficient outputs: the one-wave-per-candidate register kernel
 // (no workspace)

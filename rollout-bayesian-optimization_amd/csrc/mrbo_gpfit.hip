@@ -18,11 +18,8 @@
 // broadcasts; tr(K⁻¹δK) and cᵀδKc from K⁻¹.  K and δK are evaluated once per pair j ≤ i.  The
 // reference's operations (chol, then triangular solves); summation orders differ (tolerance).
 // 64 < N ≤ 128, or N ≤ 64 with L / c requested: gpfit_lds_kernel (below; everything in LDS).
-// Otherwise (N ≤ 256) gpfit_kernel: one workgroup per candidate;
-// N³/3 (Cholesky) + N³/2 (Z = L⁻¹δK per θ component) + N³/6 (L⁻¹) FMAs on a global workspace
-// (3·N² doubles per candidate, L2-resident at N ≤ 256).  Column-parallel steps map one thread
-// to one column; the right-looking Cholesky updates the trailing triangle with all 256 threads
-// between block barriers.
+// 128 < N ≤ 512: gpfit_tile_kernel (below): one workgroup per candidate, the blocked algorithm on
+// 32 × 32 tiles in a global workspace with the tile products on the fp64 matrix cores.
 #include <hip/hip_runtime.h>
 
 #include <utility>
@@ -84,151 +81,6 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
 __device__ __forceinline__ void cand_theta(const GpFitParams& q, int p, double& ell, double& per) {
   ell = q.thetas[(size_t)p * q.nt];
   per = (q.nt > 1) ? q.thetas[(size_t)p * q.nt + 1] : q.period;
-}
-
-// one workgroup per candidate p; work = 3·N² doubles per candidate: A (K → L, column-major),
-// G (δK_t, then L⁻¹δK_t row-major, per hyperparameter t) and V (L⁻¹, row-major), leading dimension N
-__global__ void __launch_bounds__(GPFIT_THREADS) gpfit_kernel(GpFitParams q) {
-  __shared__ double sh[GPFIT_THREADS];
-  __shared__ double cv[256];
-  __shared__ int fail;
-  const int N = q.N, d = q.d, t = threadIdx.x, p = blockIdx.x;
-  double ell, per;
-  cand_theta(q, p, ell, per);
-  double* A = q.work + (size_t)3 * N * N * p;
-  double* G = A + (size_t)N * N;
-  double* V = G + (size_t)N * N;
-  if (t == 0) fail = 0;
-  // K (eval_KXX :161-178 with ψ(0) on the diagonal)
-  for (int idx = t; idx < N * N; idx += GPFIT_THREADS) {
-    const int i = idx % N, j = idx / N;
-    double r2 = 0.0;
-    for (int a = 0; a < d; ++a) {
-      const double r = q.X[a + d * i] - q.X[a + d * j];
-      r2 += r * r;
-    }
-    double psi, dps[2];
-    psi_dtheta(q.kernel, ell, per, (i == j) ? 0.0 : sqrt(r2), psi, dps);
-    A[idx] = (i == j) ? psi + q.sn2 : psi;
-  }
-  __syncthreads();
-  // right-looking Cholesky, lower triangle of A in place (PosDefException → status 1)
-  for (int k = 0; k < N; ++k) {
-    const double piv = A[k + N * k];
-    if (!(piv > 0.0)) {
-      if (t == 0) fail = 1;
-      break;
-    }
-    const double lkk = sqrt(piv);
-    __syncthreads();   // every thread has read the pivot before it is overwritten
-    for (int i = k + t; i < N; i += GPFIT_THREADS) A[i + N * k] = (i == k) ? lkk : A[i + N * k] / lkk;
-    __syncthreads();
-    const int m = N - k - 1;
-    for (int idx = t; idx < m * m; idx += GPFIT_THREADS) {
-      const int i = k + 1 + idx % m, j = k + 1 + idx / m;
-      if (j <= i) A[i + N * j] -= A[i + N * k] * A[j + N * k];
-    }
-    __syncthreads();
-  }
-  __syncthreads();
-  if (fail) {
-    if (t == 0) {
-      q.ll[p] = NAN;
-      for (int u = 0; u < q.nt; ++u) q.grad[(size_t)p * q.nt + u] = NAN;
-      q.status[p] = 1;
-    }
-    return;
-  }
-  // c = L'\(L\y): column-oriented substitutions, c in LDS
-  for (int i = t; i < N; i += GPFIT_THREADS) cv[i] = q.y[i];
-  __syncthreads();
-  for (int k = 0; k < N; ++k) {
-    const double ck = cv[k] / A[k + N * k];
-    __syncthreads();
-    if (t == 0) cv[k] = ck;
-    for (int i = k + 1 + t; i < N; i += GPFIT_THREADS) cv[i] -= A[i + N * k] * ck;
-    __syncthreads();
-  }
-  for (int k = N - 1; k >= 0; --k) {
-    const double ck = cv[k] / A[k + N * k];
-    __syncthreads();
-    if (t == 0) cv[k] = ck;
-    for (int i = t; i < k; i += GPFIT_THREADS) cv[i] -= A[k + N * i] * ck;
-    __syncthreads();
-  }
-  // log_likelihood (:770-776)
-  double yc = 0.0, ld = 0.0;
-  for (int j = t; j < N; j += GPFIT_THREADS) {
-    yc += q.y[j] * cv[j];
-    ld += log(A[j + N * j]);
-  }
-  yc = block_sum(yc, sh);
-  ld = block_sum(ld, sh);
-  if (t == 0) {
-    q.ll[p] = -0.5 * yc - ld - 0.5 * N * log(2.0 * 3.141592653589793);
-    q.status[p] = 0;
-  }
-  for (int u = 0; u < q.nt; ++u) {
-    // δK_u (eval_Dθ_KXX :264-284, δθ = e_u), symmetric: row-major = column-major
-    for (int idx = t; idx < N * N; idx += GPFIT_THREADS) {
-      const int i = idx % N, j = idx / N;
-      double r2 = 0.0;
-      for (int a = 0; a < d; ++a) {
-        const double r = q.X[a + d * i] - q.X[a + d * j];
-        r2 += r * r;
-      }
-      double psi, dps[2];
-      psi_dtheta(q.kernel, ell, per, (i == j) ? 0.0 : sqrt(r2), psi, dps);
-      G[idx] = (i == j) ? 0.0 : dps[u];
-    }
-    __syncthreads();
-    // cᵀδKc (thread j: c_j Σ_i δK_ij c_i)
-    double cgc = 0.0;
-    for (int j = t; j < N; j += GPFIT_THREADS) {
-      double s = 0.0;
-      for (int i = 0; i < N; ++i) s += G[(size_t)N * i + j] * cv[i];   // δK symmetric: coalesced in j
-      cgc += cv[j] * s;
-    }
-    cgc = block_sum(cgc, sh);
-    // tr(L'\(L\δK)) = tr(L⁻ᵀL⁻¹δK) = Σ_ij (L⁻¹δK)_ij (L⁻¹)_ij: thread j forward-substitutes
-    // column j of δK (in place → Z) and, for the first component, of the identity (→ V), rows
-    // ascending.  Z and V are kept row-major (entry (i, j) at i·N + j) so that the threads'
-    // loads are coalesced; δK is symmetric, so G read row-major is δK itself.  L[i][k] is a
-    // wave-uniform broadcast.
-    double tr = 0.0;
-    for (int j = t; j < N; j += GPFIT_THREADS) {
-      for (int i = 0; i < N; ++i) {
-        double z = G[(size_t)N * i + j], v = (i == j) ? 1.0 : 0.0;
-        for (int k = 0; k < i; ++k) {
-          const double lik = A[i + N * k];
-          z -= lik * G[(size_t)N * k + j];
-          if (u == 0) v -= lik * V[(size_t)N * k + j];
-        }
-        const double li = A[i + N * i];
-        z /= li;
-        G[(size_t)N * i + j] = z;
-        if (u == 0) {
-          v /= li;
-          V[(size_t)N * i + j] = v;
-        } else {
-          v = V[(size_t)N * i + j];
-        }
-        tr += z * v;
-      }
-    }
-    tr = block_sum(tr, sh);
-    if (t == 0) q.grad[(size_t)p * q.nt + u] = 0.5 * (cgc - tr);
-  }
-  // optional fit outputs: L (lower, zeros above) and c of each candidate
-  if (q.L_out) {
-    double* Lo = q.L_out + (size_t)N * N * p;
-    for (int idx = t; idx < N * N; idx += GPFIT_THREADS) {
-      const int i = idx % N, j = idx / N;
-      Lo[idx] = (i >= j) ? A[idx] : 0.0;
-    }
-  }
-  if (q.c_out)
-    for (int i = t; i < N; i += GPFIT_THREADS) q.c_out[(size_t)N * p + i] = cv[i];
 }
 
 // ---- N ≤ 64: one wave per candidate, K rows in registers --------------------------------
@@ -751,6 +603,327 @@ __global__ void __launch_bounds__(GL_THREADS) gpfit_lds_kernel(GpFitParams q, in
     for (int i = tid; i < N; i += GL_THREADS) q.c_out[(size_t)N * p + i] = cv[i];
 }
 
+// ---- 128 < N ≤ 512: blocked on 32 × 32 tiles, the products on the fp64 matrix cores ----------
+// One workgroup (four waves) per candidate.  Global workspace per candidate (tile_work_doubles):
+// the lower tiles of K → L (column-major), of V = L⁻¹ (row-major) and the diagonal-tile inverses
+// W_k = L_kk⁻¹ (column-major); T = ⌈N/32⌉, rows and columns past N are identity rows of K (their
+// L, V and K⁻¹ rows are identity rows too, and they take no part in the sums).
+//   Cholesky, right-looking by tile columns k: wave 0 factors A_kk and inverts L_kk in LDS; the
+//   panel L_Ik = A_Ik·W_kᵀ and the trailing updates A_IJ −= L_Ik·L_Jkᵀ are 32³ products spread
+//   over the four waves, each 32 v_mfma_f64_16x16x4 (tile_xyt: C += X·Yᵀ with X and Y read as
+//   column-major tiles -- both fragment loads coalesced).
+//   V = L⁻¹ by tile rows I: V_IJ = −W_I·Σ_{J≤M<I} L_IM V_MJ.  V is stored row-major, i.e. as the
+//   column-major Vᵀ the later products read.
+//   u = V y, c = Vᵀu (so yᵀc = uᵀu), and K⁻¹_IJ = Σ_{M≥I} V_MIᵀ V_MJ for I ≥ J, whose tile the
+//   wave holds in registers while it adds K⁻¹_ij·δK_t,ij and c_i c_j·δK_t,ij over the strictly
+//   lower entries (δK on the fly; δK_ii = 0), as the LDS kernel above does.
+// ≈ N³/2 multiply-adds (N³/6 each for L, V and K⁻¹), all but the diagonal tiles' on the MFMA pipe.
+constexpr int TT = 32, TT_THREADS = 256, TT_LD = 33;
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// c[bi][bj][j] holds tile entry (16·bi + (lane >> 4) + 4·j, 16·bj + (lane & 15)) (the f64 MFMA's
+// accumulator map)
+__device__ __forceinline__ void tile_zero(f64x4 (&c)[2][2]) {
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) c[bi][bj] = f64x4{0.0, 0.0, 0.0, 0.0};
+}
+template <bool ROWMAJOR>
+__device__ __forceinline__ void tile_load(f64x4 (&c)[2][2], const double* t, int lane) {
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = 16 * bi + (lane >> 4) + 4 * j, col = 16 * bj + (lane & 15);
+        c[bi][bj][j] = ROWMAJOR ? t[row * TT + col] : t[col * TT + row];
+      }
+}
+template <bool ROWMAJOR>
+__device__ __forceinline__ void tile_store(const f64x4 (&c)[2][2], double* t, int lane) {
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = 16 * bi + (lane >> 4) + 4 * j, col = 16 * bj + (lane & 15);
+        if (ROWMAJOR) t[row * TT + col] = c[bi][bj][j];
+        else t[col * TT + row] = c[bi][bj][j];
+      }
+}
+// c += ±X·Yᵀ, X and Y 32 × 32 column-major (X's A-fragment: X[r][k] at k·32 + r; Yᵀ's
+// B-fragment: Y[n][k] at k·32 + n -- sixteen consecutive doubles per lane group)
+template <bool NEG>
+__device__ __forceinline__ void tile_xyt(f64x4 (&c)[2][2], const double* X, const double* Y, int lane) {
+  const int r = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int k0 = 0; k0 < TT; k0 += 4) {
+    double a0 = X[(k0 + kk) * TT + r], a1 = X[(k0 + kk) * TT + 16 + r];
+    const double b0 = Y[(k0 + kk) * TT + r], b1 = Y[(k0 + kk) * TT + 16 + r];
+    if (NEG) {
+      a0 = -a0;
+      a1 = -a1;
+    }
+    c[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, c[0][0], 0, 0, 0);
+    c[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, c[0][1], 0, 0, 0);
+    c[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, c[1][0], 0, 0, 0);
+    c[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, c[1][1], 0, 0, 0);
+  }
+}
+__device__ __forceinline__ size_t tile_at(int I, int J) { return (size_t)(I * (I + 1) / 2 + J) * (TT * TT); }
+// lower-triangle index q = I(I+1)/2 + J → (I, J)
+__device__ __forceinline__ void tile_ij(int q, int& I, int& J) {
+  I = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
+  I += ((I + 1) * (I + 2) / 2 <= q) ? 1 : 0;
+  I -= (I * (I + 1) / 2 > q) ? 1 : 0;
+  J = q - I * (I + 1) / 2;
+}
+
+template <int NT>
+__global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, int P) {
+  extern __shared__ __attribute__((aligned(16))) double tsm[];
+  const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (p >= P) return;   // whole workgroups
+  const int N = q.N, d = q.d, T = (N + TT - 1) / TT, NP = T * TT;
+  double* XS = tsm;                      // X[u][i] at u·NP + i, zero-padded
+  double* Dk = XS + (size_t)d * NP;      // diagonal tile A_kk → L_kk, 32 × 33 column-major
+  double* Wk = Dk + TT * TT_LD;          // W_k = L_kk⁻¹, 32 × 33 column-major
+  double* rd = Wk + TT * TT_LD;          // 1/L_ii of the tile
+  double* Sw = rd + TT;                  // per-wave 32 × 32 scratch (row-major S)
+  double* yv = Sw + 4 * TT * TT;         // y, then c
+  double* uv = yv + NP;                  // u = V y
+  __shared__ double part[TT_THREADS / 64][2 * NT + 2];
+  __shared__ int fail;
+  double ell, per;
+  cand_theta(q, p, ell, per);
+  const size_t ntile = (size_t)T * (T + 1) / 2;
+  double* Lt = q.work + (size_t)p * (2 * ntile + T) * (TT * TT);
+  double* Vt = Lt + ntile * (TT * TT);
+  double* Wt = Vt + ntile * (TT * TT);
+  if (tid == 0) fail = 0;
+  for (int idx = tid; idx < d * NP; idx += TT_THREADS) {
+    const int u = idx / NP, i = idx % NP;
+    XS[idx] = (i < N) ? q.X[u + (size_t)d * i] : 0.0;
+  }
+  for (int i = tid; i < NP; i += TT_THREADS) yv[i] = (i < N) ? q.y[i] : 0.0;
+  __syncthreads();
+  // K (eval_KXX :161-178, ψ(0) + σn2 on the diagonal), every entry of the lower tiles
+  for (size_t e = tid; e < ntile * (TT * TT); e += TT_THREADS) {
+    int I, J;
+    tile_ij((int)(e >> 10), I, J);
+    const int gi = TT * I + (int)(e & 31), gj = TT * J + (int)((e >> 5) & 31);
+    double v = (gi == gj) ? 1.0 : 0.0;
+    if (gi < N && gj < N) {
+      double r2 = 0.0;
+      for (int u = 0; u < d; ++u) { const double r = XS[u * NP + gi] - XS[u * NP + gj]; r2 = fma(r, r, r2); }
+      double psi, dps[2];
+      psi_dtheta(q.kernel, ell, per, (gi == gj) ? 0.0 : sqrt(r2), psi, dps);
+      v = (gi == gj) ? psi + q.sn2 : psi;
+    }
+    Lt[e] = v;
+  }
+  __syncthreads();
+  double lg = 0.0;   // Σ log L_ii (wave 0)
+  for (int k = 0; k < T; ++k) {
+    if (w == 0) {
+      // A_kk → L_kk in LDS (right-looking; PosDefException → status 1), then W_k = L_kk⁻¹
+      const int i = lane & 31, h = lane >> 5;
+      const double* A = Lt + tile_at(k, k);
+      for (int e = lane; e < TT * TT; e += 64) Dk[(e >> 5) * TT_LD + (e & 31)] = A[e];
+      gr_sync();
+      bool bad = false;
+      for (int c = 0; c < TT; ++c) {
+        const double piv = Dk[c * TT_LD + c];
+        if (!(piv > 0.0)) {   // the same value in every lane: a uniform exit
+          bad = true;
+          break;
+        }
+        double lcc, rl;
+        sqrt_rsqrt(piv, lcc, rl);
+        if (TT * k + c < N) lg += log(lcc);
+        gr_sync();
+        if (h == 0 && i > c) Dk[c * TT_LD + i] *= rl;
+        if (lane == 0) {
+          Dk[c * TT_LD + c] = lcc;
+          rd[c] = rl;
+        }
+        gr_sync();
+        if (i > c) {
+          const double lic = Dk[c * TT_LD + i];
+          for (int j = c + 1 + h; j <= i; j += 2) Dk[j * TT_LD + i] = fma(-lic, Dk[c * TT_LD + j], Dk[j * TT_LD + i]);
+        }
+        gr_sync();
+      }
+      if (bad) {
+        if (lane == 0) fail = 1;
+      } else {
+        // W column j = lane (< 32): W_ij = (δ_ij − Σ_{m<i} L_im W_mj)/L_ii, rows ascending
+        // (W_mj = 0 for m < j comes out of the same recursion)
+        if (lane < TT) {
+          for (int r = 0; r < TT; ++r) {
+            double sacc = (r == lane) ? 1.0 : 0.0;
+            for (int m = 0; m < r; ++m) sacc = fma(-Dk[m * TT_LD + r], Wk[lane * TT_LD + m], sacc);
+            Wk[lane * TT_LD + r] = sacc * rd[r];
+          }
+        }
+        gr_sync();
+        double* Lkk = Lt + tile_at(k, k);
+        double* Vkk = Vt + tile_at(k, k);
+        double* Wkk = Wt + (size_t)k * (TT * TT);
+        for (int e = lane; e < TT * TT; e += 64) {
+          const int r = e & 31, cc = e >> 5;                 // column-major (r, cc)
+          Lkk[e] = (r >= cc) ? Dk[cc * TT_LD + r] : 0.0;
+          Wkk[e] = Wk[cc * TT_LD + r];
+          Vkk[r * TT + cc] = Wk[cc * TT_LD + r];              // row-major copy: V_kk = W_k
+        }
+      }
+    }
+    __syncthreads();
+    if (fail) break;
+    // panel: L_Ik = A_Ik·W_kᵀ
+    for (int I = k + 1 + w; I < T; I += 4) {
+      f64x4 c[2][2];
+      tile_zero(c);
+      tile_xyt<false>(c, Lt + tile_at(I, k), Wt + (size_t)k * (TT * TT), lane);
+      tile_store<false>(c, Lt + tile_at(I, k), lane);
+    }
+    __syncthreads();
+    // trailing update A_IJ −= L_Ik·L_Jkᵀ, k < J ≤ I
+    const int m = T - k - 1, npair = m * (m + 1) / 2;
+    for (int pi = w; pi < npair; pi += 4) {
+      int I, J;
+      tile_ij(pi, I, J);
+      I += k + 1;
+      J += k + 1;
+      f64x4 c[2][2];
+      tile_load<false>(c, Lt + tile_at(I, J), lane);
+      tile_xyt<true>(c, Lt + tile_at(I, k), Lt + tile_at(J, k), lane);
+      tile_store<false>(c, Lt + tile_at(I, J), lane);
+    }
+    __syncthreads();
+  }
+  if (fail) {
+    if (tid == 0) {
+      q.ll[p] = NAN;
+      for (int t = 0; t < NT; ++t) q.grad[(size_t)p * NT + t] = NAN;
+      q.status[p] = 1;
+    }
+    return;
+  }
+  if (tid == 0) part[0][2 * NT + 1] = lg;   // wave 0's sum
+  // V = L⁻¹ below the diagonal tiles, by tile rows
+  for (int I = 1; I < T; ++I) {
+    for (int J = w; J < I; J += 4) {
+      f64x4 c[2][2];
+      tile_zero(c);
+      for (int M = J; M < I; ++M) tile_xyt<false>(c, Lt + tile_at(I, M), Vt + tile_at(M, J), lane);   // L_IM·V_MJ
+      double* S = Sw + w * (TT * TT);
+      tile_store<true>(c, S, lane);
+      gr_sync();
+      tile_zero(c);
+      tile_xyt<true>(c, Wt + (size_t)I * (TT * TT), S, lane);   // −W_I·S
+      tile_store<true>(c, Vt + tile_at(I, J), lane);
+      gr_sync();
+    }
+    __syncthreads();
+  }
+  // u = V y, yᵀc = uᵀu, c = Vᵀu (rows / columns of the row-major tiles)
+  double yc = 0.0;
+  for (int i = tid; i < NP; i += TT_THREADS) {
+    const int I = i / TT, ii = i % TT;
+    double s = 0.0;
+    for (int J = 0; J <= I; ++J) {
+      const double* v = Vt + tile_at(I, J) + ii * TT;
+      for (int jj = 0; jj < TT; ++jj) s = fma(v[jj], yv[TT * J + jj], s);
+    }
+    uv[i] = s;
+    yc = fma(s, s, yc);
+  }
+  yc = gr_sum(yc);
+  if (lane == 0) part[w][2 * NT] = yc;
+  __syncthreads();
+  for (int j = tid; j < NP; j += TT_THREADS) {
+    const int J = j / TT, jj = j % TT;
+    double s = 0.0;
+    for (int I = J; I < T; ++I) {
+      const double* v = Vt + tile_at(I, J) + jj;
+      for (int ii = 0; ii < TT; ++ii) s = fma(v[ii * TT], uv[TT * I + ii], s);
+    }
+    yv[j] = s;   // c
+  }
+  __syncthreads();
+  // K⁻¹ tiles and the traces over the strictly lower entries
+  double tr[NT], cgc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) tr[t] = cgc[t] = 0.0;
+  for (int pi = w; pi < (int)ntile; pi += 4) {
+    int I, J;
+    tile_ij(pi, I, J);
+    f64x4 c[2][2];
+    tile_zero(c);
+    for (int M = I; M < T; ++M) tile_xyt<false>(c, Vt + tile_at(M, I), Vt + tile_at(M, J), lane);   // V_MIᵀ·V_MJ
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int gi = TT * I + 16 * bi + (lane >> 4) + 4 * j, gj = TT * J + 16 * bj + (lane & 15);
+          if (gi > gj && gi < N) {
+            double r2 = 0.0;
+            for (int u = 0; u < d; ++u) { const double r = XS[u * NP + gi] - XS[u * NP + gj]; r2 = fma(r, r, r2); }
+            double psi, dps[2];
+            psi_dtheta(q.kernel, ell, per, sqrt(r2), psi, dps);
+            const double cc = yv[gi] * yv[gj], kij = c[bi][bj][j];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+              tr[t] = fma(kij, dps[t], tr[t]);
+              cgc[t] = fma(cc, dps[t], cgc[t]);
+            }
+          }
+        }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const double trs = gr_sum(tr[t]), cgs = gr_sum(cgc[t]);
+    if (lane == 0) { part[w][t] = trs; part[w][NT + t] = cgs; }
+  }
+  __syncthreads();
+  if (tid == 0) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {   // both triangles: 2·Σ_{j<i}, halved by δlog_likelihood's 1/2
+      const double trs = (part[0][t] + part[1][t]) + (part[2][t] + part[3][t]);
+      const double cgs = (part[0][NT + t] + part[1][NT + t]) + (part[2][NT + t] + part[3][NT + t]);
+      q.grad[(size_t)p * NT + t] = cgs - trs;
+    }
+    const double ycs = (part[0][2 * NT] + part[1][2 * NT]) + (part[2][2 * NT] + part[3][2 * NT]);
+    q.ll[p] = -0.5 * ycs - part[0][2 * NT + 1] - 0.5 * N * log(2.0 * 3.141592653589793);
+    q.status[p] = 0;
+  }
+  if (q.L_out) {
+    double* Lo = q.L_out + (size_t)N * N * p;
+    for (size_t idx = tid; idx < (size_t)N * N; idx += TT_THREADS) {
+      const int i = (int)(idx % N), j = (int)(idx / N);
+      Lo[idx] = (i >= j) ? Lt[tile_at(i / TT, j / TT) + (j % TT) * TT + i % TT] : 0.0;
+    }
+  }
+  if (q.c_out)
+    for (int i = tid; i < N; i += TT_THREADS) q.c_out[(size_t)N * p + i] = yv[i];
+}
+
+size_t gpfit_tile_lds(int d, int N) {
+  const int NP = ((N + TT - 1) / TT) * TT;
+  return sizeof(double) * ((size_t)d * NP + 2 * TT * TT_LD + TT + 4 * TT * TT + 2 * (size_t)NP);
+}
+
+size_t gpfit_tile_work_doubles(int N) {
+  const size_t T = (N + TT - 1) / TT;
+  return (T * (T + 1) + T) * TT * TT;
+}
+
 size_t gpfit_lds_bytes() { return sizeof(double) * ((size_t)GL_N * GL_LD + 16 * GL_N + 3 * GL_N); }
 
 size_t gpfit_reg_lds(int nt) { return sizeof(double) * ((size_t)(1 + nt) * 64 * GR_LD + 64 + 16 * 64); }
@@ -770,7 +943,10 @@ void launch_gpfit(int P, hipStream_t st, const GpFitParams& q) {
       hipLaunchKernelGGL(gpfit_lds_kernel<1>, dim3(P), dim3(GL_THREADS), gpfit_lds_bytes(), st, q, P);
     return;
   }
-  hipLaunchKernelGGL(gpfit_kernel, dim3(P), dim3(GPFIT_THREADS), 0, st, q);
+  if (q.nt == 2)
+    hipLaunchKernelGGL(gpfit_tile_kernel<2>, dim3(P), dim3(TT_THREADS), gpfit_tile_lds(q.d, q.N), st, q, P);
+  else
+    hipLaunchKernelGGL(gpfit_tile_kernel<1>, dim3(P), dim3(TT_THREADS), gpfit_tile_lds(q.d, q.N), st, q, P);
 }
 
 }  // namespace mrbo

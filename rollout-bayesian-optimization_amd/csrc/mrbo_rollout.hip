@@ -69,8 +69,8 @@ struct Lay {
   static constexpr int U_DINV = U_GF + FMAX * D;         // Dinv row-major        FMAX*FMAX
   static constexpr int U_CF = U_DINV + FMAX * FMAX;      // fantasy coeffs/surf.  (FMAX+1)*FMAX
   static constexpr int U_FMIN = U_CF + (FMAX + 1) * FMAX;// fmin per surface      FMAX+1
-  static constexpr int U_SC = U_FMIN + FMAX + 1;         // scalars: μ,σ,α,G00,σ²,... 18
-  static constexpr int U_GMU = U_SC + 18;                // ∇μ   D
+  static constexpr int U_SC = U_FMIN + FMAX + 1;         // scalars: μ,σ,α,G00,σ²,... 20
+  static constexpr int U_GMU = U_SC + 20;                // ∇μ   D
   static constexpr int U_GSIG = U_GMU + D;               // ∇σ   D
   static constexpr int U_GAL = U_GSIG + D;               // ∇α   D
   static constexpr int U_MIX = U_GAL + D;                // d2α/dxdθ D
@@ -92,7 +92,7 @@ struct Lay {
   static constexpr int U_HF = U_UB + D;                  // fantasy rows: [x - X_r (D), g1, g2]  FMAX×(D+2)
   static constexpr int U_STAMP = U_HF + FMAX * (D + 2);   // cycle accumulators (MRBO_STAMPS) 20
   static constexpr int U_KC = U_STAMP + 20;              // launch constants (KC_*), see wave_setup
-  static constexpr int U_SIZE = ((U_KC + 12) + 1) & ~1;
+  static constexpr int U_SIZE = ((U_KC + 13) + 1) & ~1;
   static constexpr int G12 = 3 * NR;                     // per-lane [g1, g2, Y0] of the base rows
   static constexpr int EC = SQ ? (2 * FMAX + 1) * NR : 0;  // E (FMAX×NR) + C ((FMAX+1)×NR) in LDS
   static constexpr int WAVE_LDS = BROWS * BS + REDN + U_SIZE + G12 + EC;
@@ -121,14 +121,16 @@ enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, 
        SC_GSIGSIG = 8, SC_GMUTH = 9, SC_GSIGTH = 10, SC_FMIN = 11, SC_ST = 12, SC_CABS = 13,
        // NonUniformCost (kp.cost): the rule value g before weighting, c(x), max_a |∂_a c(x)|
        SC_ARAW = 14, SC_COSTC = 15, SC_GCMAX = 16,
-       SC_ISIG = 17 };   // 1/σ
+       SC_ISIG = 17,     // 1/σ
+       SC_FREE = 18 };   // free set of the last projected-gradient test (bit a: coordinate a free)
 
 // Launch constants the trajectory code reads in its loops, copied into each wave's lane-uniform
 // LDS at wave_setup: read back with ds_read at the point of use instead of being held in SGPRs
 // for the whole kernel, where they overflowed the 102-SGPR budget and were spilled to VGPR lanes
 // (a v_readlane per reload, on the VALU).  Branch conditions keep the kernel-argument copy.
 enum { KC_PSI0 = 0, KC_D2PSI0 = 1, KC_THETA = 2, KC_SIGTOL = 3, KC_GTOL = 4, KC_GCMU = 5, KC_GCSIG = 6,
-       KC_GCD2 = 7, KC_XTOL = 8, KC_FTOL = 9, KC_HTOL = 10, KC_SN2 = 11 };
+       KC_GCD2 = 7, KC_XTOL = 8, KC_FTOL = 9, KC_HTOL = 10, KC_SN2 = 11,
+       KC_BOX = 12 };   // max_a (ub_a − lb_a): the Newton step's length cap
 #define KCV(F) (W.U[Lay<D, RPL>::U_KC + KC_##F])
 
 // ∂_lane c(x) by unrolled select (lane < D; a runtime index would put gc in scratch)
@@ -1067,8 +1069,7 @@ __device__ __forceinline__ bool chol_packed(double (&A)[D * (D + 1) / 2], double
 // operands are loaded unconditionally and combined without short-circuits: a load behind
 // && / || becomes a branch with a full LDS round trip.
 template <int D, int RPL>
-__device__ __forceinline__ double newton_free_set(const WaveCtx<D, RPL>& W, bool (&fr)[D], double (&gs)[D],
-                                                  double& box) {
+__device__ __forceinline__ double newton_free_set(const WaveCtx<D, RPL>& W, bool (&fr)[D], double (&gs)[D]) {
   using Ly = Lay<D, RPL>;
   const double* U = W.U;
   double xs[D], lb[D], ub[D];
@@ -1080,55 +1081,61 @@ __device__ __forceinline__ double newton_free_set(const WaveCtx<D, RPL>& W, bool
     ub[a] = U[Ly::U_UB + a];
   }
   double pg = 0.0;
-  box = 0.0;
 #pragma unroll
   for (int a = 0; a < D; ++a) {
     const bool act = ((xs[a] <= lb[a]) & (gs[a] > 0.0)) | ((xs[a] >= ub[a]) & (gs[a] < 0.0));
     fr[a] = !act;
     pg = act ? pg : fmax(pg, fabs(gs[a]));
-    box = fmax(box, ub[a] - lb[a]);
   }
   return pg;
 }
 
 // Projected-gradient test of the Newton iteration: max |g_a| over the free coordinates > g_tol.
+// The free set is kept (U_SC + SC_FREE, a bit mask) for the direction that follows a passed test.
 template <int D, int RPL>
 __device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL>& W, const KParams& kp) {
   bool fr[D];
-  double gs[D], box;
-  return newton_free_set<D, RPL>(W, fr, gs, box) > KCV(GTOL);
+  double gs[D];
+  const double pg = newton_free_set<D, RPL>(W, fr, gs);
+  int m = 0;
+#pragma unroll
+  for (int a = 0; a < D; ++a) m |= fr[a] ? (1 << a) : 0;
+  if (W.ln() == 0) W.U[Lay<D, RPL>::U_SC + SC_FREE] = (double)m;
+  return pg > KCV(GTOL);
 }
 
-// One projected-Newton direction from the state in U (x = U_NX, g = U_NG, H = U_H).
-// Returns false when the iteration must stop (stationary).  Writes p to U_NP.
+// One projected-Newton direction from the state in U (g = U_NG, H = U_H, the free set of the
+// projected-gradient test that just passed in U_SC + SC_FREE).  Writes p to U_NP.
+// The reduced Hessian A0 (identity on the active set) is formed once: the Gershgorin shift's row
+// sums run over it directly (its masked entries are exact zeros, so the sums are those over the
+// free columns) and the retry adds τ to its free diagonal -- the same values as forming both
+// from Hα with the free-set tests.  p leaves through lane 0's LDS stores (no per-lane select).
 template <int D, int RPL>
 __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KParams& kp) {
   using Ly = Lay<D, RPL>;
+  constexpr int NH = D * (D + 1) / 2;
   double* U = W.U;
+  const int fm = (int)U[Ly::U_SC + SC_FREE];
   bool fr[D];
-  double gs[D], box;
-  const double pg = newton_free_set<D, RPL>(W, fr, gs, box);
-  if (!(pg > KCV(GTOL))) return false;
-  // lower triangle of Hα, read unconditionally (a load under a select becomes a branch with a
-  // full LDS round trip per element)
-  double Hl[D * (D + 1) / 2];
+  double gs[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) {
+    fr[a] = (fm >> a) & 1;
+    gs[a] = U[Ly::U_NG + a];
+  }
+  // masked reduced Hessian of f = -α, packed lower; H read unconditionally (a load under a
+  // select becomes a branch with a full LDS round trip per element)
+  double A0[NH];
 #pragma unroll
   for (int i = 0; i < D; ++i)
 #pragma unroll
-    for (int j = 0; j <= i; ++j) Hl[i * (i + 1) / 2 + j] = U[Ly::U_H + i * D + j];
-  // masked reduced Hessian of f = -α (identity on the active set), packed lower
-  double A[D * (D + 1) / 2];
-  {
-    int t = 0;
+    for (int j = 0; j <= i; ++j) {
+      const double h = U[Ly::U_H + i * D + j];
+      A0[i * (i + 1) / 2 + j] = (fr[i] && fr[j]) ? -h : ((i == j) ? 1.0 : 0.0);
+    }
+  double A[NH], idg[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i)
-#pragma unroll
-      for (int j = 0; j <= i; ++j) {
-        A[t] = (fr[i] && fr[j]) ? -Hl[t] : ((i == j) ? 1.0 : 0.0);
-        ++t;
-      }
-  }
-  double idg[D];
+  for (int t = 0; t < NH; ++t) A[t] = A0[t];
   bool ok = chol_packed<D>(A, idg);
   STAMP(W, 13);
   if (!ok) {  // Gershgorin shift over the free block, one retry
@@ -1140,23 +1147,17 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
     for (int i = 0; i < D; ++i) {
       double off = 0.0;
 #pragma unroll
-      for (int j = 0; j < D; ++j) {
-        const double hij = (j <= i) ? Hl[i * (i + 1) / 2 + j] : Hl[j * (j + 1) / 2 + i];
-        off += (j == i || !fr[j]) ? 0.0 : fabs(hij);
-      }
-      const double hii = -Hl[i * (i + 1) / 2 + i];
+      for (int j = 0; j < D; ++j)
+        if (j != i) off += fabs((j < i) ? A0[i * (i + 1) / 2 + j] : A0[j * (j + 1) / 2 + i]);
+      const double hii = A0[i * (i + 1) / 2 + i];
       tau = fr[i] ? fmax(tau, off - hii) : tau;
       hmax = fr[i] ? fmax(hmax, fabs(hii)) : hmax;
     }
     tau += 1e-8 * (1.0 + hmax);
-    int t = 0;
 #pragma unroll
-    for (int i = 0; i < D; ++i)
+    for (int t = 0; t < NH; ++t) A[t] = A0[t];
 #pragma unroll
-      for (int j = 0; j <= i; ++j) {
-        A[t] = (fr[i] && fr[j]) ? -Hl[t] + ((i == j) ? tau : 0.0) : ((i == j) ? 1.0 : 0.0);
-        ++t;
-      }
+    for (int i = 0; i < D; ++i) A[i * (i + 1) / 2 + i] = fr[i] ? A0[i * (i + 1) / 2 + i] + tau : 1.0;
     ok = chol_packed<D>(A, idg);
   }
   STAMP(W, 17);
@@ -1186,13 +1187,13 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
   double pn = 0.0;
 #pragma unroll
   for (int i = 0; i < D; ++i) pn = fmax(pn, fabs(p[i]));
+  const double box = KCV(BOX);
   const double sc = (pn > box) ? box / pn : 1.0;
   wave_sync();
-  const int lane = W.ln();
-  double pmine = 0.0;   // p[lane] by unrolled select (a runtime index puts p in scratch)
+  if (W.ln() == 0) {
 #pragma unroll
-  for (int a = 0; a < D; ++a) pmine = (a == lane) ? p[a] : pmine;
-  if (lane < D) U[Ly::U_NP + lane] = (pn > box) ? pmine * sc : pmine;
+    for (int a = 0; a < D; ++a) U[Ly::U_NP + a] = (pn > box) ? p[a] * sc : p[a];
+  }
   wave_sync();
   STAMP(W, 18);
   return true;
@@ -2279,6 +2280,9 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
     kc[KC_FTOL] = kp.f_tol;
     kc[KC_HTOL] = kp.htol;
     kc[KC_SN2] = kp.sn2;
+    double box = 0.0;
+    for (int a = 0; a < D; ++a) box = fmax(box, kp.ubs[a] - kp.lbs[a]);
+    kc[KC_BOX] = box;
   }
 }
 

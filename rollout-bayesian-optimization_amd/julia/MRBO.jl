@@ -9,7 +9,7 @@
 # Python ctypes harness (rollout-bayesian-optimization_amd/mrbo/_lib.py) and tests/test_gpu.py.
 module MRBO
 
-export MrboBackend, MrboPlan, mrbo_simulate!, mrbo_log_likelihood
+export MrboBackend, MrboPlan, mrbo_simulate!, mrbo_log_likelihood, mrbo_multistart_base_solve!
 
 const libmrbo = joinpath(@__DIR__, "..", "mrbo", "libmrbo.so")
 const MRBO_FLAG_HOST_POINTERS = UInt32(1)
@@ -175,6 +175,50 @@ function simulate_trajectory_ghq(T::Trajectory, tp::TrajectoryParameters, backen
     ∇μθ = vec(Distributions.mean(hyperparameter_gradients_container, dims=2))
     σ_∇μθ = vec(Distributions.std(hyperparameter_gradients_container, dims=2, mean=∇μθ))
     return ExpectedTrajectoryOutput(μxθ=μxθ, σ_μxθ=σ_μxθ, ∇μx=∇μx, σ_∇μx=σ_∇μx, ∇μθ=∇μθ, σ_∇μθ=σ_∇μθ)
+end
+
+
+# multistart_base_solve!(s::Surrogate, xfinal; spatial_lbs, spatial_ubs, guesses, θfixed)
+# (rbf_optim.jl:103-135) with every start's base_solve (:35-66) on the GPU (mrbo_base_solve, one
+# wavefront per start, the build's projected Newton in place of IPNewton) and the reference's
+# candidate filter and findmin here -- the acquisition step of experiments/myopic_bayesopt.jl.
+function mrbo_multistart_base_solve!(s::Surrogate, xfinal::Vector{Float64}; spatial_lbs::Vector{Float64},
+                                     spatial_ubs::Vector{Float64}, guesses::Matrix{Float64},
+                                     θfixed::Vector{Float64}, device::Int = 0)
+    if get_name(get_decision_rule(s)) == "Random"
+        xfinal[:] = spatial_lbs .+ (spatial_ubs .- spatial_lbs) .* rand(length(spatial_lbs))
+        return nothing
+    end
+    N = get_observed(s)
+    X = Matrix(get_active_covariates(s))
+    L = Matrix(get_active_cholesky(s))
+    c = Vector(get_active_coefficients(s))
+    y = Vector(get_active_observations(s))
+    d, n = size(guesses)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    GC.@preserve X L c y spatial_lbs spatial_ubs begin
+        sd = MrboSurrogateC(d, N, kernel_id(get_kernel(s)), get_kernel(s).θ[1], s.σn2, minimum(get_observations(s)),
+                            pointer(X), pointer(L), N, pointer(c), pointer(y), kernel_period(get_kernel(s)))
+        pd = MrboParamsC(0, 1, 1, 1, rule_id(get_decision_rule(s)), θfixed[1], pointer(spatial_lbs),
+                         pointer(spatial_ubs), 50, 20, 1e-3, 1e-3, 1e-8, 1e-4, 1e-8, 1906, 0, 0, 0, 1.0, C_NULL)
+        check(ccall((:mrbo_plan_create, libmrbo), Cint,
+                    (Ref{MrboSurrogateC}, Ref{MrboParamsC}, Cint, Ref{Ptr{Cvoid}}), sd, pd, device, h))
+    end
+    xs, fs, st = zeros(d, n), zeros(n), zeros(Int32, n)
+    try
+        check(ccall((:mrbo_base_solve, libmrbo), Cint,
+                    (Ptr{Cvoid}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int64}, UInt32,
+                     Ptr{Cvoid}),
+                    h[], n, guesses, xs, fs, st, C_NULL, MRBO_FLAG_HOST_POINTERS, C_NULL))
+    finally
+        ccall((:mrbo_plan_destroy, libmrbo), Cint, (Ptr{Cvoid},), h[])
+    end
+    any(!=(0), st) && throw(DomainError(st, "negative posterior variance in base_solve"))
+    candidates = [(xs[:, i], fs[i]) for i in 1:n]
+    candidates = filter(pair -> !any(isnan.(pair[1])), candidates)       # rbf_optim.jl:129
+    mini, j_mini = findmin(pair -> pair[2], candidates)                   # :130
+    xfinal .= candidates[j_mini][1]
+    return nothing
 end
 
 

@@ -120,7 +120,8 @@ def _surrogate(X, y, kernel, ell, sn2=1e-6):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kernel", KERNELS)
-@pytest.mark.parametrize("d,N", [(1, 8), (3, 20), (6, 64), (6, 100), (4, 128), (12, 96), (5, 150), (8, 256)])
+@pytest.mark.parametrize("d,N", [(1, 8), (3, 20), (6, 64), (6, 100), (4, 128), (12, 96), (5, 150), (8, 256),
+                                 (6, 300), (3, 384), (8, 512), (16, 200)])
 def test_gp_fit_vs_oracle(gpu, oracle, kernel, d, N):
     from mrbo.mle import gp_fit_batch
     X, y = _data(d, N, seed=d)
@@ -207,7 +208,7 @@ def _per_surrogate(X, y, th, sn2):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N", [16, 64, 100])
+@pytest.mark.parametrize("N", [16, 64, 100, 300])
 def test_gp_fit_periodic_vs_oracle(gpu, oracle, N):
     from mrbo.mle import gp_fit_batch
     X, y = _per_data(N, seed=N)

@@ -127,9 +127,9 @@ def row_gp_fit(args, N, P=256, d=6):
     wall = (time.perf_counter() - t0) / steps
     assert (stt.cpu().numpy() == 0).all()
     kms, call_ms = float(np.median(kms)), float(np.median(calls))
-    # algorithmic FMAs per fit: Cholesky N³/6, then N ≤ 128 (register / LDS kernels) L⁻¹ N³/6 +
-    # lower(VᵀV) N³/6; N > 128 (gpfit_kernel) Z = L⁻¹δK N³/2 + L⁻¹ N³/6; 2 flops per FMA
-    flops = 2.0 * (N ** 3 / 6 + (N ** 3 / 3 if N <= 128 else N ** 3 / 2 + N ** 3 / 6)) * P
+    # algorithmic FMAs per fit: Cholesky N³/6, L⁻¹ N³/6, lower(VᵀV) N³/6 (register / LDS kernels
+    # and the tile kernel alike); 2 flops per FMA
+    flops = 2.0 * (N ** 3 / 2) * P
     # oracle: one fit per call, threads over candidates
     nt = cpu_threads()
     nP = min(P, 16)
@@ -162,7 +162,7 @@ def main():
     if "ghq" in rows:
         print(json.dumps(row_ghq(args)), flush=True)
     if "gp_fit" in rows:
-        for N in (64, 128, 256):
+        for N in (64, 128, 256, 384, 512):
             print(json.dumps(row_gp_fit(args, N)), flush=True)
 
 

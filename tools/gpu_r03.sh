@@ -5,6 +5,9 @@
 #   smoke     __graft_entry__.smoke()
 #   bench     python bench.py (the driver's default line, C3)
 #   rows      bench rows: C3 at the MLE ℓ, C4 at ℓ = 0.5 and MLE, C2 (no CPU baseline)
+#   ab        A/B of the library variants in mrbo/variants (AB_VARIANTS, default "old new oldst newst")
+#   gpfit     tools/bench_rows.py gp_fit rows (N = 64 .. 512, 256 lengthscales per launch)
+#   bo        tools/bo_compare.py, 40 trials per case, every case -> bo_compare.jsonl
 #   prof      rocprofv3 --kernel-trace --stats of the default bench (1 step) + FETCH_SIZE / WRITE_SIZE
 #             passes (tools/profile.sh), C3 and C3-MLE
 # Outputs under gpurun_out/<tag>/.
@@ -41,6 +44,19 @@ for step in "$@"; do
     prof)
       bash tools/profile.sh "${tag}_c3" && bash tools/profile.sh "${tag}_c3mle" --steps 1 --warmup 1 --no-cpu-baseline --mle
       rc=$? ;;
+    ab)
+      AB_TAG="" timeout -k 10 400 bash tools/ab_run.sh ${AB_VARIANTS:-old new oldst newst} > "$out/ab.log" 2>&1
+      rc=$?; cp gpurun_out/ab_*.json gpurun_out/ab_*.err "$out/" 2>/dev/null; grep -v "^\[mrbo stamps\] .*0.00%" "$out/ab.log" | tail -60 ;;
+    gpfit)
+      timeout -k 10 400 python -u tools/bench_rows.py --rows gp_fit --cpu-seconds 2 > "$out/gpfit_rows.jsonl" 2> "$out/gpfit_rows.err"
+      rc=$?; python -c "
+import sys, json
+for l in open(sys.argv[1]):
+    if l.startswith('{'):
+        d = json.loads(l); print(d['config']['workload'], round(d['value']), 'fits/s;', round(d['kernel_ms'], 3), 'ms kernel; frac', round(d['roofline']['frac'], 4))" "$out/gpfit_rows.jsonl" ;;
+    bo)
+      timeout -k 10 900 python -u tools/bo_compare.py --trials 40 --out "$out/bo_compare.jsonl" > /dev/null 2> "$out/bo_compare.err"
+      rc=$?; grep "final gap" "$out/bo_compare.err" ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac
   echo "== $step rc=$rc $(date +%T)"
