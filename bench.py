@@ -167,7 +167,7 @@ def main():
     import torch
     import torch.distributed as dist
     from mrbo import configs, flops, parallel
-    from mrbo.engine import to_device
+    from mrbo.engine import from_device, to_device
     from mrbo.rollout import _plan_for
     from mrbo.utils import sga_step_batch
 
@@ -207,13 +207,23 @@ def main():
     out = plan.alloc_outputs(with_gradient=True)
     evals_acc = torch.zeros_like(out["evals"])
     active = np.ones(R, dtype=bool)
+    dactive = torch.ones(R, dtype=torch.int32, device=dev)
     W = parallel.width(d)
     kernel_ms = []
+    events = []
     last = {}
+    stream = torch.cuda.current_stream(local)
 
     def step(timed):
-        dx0.copy_(torch.from_numpy(x0.ravel(order="F")), non_blocking=False)
+        if world > 1:
+            dx0.copy_(torch.from_numpy(x0.ravel(order="F")), non_blocking=False)
+        if timed:   # HIP events on the launch stream around the rollout launch, read after the loop
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(stream)
         plan.simulate(dx0, drn, dxs, out)
+        if timed:
+            ev[1].record(stream)
+            events.append(ev)
         if world == 1:
             e = plan.eto(out)                           # two-pass mean / std(n-1) on the device
         else:
@@ -222,14 +232,15 @@ def main():
         if args.longest_first:
             plan.order_longest_first(out)   # the next step's schedule (same work)
         if world == 1:
-            eto = e.cpu().numpy().reshape((W, R), order="F")
+            # eswavs + StandardSGA of every active restart on the device (mrbo_sga_step): x0 and the
+            # stop flags stay in HBM, so the next launch follows without a host round trip
+            plan.sga_step(e, dx0, dactive, M_total, args.eta)
+            last["eto_dev"] = e
         else:
             eto = parallel.sharded_eto(e, [b - a for a, b in shards], d)
-        last["eto"] = eto
-        # eswavs + StandardSGA of every active restart at once (utils.jl:114-123, optimizers.jl:16-22)
-        sga_step_batch(x0, active, eto[2:2 + d], eto[2 + d:2 + 2 * d], M_total, args.eta)
-        if timed:
-            kernel_ms.append(plan.last_kernel_ms())
+            last["eto"] = eto
+            # eswavs + StandardSGA of every active restart at once (utils.jl:114-123, optimizers.jl:16-22)
+            sga_step_batch(x0, active, eto[2:2 + d], eto[2 + d:2 + 2 * d], M_total, args.eta)
 
     for _ in range(args.warmup):
         step(False)
@@ -250,6 +261,11 @@ def main():
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    kernel_ms = [a.elapsed_time(b) for a, b in events]
+    if world == 1:
+        last["eto"] = last["eto_dev"].cpu().numpy().reshape((W, R), order="F")
+        x0 = from_device(dx0, (d, R))
+        active = dactive.cpu().numpy().astype(bool)
 
     st = out["status"].cpu().numpy()
     ev = evals_acc.cpu().numpy().reshape((flops.NCOUNTERS, hi - lo, R), order="F") / max(args.steps, 1)

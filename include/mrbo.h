@@ -179,6 +179,16 @@ int mrbo_simulate_ghq(mrbo_plan_t* plan, const double* x0s, const double* nodes,
 int mrbo_eto_reduce(mrbo_plan_t* plan, const double* values, const double* grad_x, const double* grad_theta,
                     double* eto, uint32_t flags, void* stream);
 
+/* One step of the outer stochastic gradient ascent for the plan's R restarts, on the device
+ * (stochastic_solve utils.jl:235-265): for every restart r with active[r] ≠ 0, eswavs
+ * (utils.jl:114-123) on the ETO row r of eto (mrbo_eto_reduce's layout) with sample_size = the
+ * global MC samples -- 1 − (sample_size/d)·Σ_a ∇μx_a²/σ_∇μx_a² > 0 sets active[r] = 0 -- else
+ * StandardSGA update! (optimizers.jl:16-22) x0s[:, r] += η·∇μx.  Device pointers only (eto R×W,
+ * x0s d×R, active R int32); asynchronous on `stream`, so consecutive launches of the ascent need
+ * no host round trip.                                                                           */
+int mrbo_sga_step(mrbo_plan_t* plan, const double* eto, double* x0s, int32_t* active, double sample_size, double eta,
+                  uint32_t flags, void* stream);
+
 /* Shard moments for the multi-GPU exchange: moments R×(2+2d+2) = [Σα, M2α, Σ∇x(d), M2∇x(d), Σ∇θ, M2∇θ]
  * over the first M_local samples of each restart (the outputs keep the plan's M as the restart
  * stride; 1 ≤ M_local ≤ M), M2 = Σ(x − x̄_local)² by two passes.  Ranks all-gather

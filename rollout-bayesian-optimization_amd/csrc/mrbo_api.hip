@@ -200,6 +200,28 @@ __global__ void __launch_bounds__(256) reduce_kernel(const double* values, const
   }
 }
 
+// ---- outer ascent step on the device (stochastic_solve utils.jl:235-265): per active restart r,
+// eswavs (utils.jl:114-123) on the ETO's ∇μx and σ_∇μx -- stop when 1 − (M/d)·Σ_a ∇_a²/σ_a² > 0 (a
+// NaN ratio keeps iterating, as in Julia) -- else StandardSGA update! x += η·∇ (optimizers.jl:16-22).
+// One thread per restart; the x0 batch never leaves the device between launches.
+__global__ void __launch_bounds__(64) sga_kernel(const double* eto, double* x0s, int* active, int R, int d,
+                                                 double sample_size, double eta) {
+#pragma clang fp contract(off)   // the host mirror's (numpy) roundings: no fused multiply-adds
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R || !active[r]) return;
+  const double* e = eto + (size_t)(2 + 2 * d + 2) * r;
+  double ratio = 0.0;
+  for (int a = 0; a < d; ++a) {
+    const double g = e[2 + a], s = e[2 + d + a];
+    ratio += (g * g) / (s * s);
+  }
+  if (1.0 - (sample_size / d) * ratio > 0.0) {
+    active[r] = 0;
+    return;
+  }
+  for (int a = 0; a < d; ++a) x0s[(size_t)d * r + a] = x0s[(size_t)d * r + a] + eta * e[2 + a];
+}
+
 // ---- host Sobol (Joe-Kuo directions, Gray code, zero point skipped) ---------------------
 struct Sobol {
   int dim;
@@ -648,6 +670,18 @@ int mrbo_partial_moments(mrbo_plan_t* P, const double* values, const double* gra
   // reduces the first M_local samples of every restart
   if (P && (M_local < 1 || M_local > P->p.M)) return fail(MRBO_ERR_ARG, "M_local=%d outside [1, %d]", M_local, P->p.M);
   return reduce_common(P, values, grad_x, grad_theta, M_local, moments, 1, flags, stream);
+}
+
+int mrbo_sga_step(mrbo_plan_t* P, const double* eto, double* x0s, int32_t* active, double sample_size, double eta,
+                  uint32_t flags, void* stream) {
+  if (!P || !eto || !x0s || !active) return fail(MRBO_ERR_ARG, "null argument");
+  if (flags & MRBO_FLAG_HOST_POINTERS) return fail(MRBO_ERR_ARG, "mrbo_sga_step takes device pointers");
+  if (hipSetDevice(P->device) != hipSuccess) return fail(MRBO_ERR_HIP, "hipSetDevice");
+  const int R = P->p.R;
+  hipLaunchKernelGGL(sga_kernel, dim3((R + 63) / 64), dim3(64), 0, (hipStream_t)stream, eto, x0s, (int*)active, R, P->d,
+                     sample_size, eta);
+  HIP_TRY(hipGetLastError());
+  return MRBO_OK;
 }
 
 int mrbo_eval_base(mrbo_plan_t* P, int32_t npts, const double* xs, double* out, uint32_t flags, void* stream) {

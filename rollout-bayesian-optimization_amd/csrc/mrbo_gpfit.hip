@@ -609,12 +609,12 @@ __global__ void __launch_bounds__(GL_THREADS) gpfit_lds_kernel(GpFitParams q, in
 // W_k = L_kk⁻¹ (column-major); T = ⌈N/32⌉, rows and columns past N are identity rows of K (their
 // L, V and K⁻¹ rows are identity rows too, and they take no part in the sums).
 //   Cholesky, right-looking by tile columns k: wave 0 factors A_kk and inverts L_kk in LDS; the
-//   panel L_Ik = A_Ik·W_kᵀ and the trailing updates A_IJ −= L_Ik·L_Jkᵀ are 32³ products spread
-//   over the four waves, each 32 v_mfma_f64_16x16x4 (tile_xyt: C += X·Yᵀ with X and Y read as
-//   column-major tiles -- both fragment loads coalesced).
+//   panel L_Ik = A_Ik·L_kk⁻ᵀ by substitution (one row per lane); the trailing updates
+//   A_IJ −= L_Ik·L_Jkᵀ are 32³ products spread over the four waves, each 32 v_mfma_f64_16x16x4
+//   (tile_xyt: C += X·Yᵀ with X and Y read as column-major tiles -- both fragment loads coalesced).
 //   V = L⁻¹ by tile rows I: V_IJ = −W_I·Σ_{J≤M<I} L_IM V_MJ.  V is stored row-major, i.e. as the
 //   column-major Vᵀ the later products read.
-//   u = V y, c = Vᵀu (so yᵀc = uᵀu), and K⁻¹_IJ = Σ_{M≥I} V_MIᵀ V_MJ for I ≥ J, whose tile the
+//   c = L'\(L\y) by blocked substitution, and K⁻¹_IJ = Σ_{M≥I} V_MIᵀ V_MJ for I ≥ J, whose tile the
 //   wave holds in registers while it adds K⁻¹_ij·δK_t,ij and c_i c_j·δK_t,ij over the strictly
 //   lower entries (δK on the fly; δK_ii = 0), as the LDS kernel above does.
 // ≈ N³/2 multiply-adds (N³/6 each for L, V and K⁻¹), all but the diagonal tiles' on the MFMA pipe.
@@ -694,7 +694,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   double* rd = Wk + TT * TT_LD;          // 1/L_ii of the tile
   double* Sw = rd + TT;                  // per-wave 32 × 32 scratch (row-major S)
   double* yv = Sw + 4 * TT * TT;         // y, then c
-  double* uv = yv + NP;                  // u = V y
+  double* uv = yv + NP;                  // z = L⁻¹y
   __shared__ double part[TT_THREADS / 64][2 * NT + 2];
   __shared__ int fail;
   double ell, per;
@@ -783,12 +783,30 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     }
     __syncthreads();
     if (fail) break;
-    // panel: L_Ik = A_Ik·W_kᵀ
+    // panel: L_Ik = A_Ik·L_kk⁻ᵀ by forward substitution, one row per lane (lanes < 32) in the
+    // wave's LDS scratch: L_Ik[r][c] = (A_Ik[r][c] − Σ_{m<c} L_Ik[r][m]·L_kk[c][m]) / L_kk[c][c], the
+    // factor's own recurrence (a product with the explicit inverse W_k is ≈ κ(L_kk) less accurate)
     for (int I = k + 1 + w; I < T; I += 4) {
-      f64x4 c[2][2];
-      tile_zero(c);
-      tile_xyt<false>(c, Lt + tile_at(I, k), Wt + (size_t)k * (TT * TT), lane);
-      tile_store<false>(c, Lt + tile_at(I, k), lane);
+      double* A = Lt + tile_at(I, k);
+      double* S = Sw + w * (TT * TT);
+      for (int e = lane; e < TT * TT; e += 64) S[e] = A[e];
+      gr_sync();
+      if (lane < TT) {
+        const int r = lane;
+        for (int c = 0; c < TT; ++c) {
+          double v0 = S[c * TT + r], v1 = 0.0;
+          int m = 0;
+          for (; m + 2 <= c; m += 2) {
+            v0 = fma(-S[m * TT + r], Dk[m * TT_LD + c], v0);
+            v1 = fma(-S[(m + 1) * TT + r], Dk[(m + 1) * TT_LD + c], v1);
+          }
+          if (m < c) v0 = fma(-S[m * TT + r], Dk[m * TT_LD + c], v0);
+          S[c * TT + r] = (v0 + v1) * rd[c];
+        }
+      }
+      gr_sync();
+      for (int e = lane; e < TT * TT; e += 64) A[e] = S[e];
+      gr_sync();
     }
     __syncthreads();
     // trailing update A_IJ −= L_Ik·L_Jkᵀ, k < J ≤ I
@@ -830,29 +848,49 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     }
     __syncthreads();
   }
-  // u = V y, yᵀc = uᵀu, c = Vᵀu (rows / columns of the row-major tiles)
-  double yc = 0.0;
-  for (int i = tid; i < NP; i += TT_THREADS) {
-    const int I = i / TT, ii = i % TT;
-    double s = 0.0;
-    for (int J = 0; J <= I; ++J) {
-      const double* v = Vt + tile_at(I, J) + ii * TT;
-      for (int jj = 0; jj < TT; ++jj) s = fma(v[jj], yv[TT * J + jj], s);
+  // c = L'\(L\y) by blocked substitution (wave 0; lane i < 32 = row i of the current tile):
+  // forward z_I = L_II⁻¹(y_I − Σ_{J<I} L_IJ z_J), backward c_I = L_II⁻ᵀ(z_I − Σ_{J>I} L_JIᵀ c_J);
+  // inside a tile the column-oriented substitution with the solved entry broadcast by readlane.
+  // yᵀc as the reference's log_likelihood forms it.
+  if (w == 0) {
+    const int i = lane & 31;
+    double yc = 0.0;
+    for (int I = 0; I < T; ++I) {
+      double r = yv[TT * I + i];
+      for (int J = 0; J < I; ++J) {
+        const double* L = Lt + tile_at(I, J);
+        for (int j = 0; j < TT; ++j) r = fma(-L[j * TT + i], uv[TT * J + j], r);
+      }
+      const double* L = Lt + tile_at(I, I);
+      for (int m = 0; m < TT; ++m) {
+        const double zm = readlane_d(r, m) / L[m * TT + m];
+        if (i == m) r = zm;
+        else if (i > m) r = fma(-L[m * TT + i], zm, r);
+      }
+      if (lane < TT) uv[TT * I + i] = r;   // z
+      gr_sync();
     }
-    uv[i] = s;
-    yc = fma(s, s, yc);
-  }
-  yc = gr_sum(yc);
-  if (lane == 0) part[w][2 * NT] = yc;
-  __syncthreads();
-  for (int j = tid; j < NP; j += TT_THREADS) {
-    const int J = j / TT, jj = j % TT;
-    double s = 0.0;
-    for (int I = J; I < T; ++I) {
-      const double* v = Vt + tile_at(I, J) + jj;
-      for (int ii = 0; ii < TT; ++ii) s = fma(v[ii * TT], uv[TT * I + ii], s);
+    for (int I = T - 1; I >= 0; --I) {
+      double r = uv[TT * I + i];
+      for (int J = I + 1; J < T; ++J) {
+        const double* L = Lt + tile_at(J, I);
+        for (int j = 0; j < TT; ++j) r = fma(-L[i * TT + j], yv[TT * J + j], r);
+      }
+      const double* L = Lt + tile_at(I, I);
+      for (int m = TT - 1; m >= 0; --m) {
+        const double cm = readlane_d(r, m) / L[m * TT + m];
+        if (i == m) r = cm;
+        else if (i < m) r = fma(-L[i * TT + m], cm, r);
+      }
+      gr_sync();
+      if (lane < TT) {
+        if (TT * I + i < N) yc = fma(q.y[TT * I + i], r, yc);
+        yv[TT * I + i] = r;   // c (y_I is no longer needed: rows > I are done)
+      }
+      gr_sync();
     }
-    yv[j] = s;   // c
+    yc = gr_sum(yc);
+    if (lane == 0) part[0][2 * NT] = yc;
   }
   __syncthreads();
   // K⁻¹ tiles and the traces over the strictly lower entries
@@ -899,8 +937,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       const double cgs = (part[0][NT + t] + part[1][NT + t]) + (part[2][NT + t] + part[3][NT + t]);
       q.grad[(size_t)p * NT + t] = cgs - trs;
     }
-    const double ycs = (part[0][2 * NT] + part[1][2 * NT]) + (part[2][2 * NT] + part[3][2 * NT]);
-    q.ll[p] = -0.5 * ycs - part[0][2 * NT + 1] - 0.5 * N * log(2.0 * 3.141592653589793);
+    q.ll[p] = -0.5 * part[0][2 * NT] - part[0][2 * NT + 1] - 0.5 * N * log(2.0 * 3.141592653589793);
     q.status[p] = 0;
   }
   if (q.L_out) {

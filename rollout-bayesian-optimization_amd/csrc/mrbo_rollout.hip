@@ -1065,43 +1065,23 @@ __device__ __forceinline__ bool chol_packed(double (&A)[D * (D + 1) / 2], double
   return ok;
 }
 
-// Free set of the projected Newton step and the projected-gradient norm max_F |g_a|.  All
-// operands are loaded unconditionally and combined without short-circuits: a load behind
-// && / || becomes a branch with a full LDS round trip.
-template <int D, int RPL>
-__device__ __forceinline__ double newton_free_set(const WaveCtx<D, RPL>& W, bool (&fr)[D], double (&gs)[D]) {
-  using Ly = Lay<D, RPL>;
-  const double* U = W.U;
-  double xs[D], lb[D], ub[D];
-#pragma unroll
-  for (int a = 0; a < D; ++a) {
-    xs[a] = U[Ly::U_NX + a];
-    gs[a] = U[Ly::U_NG + a];
-    lb[a] = U[Ly::U_LB + a];
-    ub[a] = U[Ly::U_UB + a];
-  }
-  double pg = 0.0;
-#pragma unroll
-  for (int a = 0; a < D; ++a) {
-    const bool act = ((xs[a] <= lb[a]) & (gs[a] > 0.0)) | ((xs[a] >= ub[a]) & (gs[a] < 0.0));
-    fr[a] = !act;
-    pg = act ? pg : fmax(pg, fabs(gs[a]));
-  }
-  return pg;
-}
-
-// Projected-gradient test of the Newton iteration: max |g_a| over the free coordinates > g_tol.
-// The free set is kept (U_SC + SC_FREE, a bit mask) for the direction that follows a passed test.
+// Projected-gradient test of the Newton iteration: max |g_a| over the free coordinates > g_tol,
+// i.e. some free coordinate's |g_a| exceeds g_tol (NaN components count in neither form).  Lane
+// a < D tests coordinate a; the free set (bit a: coordinate a free, i.e. not at a bound with the
+// gradient pushing out of the box) is kept in U_SC + SC_FREE for the direction that follows.
 template <int D, int RPL>
 __device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL>& W, const KParams& kp) {
-  bool fr[D];
-  double gs[D];
-  const double pg = newton_free_set<D, RPL>(W, fr, gs);
-  int m = 0;
-#pragma unroll
-  for (int a = 0; a < D; ++a) m |= fr[a] ? (1 << a) : 0;
-  if (W.ln() == 0) W.U[Lay<D, RPL>::U_SC + SC_FREE] = (double)m;
-  return pg > KCV(GTOL);
+  using Ly = Lay<D, RPL>;
+  const double* U = W.U;
+  const int lane = W.ln();
+  const int a = lane < D ? lane : 0;
+  const double xs = U[Ly::U_NX + a], gs = U[Ly::U_NG + a], lb = U[Ly::U_LB + a], ub = U[Ly::U_UB + a];
+  const bool act = ((xs <= lb) & (gs > 0.0)) | ((xs >= ub) & (gs < 0.0));
+  const bool fr = (lane < D) & !act;
+  const unsigned long long fm = __ballot(fr);
+  const unsigned long long big = __ballot(fr & (fabs(gs) > KCV(GTOL)));
+  if (lane == 0) W.U[Ly::U_SC + SC_FREE] = (double)(unsigned)fm;
+  return big != 0ull;
 }
 
 // One projected-Newton direction from the state in U (g = U_NG, H = U_H, the free set of the
@@ -1199,22 +1179,23 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
   return true;
 }
 
-// x_t = clamp(x + t p) -> U_X ; returns gᵀ(x_t - x)
+// x_t = clamp(x + t p) -> U_X ; returns gᵀ(x_t - x).  Lane a < D computes coordinate a (its own
+// LDS loads and clamp, one store); the inner product is then summed in coordinate order from the
+// lanes' terms by readlane -- the same fused multiply-adds in the same order as a lane-uniform loop.
 template <int D, int RPL>
 __device__ __forceinline__ double newton_trial_point(WaveCtx<D, RPL>& W, double t) {
   using Ly = Lay<D, RPL>;
   double* U = W.U;
   const int lane = W.ln();
-  double dec = 0.0, mine = 0.0;
-#pragma unroll
-  for (int a = 0; a < D; ++a) {
-    const double xa = U[Ly::U_NX + a];
-    const double xt = clampd(xa + t * U[Ly::U_NP + a], U[Ly::U_LB + a], U[Ly::U_UB + a]);
-    dec += U[Ly::U_NG + a] * (xt - xa);
-    if (a == lane) mine = xt;
-  }
+  const int a = lane < D ? lane : 0;
+  const double xa = U[Ly::U_NX + a];
+  const double xt = clampd(xa + t * U[Ly::U_NP + a], U[Ly::U_LB + a], U[Ly::U_UB + a]);
+  const double ga = U[Ly::U_NG + a], da = xt - xa;
   wave_sync();
-  if (lane < D) U[Ly::U_X + lane] = mine;
+  if (lane < D) U[Ly::U_X + lane] = xt;
+  double dec = 0.0;
+#pragma unroll
+  for (int b = 0; b < D; ++b) dec = fma(readlane_d(ga, b), readlane_d(da, b), dec);
   wave_sync();
   return dec;
 }
@@ -1390,16 +1371,16 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
         dec = newton_trial_point<D, RPL>(W, t);
         continue;
       }
-      double dx = 0.0, mine = 0.0;                 // accept x_t
+      // accept x_t: lane a < D moves its coordinate; ‖Δx‖∞ from the lanes' |Δx_a| (max: order-free)
+      const int ca = lane < D ? lane : 0;
+      const double xt = U[Ly::U_X + ca];
+      const double dxa = fabs(xt - U[Ly::U_NX + ca]);
+      double dx = 0.0;
 #pragma unroll
-      for (int a = 0; a < D; ++a) {
-        const double xt = U[Ly::U_X + a];
-        dx = fmax(dx, fabs(xt - U[Ly::U_NX + a]));
-        if (a == lane) mine = xt;
-      }
+      for (int a = 0; a < D; ++a) dx = fmax(dx, readlane_d(dxa, a));
       const double df = fabs(ft - f);
       wave_sync();
-      if (lane < D) U[Ly::U_NX + lane] = mine;
+      if (lane < D) U[Ly::U_NX + lane] = xt;
       wave_sync();
       f = ft;
       ++it;

@@ -144,6 +144,15 @@ class RolloutPlan:
                                               ctypes.c_void_p(st.cuda_stream)))
         return e
 
+    def sga_step(self, eto, x0s, active, sample_size, eta, stream=None):
+        """mrbo_sga_step: eswavs + StandardSGA for every active restart, in place on the device
+        tensors x0s (d·R, column-major) and active (R, int32); eto from `eto()`."""
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())
+        _lib.check(self.lib.mrbo_sga_step(self.handle, p(eto), p(x0s), p(active), float(sample_size), float(eta), 0,
+                                          ctypes.c_void_p(st.cuda_stream)))
+
     def eval_base(self, xs):
         """eval(s, x, θ) at the columns of xs (d×P); returns (3+4d+d²)×P numpy."""
         torch = _torch()

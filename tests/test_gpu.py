@@ -298,3 +298,27 @@ def test_work_order_changes_nothing_but_the_schedule(gpu, name, M, R):
     plan.set_order(None)
     r_none = _run(plan, g)
     np.testing.assert_array_equal(r_id["values"], r_none["values"])
+
+
+def test_device_sga_step_matches_host(gpu):
+    """mrbo_sga_step (eswavs utils.jl:114-123 + StandardSGA optimizers.jl:16-22 on the device, as
+    bench.py's outer step) against the host mirror sga_step_batch, bit for bit: both branches of
+    the stop rule, an already-stopped restart untouched."""
+    import torch
+    from mrbo.engine import from_device, to_device
+    from mrbo.utils import sga_step_batch
+    g = _problem_arrays("C3", 32, 8)
+    p = _plan(g)
+    r = _run(p, g, want_policy=False)
+    d, R = p.d, p.R
+    eto = np.asfortranarray(r["eto"])
+    for sample_size in (32.0, 1e-3, 1e6):     # iterate / stop everything / mixed
+        x0 = np.array(g["x0s"], dtype=np.float64, order="F")
+        active = np.ones(R, dtype=bool)
+        active[3] = False
+        dx, da = to_device(x0, "cuda:0"), torch.tensor(active.astype(np.int32), device="cuda:0")
+        p.sga_step(to_device(eto, "cuda:0"), dx, da, sample_size, 0.01)
+        torch.cuda.synchronize()
+        sga_step_batch(x0, active, eto[2:2 + d], eto[2 + d:2 + 2 * d], sample_size, 0.01)
+        np.testing.assert_array_equal(from_device(dx, (d, R)), x0)
+        np.testing.assert_array_equal(da.cpu().numpy().astype(bool), active)
