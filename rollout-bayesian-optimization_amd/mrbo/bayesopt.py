@@ -46,6 +46,11 @@ TESTFNS = {
     "rosenbrock": T.TestRosenbrock,
     **{f"ackley{d}d": (lambda d=d: T.TestAckley(d)) for d in (1, 2, 3, 4, 5, 8)},
     **{f"rastrigin{d}d": (lambda d=d: T.TestRastrigin(d)) for d in (1, 4)},
+    "hartmann3d": T.TestHartmann3D,
+    "sixhump": T.TestSixHump,
+    "goldsteinprice": T.TestGoldsteinPrice,
+    "griewank3d": lambda: T.TestGriewank(3),
+    "levy10d": lambda: T.TestLevy(10),
 }
 
 

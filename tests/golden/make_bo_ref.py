@@ -5,8 +5,9 @@ Data only: the per-trial `gaps` rows the reference's experiment drivers wrote (c
 write_to_csv, utils.jl:155-172; gap = (initial_best − observed_best)/(initial_best − f*), utils.jl
 `gap`), for the cases tools/bo_compare.py runs against the MI355X BO loop (mrbo/bayesopt.py):
 
-  myopic_<fn>_ei     experiments/myopic/<fn>/ei_gaps.csv (myopic_bayesopt.jl: EI multistart
-                     solve, 64 starts, 5 initial points, budget 100, 60 trials, optimize!)
+  myopic_<fn>_<rule> experiments/myopic/<fn>/<rule>_gaps.csv (myopic_bayesopt.jl: EI / POI / LCB
+                     multistart solve, 64 starts, 5 initial points, budget 100 -- steps 1..30
+                     kept --, 60 trials, optimize!)
   rollout_h<h>_<fn>  experiments/archived/nonmyopic-shortrun-gaps-and-time/nonmyopic_bayesopt/
                      <fn>/rollout_h<h>_gaps.csv (an earlier nonmyopic_bayesopt.jl: rollout
                      acquisition, 8 starts, batch 8, 100 MC samples, 50 SGD iterations, budget 20,
@@ -23,14 +24,14 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
-CASES = {
-    "myopic_braninhoo_ei": "experiments/myopic/braninhoo/ei_gaps.csv",
-    "myopic_hartmann6d_ei": "experiments/myopic/hartmann6d/ei_gaps.csv",
-    "rollout_h0_braninhoo": "experiments/archived/nonmyopic-shortrun-gaps-and-time/nonmyopic_bayesopt/braninhoo/rollout_h0_gaps.csv",
-    "rollout_h1_braninhoo": "experiments/archived/nonmyopic-shortrun-gaps-and-time/nonmyopic_bayesopt/braninhoo/rollout_h1_gaps.csv",
-    "rollout_h0_gramacylee": "experiments/archived/nonmyopic-shortrun-gaps-and-time/nonmyopic_bayesopt/gramacylee/rollout_h0_gaps.csv",
-    "rollout_h1_gramacylee": "experiments/archived/nonmyopic-shortrun-gaps-and-time/nonmyopic_bayesopt/gramacylee/rollout_h1_gaps.csv",
-}
+ARCHIVE = "experiments/archived/nonmyopic-shortrun-gaps-and-time/nonmyopic_bayesopt"
+MYOPIC_FNS = ["braninhoo", "hartmann6d", "ackley5d", "goldsteinprice", "sixhump", "griewank3d", "levy10d"]
+ROLLOUT_FNS = ["braninhoo", "gramacylee", "ackley1d", "ackley2d", "ackley3d", "ackley4d", "rosenbrock", "hartmann3d",
+               "sixhump", "goldsteinprice"]
+CASES = {f"myopic_{fn}_{rule}": f"experiments/myopic/{fn}/{rule}_gaps.csv"
+         for fn in MYOPIC_FNS for rule in ("ei", "poi", "lcb")}
+CASES.update({f"rollout_h{h}_{fn}": f"{ARCHIVE}/{fn}/rollout_h{h}_gaps.csv" for fn in ROLLOUT_FNS for h in (0, 1)})
+MYOPIC_LABELS = 30   # the myopic files run to budget 100; the comparison uses steps 1..30
 
 
 def read_gaps(path):
@@ -56,6 +57,9 @@ def main():
         header, trials = read_gaps(os.path.join(a.reference, rel))
         trel = rel.replace("_gaps.csv", "_times.csv")
         theader, times = read_gaps(os.path.join(a.reference, trel))
+        if key.startswith("myopic"):   # keep the compared steps only (the fixture travels with the repo)
+            header, trials = header[:MYOPIC_LABELS], [r[:MYOPIC_LABELS] for r in trials]
+            theader, times = theader[:MYOPIC_LABELS], [r[:MYOPIC_LABELS] for r in times]
         out[key] = {"source": rel, "budget_labels": header, "gaps": trials, "times_source": trel,
                     "times_labels": theader, "times": times}
     with open(os.path.join(HERE, "bo_ref_gaps.json"), "w") as f:

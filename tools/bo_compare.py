@@ -35,16 +35,18 @@ sys.path[:0] = [os.path.join(ROOT, "rollout-bayesian-optimization_amd"), ROOT]
 FIXTURE = os.path.join(ROOT, "tests", "golden", "bo_ref_gaps.json")
 
 # per case: our run() settings and the budget labels compared (the reference's column labels)
-SETTINGS = {
-    "myopic_braninhoo_ei": dict(fn="braninhoo", horizon=0, budget=30, initial=5, starts=64, batch=0,
-                                labels=["10", "20", "30"]),
-    "myopic_hartmann6d_ei": dict(fn="hartmann6d", horizon=0, budget=30, initial=5, starts=64, batch=0,
-                                 labels=["10", "20", "30"]),
-    "rollout_h0_braninhoo": dict(fn="braninhoo", horizon=0, budget=20, initial=1, starts=8, batch=8, labels=["5", "10", "20"]),
-    "rollout_h1_braninhoo": dict(fn="braninhoo", horizon=1, budget=20, initial=1, starts=8, batch=8, labels=["5", "10", "20"]),
-    "rollout_h0_gramacylee": dict(fn="gramacylee", horizon=0, budget=20, initial=1, starts=8, batch=8, labels=["5", "10", "20"]),
-    "rollout_h1_gramacylee": dict(fn="gramacylee", horizon=1, budget=20, initial=1, starts=8, batch=8, labels=["5", "10", "20"]),
-}
+MYOPIC_FNS = ["braninhoo", "hartmann6d", "ackley5d", "goldsteinprice", "sixhump", "griewank3d", "levy10d"]
+ROLLOUT_FNS = ["braninhoo", "gramacylee", "ackley1d", "ackley2d", "ackley3d", "ackley4d", "rosenbrock", "hartmann3d",
+               "sixhump", "goldsteinprice"]
+SETTINGS = {f"myopic_{fn}_{rule}": dict(fn=fn, rule=rule, horizon=0, budget=30, initial=5, starts=64, batch=0,
+                                        labels=["10", "20", "30"])
+            for fn in MYOPIC_FNS for rule in ("ei", "poi", "lcb")}
+SETTINGS.update({f"rollout_h{h}_{fn}": dict(fn=fn, rule="ei", horizon=h, budget=20, initial=1, starts=8, batch=8,
+                                            labels=["5", "10", "20"])
+                 for fn in ROLLOUT_FNS for h in (0, 1)})
+# the cases the GPU test asserts (tests/test_bayesopt.py): the round-2 set
+ASSERTED = ["myopic_braninhoo_ei", "myopic_hartmann6d_ei", "rollout_h0_braninhoo", "rollout_h1_braninhoo",
+            "rollout_h0_gramacylee", "rollout_h1_gramacylee"]
 
 
 def load_reference(path=FIXTURE):
@@ -111,7 +113,7 @@ def run_case(key, case, trials, seed, log, solver="sga", eta=0.5, q3=True):
         lg = lambda *m: log(f"[{key}] " + " ".join(map(str, m)))
         if myopic:
             res = bayesopt.run_myopic(s["fn"], tmp, budget=s["budget"], trials=trials, starts=s["starts"], seed=seed,
-                                      rules=("ei",), initial_observations=s["initial"], log=lg)
+                                      rules=(s["rule"],), initial_observations=s["initial"], log=lg)
         else:
             res = bayesopt.run(s["fn"], tmp, budget=s["budget"], trials=trials, starts=s["starts"], horizon=s["horizon"],
                                mc_samples=100, batch_size=s["batch"], sgd_iterations=50, optimize=True, seed=seed,
@@ -120,7 +122,7 @@ def run_case(key, case, trials, seed, log, solver="sga", eta=0.5, q3=True):
         wall = time.perf_counter() - t0
     trials_res = []
     for t in range(trials):
-        r = res[("ei", t) if myopic else (f"rollout_{s['horizon']}_ei", t)]
+        r = res[(s["rule"], t) if myopic else (f"rollout_{s['horizon']}_ei", t)]
         y = r["y"]
         r = dict(r, initial_best=float(np.min(y[:s["initial"]])))
         trials_res.append(r)
@@ -142,7 +144,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--trials", type=int, default=20)
     ap.add_argument("--seed", type=int, default=1906)
-    ap.add_argument("--cases", default=",".join(SETTINGS))
+    ap.add_argument("--cases", default=",".join(SETTINGS), help="comma list, or 'asserted'")
     ap.add_argument("--out", default="")
     ap.add_argument("--solver", default="sga", choices=["sga", "adam"],
                     help="outer solver of the build-defined rollout acquisition (mrbo/bayesopt.py)")
@@ -152,7 +154,7 @@ def main():
     a = ap.parse_args()
     ref = load_reference()
     log = lambda m: print(m, file=sys.stderr, flush=True)
-    for key in a.cases.split(","):
+    for key in (ASSERTED if a.cases == "asserted" else a.cases.split(",")):
         eta = a.eta or (0.5 if a.solver == "sga" else 0.02)
         row = run_case(key, ref[key], a.trials, a.seed, log, solver=a.solver, eta=eta, q3=not a.no_q3)
         line = json.dumps(row)

@@ -7,7 +7,8 @@
 #   rows      bench rows: C3 at the MLE ℓ, C4 at ℓ = 0.5 and MLE, C2 (no CPU baseline)
 #   ab        A/B of the library variants in mrbo/variants (AB_VARIANTS, default "old new oldst newst")
 #   gpfit     tools/bench_rows.py gp_fit rows (N = 64 .. 512, 256 lengthscales per launch)
-#   bo        tools/bo_compare.py, 40 trials per case, every case -> bo_compare.jsonl
+#   bo        tools/bo_compare.py, BO_TRIALS (40) trials per case, BO_CASES (default: the asserted
+#             set; a comma list of tools/bo_compare.py SETTINGS keys) -> bo_compare.jsonl
 #   prof      rocprofv3 --kernel-trace --stats of the default bench (1 step) + FETCH_SIZE / WRITE_SIZE
 #             passes (tools/profile.sh), C3 and C3-MLE
 # Outputs under gpurun_out/<tag>/.
@@ -55,7 +56,8 @@ for l in open(sys.argv[1]):
     if l.startswith('{'):
         d = json.loads(l); print(d['config']['workload'], round(d['value']), 'fits/s;', round(d['kernel_ms'], 3), 'ms kernel; frac', round(d['roofline']['frac'], 4))" "$out/gpfit_rows.jsonl" ;;
     bo)
-      timeout -k 10 900 python -u tools/bo_compare.py --trials 40 --out "$out/bo_compare.jsonl" > /dev/null 2> "$out/bo_compare.err"
+      timeout -k 10 1000 python -u tools/bo_compare.py --trials ${BO_TRIALS:-40} --cases ${BO_CASES:-asserted} \
+        --out "$out/bo_compare.jsonl" > /dev/null 2> "$out/bo_compare.err"
       rc=$?; grep "final gap" "$out/bo_compare.err" ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac
