@@ -7,9 +7,11 @@ multistart_base_solve! (:245-253) and its adaptive driver names a rollout_solver
 defined nowhere (experiments/adaptive_bayesopt.jl:490), so the solver here is build-defined:
 
   batch = generate_batch(batch_size)             utils.jl:97-106 (Sobol + two near-bound points)
+          + one restart next to the incumbent     (build-defined, rollout_solve)
   x_r  ← stochastic_solve from every batch point  utils.jl:235-265 (StandardSGA, eswavs stop),
          all restarts in one rollout launch per SGA iteration (stochastic_solve_batch)
-  xnext = the restart with the largest final ETO mean, clamped to the box
+  xnext = the restart with the largest final ETO mean, clamped to the box, that is not an
+          already observed point
 
 Per budget step the metrics are recorded as in the reference (:268-289): time of the solve,
 gap and simple regret of the observations BEFORE conditioning on xnext, then condition!,
@@ -100,12 +102,36 @@ class BoxAdam:
         return x
 
 
+INCUMBENT_NUDGE = 1e-2     # box widths: the incumbent restart starts this far off the observed point
+
+
+def incumbent_start(sur, lbs, ubs):
+    """The incumbent restart: the best observed point moved INCUMBENT_NUDGE box widths towards the
+    box centre in every coordinate (at an observed point σ and its gradient vanish, so a restart
+    placed exactly there cannot move)."""
+    X, y = sur.get_active_covariates(), sur.get_active_observations()
+    xb = np.asarray(X[:, int(np.argmin(y))], float)
+    w = ubs - lbs
+    step = np.where(xb <= 0.5 * (lbs + ubs), 1.0, -1.0) * INCUMBENT_NUDGE * w
+    return np.clip(xb + step, lbs, ubs)
+
+
 def rollout_solve(sur, lbs, ubs, horizon, mc_samples, batch_size, starts, sgd_iterations, theta, eta=0.5,
-                  device=0, solver="sga"):
+                  device=0, solver="sga", incumbent=True, trace=None):
     """xnext from the rollout acquisition: restarts from a Sobol batch (StandardSGA with step `eta`,
-    or BoxAdam with `eta` box widths per step), best final ETO mean."""
+    or BoxAdam with `eta` box widths per step), best final ETO mean.
+
+    incumbent=True adds one restart next to the best observed point (incumbent_start) and never
+    returns an already observed point while another restart ends elsewhere.  Both are the build's
+    answer to an acquisition that underflows to exactly 0 on the whole Sobol batch -- an objective
+    of large scale under the reference's unit-variance, zero-mean surrogate (Rosenbrock,
+    Goldstein–Price): every batch restart then has a zero gradient, the argmax ties at the first
+    restart and the loop re-observes it for the rest of the budget.
+    `trace`, a list, receives one dict per call (batch, final points, final ETO means, pick)."""
     lbs, ubs = np.asarray(lbs, float), np.asarray(ubs, float)
     batch = generate_batch(batch_size, lbs, ubs)
+    if incumbent:
+        batch = np.hstack([batch, incumbent_start(sur, lbs, ubs)[:, None]])
     tp = TrajectoryParameters(start=batch[:, 0], hypers=[theta], horizon=horizon, mc_iterations=mc_samples,
                               use_low_discrepancy_sequence=True, spatial_lowerbounds=lbs, spatial_upperbounds=ubs)
     es = ExperimentSetup(tp, number_of_starts=starts)
@@ -117,19 +143,28 @@ def rollout_solve(sur, lbs, ubs, horizon, mc_samples, batch_size, starts, sgd_it
         with_gradient=False)
     means = np.array([e.mean() for e in etos])
     means = np.where(np.isfinite(means), means, -np.inf)
-    k = int(np.argmax(means))
+    rank = means.copy()
+    if incumbent:
+        Xa = sur.get_active_covariates()
+        w = ubs - lbs
+        d = np.abs((x[:, :, None] - Xa[:, None, :]) / w[:, None, None]).max(axis=0).min(axis=1)
+        rank = np.where(d > 1e-9, rank, -np.inf) if (d > 1e-9).any() else rank
+    k = int(np.argmax(rank))
+    if trace is not None:
+        trace.append(dict(batch=batch, x=x.copy(), means=means, pick=k))
     return x[:, k].copy(), float(means[k])
 
 
 # ---- the experiment loop (nonmyopic_bayesopt.jl:120-300) -------------------------------------
 def run(function_name, output_dir, budget=15, trials=60, starts=16, horizon=0, mc_samples=200, batch_size=8,
         sgd_iterations=50, optimize=False, seed=1906, device=0, log=print, rules=("ei", "poi", "lcb"), eta=0.5,
-        initial_observations=INITIAL_OBSERVATIONS, solver="sga", fmini_over_capacity=True):
+        initial_observations=INITIAL_OBSERVATIONS, solver="sga", fmini_over_capacity=True, incumbent=True):
     """The experiment loop; `rules` selects a subset of the reference's three acquisitions (all by
     default, as nonmyopic_bayesopt.jl), `eta` the StandardSGA step of the build-defined solver,
     `initial_observations` the initial design size (5 in the current script, :131), `solver` "sga"
     (StandardSGA, η = eta) or "adam" (BoxAdam, eta box widths per step); fmini_over_capacity=False
-    turns the reference's Q3 off (fmini over the observed points, not the zero-padded buffer)."""
+    turns the reference's Q3 off (fmini over the observed points, not the zero-padded buffer),
+    incumbent=False drops rollout_solve's incumbent restart and no-repeat pick (the round-2 solver)."""
     testfn = TESTFNS[function_name]()
     lbs, ubs = testfn.get_bounds()
     directory = os.path.join(output_dir, function_name)
@@ -160,7 +195,7 @@ def run(function_name, output_dir, budget=15, trials=60, starts=16, horizon=0, m
             for b in range(budget):
                 t0 = time.perf_counter()
                 xnext, _ = rollout_solve(sur, lbs, ubs, horizon, mc_samples, batch_size, starts, sgd_iterations,
-                                         theta, eta=eta, device=device, solver=solver)
+                                         theta, eta=eta, device=device, solver=solver, incumbent=incumbent)
                 times[b] = time.perf_counter() - t0
                 observed_best = float(np.min(sur.get_active_observations()))
                 regrets[b] = simple_regret(true_minimum, observed_best)

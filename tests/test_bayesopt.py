@@ -116,15 +116,17 @@ def test_myopic_loop_end_to_end(gpu, tmp_path):
 @pytest.mark.gpu
 def test_bo_comparison_with_reference_runs(gpu):
     """tools/bo_compare.py at 20 trials against the reference's recorded gap curves
-    (tests/golden/bo_ref_gaps.json), at the final budget label of each case:
-      rollout rows (the archived non-myopic runs): no significant difference from the reference's
-        runs (two-sided Mann–Whitney p ≥ 0.05);
-      myopic rows (multistart_base_solve! of analytic EI from 64 + 2 starts,
-        experiments/myopic_bayesopt.jl): no evidence that the build closes LESS of the gap (one-sided
-        p ≥ 0.05).  On Hartmann-6 the build's projected Newton closes more of it than the
-        reference's recorded IPNewton runs (Optim.jl, absent and unpinned).
-    These are tests of NO DETECTED difference at these sample sizes, not of equivalence; the 95 %
-    interval of the difference of mean gaps is recorded beside them (profiles/r03/bo_compare_*.jsonl)."""
+    (tests/golden/bo_ref_gaps.json), at the final budget label of each case: no evidence that the
+    build closes LESS of the gap than the reference's recorded runs (one-sided Mann–Whitney
+    p ≥ 0.05), for
+      rollout rows: the archived non-myopic runs, against the build-defined rollout solver
+        (mrbo/bayesopt.py rollout_solve, with its incumbent restart); it closes more of the gap than
+        the archived runs on Branin, so the test is one-sided, as for
+      myopic rows: multistart_base_solve! of analytic EI from 64 + 2 starts
+        (experiments/myopic_bayesopt.jl); on Hartmann-6 the build's projected Newton closes more of
+        it than the reference's recorded IPNewton runs (Optim.jl, absent and unpinned).
+    A test of NO DETECTED deficit at these sample sizes, not of equivalence; the 95 % interval of
+    the difference of mean gaps is recorded beside them (profiles/r03/bo_compare_*.jsonl)."""
     import sys
     from conftest import ROOT
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -134,6 +136,5 @@ def test_bo_comparison_with_reference_runs(gpu):
     for key in B.ASSERTED:
         row = B.run_case(key, ref[key], 20, 1906, lambda m: None)
         rows[key] = row["gaps"][B.SETTINGS[key]["labels"][-1]]
-    bad = {k: v for k, v in rows.items()
-           if not (v["mannwhitney_p_worse"] if k.startswith("myopic") else v["mannwhitney_p"]) >= 0.05}
+    bad = {k: v for k, v in rows.items() if not v["mannwhitney_p_worse"] >= 0.05}
     assert not bad, bad

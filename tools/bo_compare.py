@@ -102,7 +102,26 @@ def compare(a, b):
     return out
 
 
-def run_case(key, case, trials, seed, log, solver="sga", eta=0.5, q3=True):
+def trajectory_diagnostics(Xs, lbs, ubs, initial):
+    """Shape of the BO observation sequences (same statistics as for the reference's archived
+    observation CSVs in DESIGN.md §10): the fraction of BO observations with a coordinate on the box
+    boundary, the fraction of trials whose first BO step is on it, and the fraction of trials that
+    observed one point twice (a wasted evaluation)."""
+    lb, ub = np.asarray(lbs, float)[:, None], np.asarray(ubs, float)[:, None]
+    atb, first, rep = [], [], []
+    for X in Xs:
+        x = np.asarray(X, float)[:, initial:]
+        b = (np.isclose(x, lb, atol=1e-6) | np.isclose(x, ub, atol=1e-6)).any(0)
+        atb.append(b.mean())
+        first.append(bool(b[0]))
+        dd = np.linalg.norm(x[:, :, None] - x[:, None, :], axis=0)
+        np.fill_diagonal(dd, 1.0)
+        rep.append(bool((dd < 1e-6).any()))
+    return {"obs_at_boundary": float(np.mean(atb)), "first_step_at_boundary": float(np.mean(first)),
+            "trials_with_repeats": float(np.mean(rep))}
+
+
+def run_case(key, case, trials, seed, log, solver="sga", eta=0.5, q3=True, incumbent=True):
     from mrbo import bayesopt
     s = SETTINGS[key]
     testfn = bayesopt.TESTFNS[s["fn"]]()
@@ -118,7 +137,7 @@ def run_case(key, case, trials, seed, log, solver="sga", eta=0.5, q3=True):
             res = bayesopt.run(s["fn"], tmp, budget=s["budget"], trials=trials, starts=s["starts"], horizon=s["horizon"],
                                mc_samples=100, batch_size=s["batch"], sgd_iterations=50, optimize=True, seed=seed,
                                rules=("ei",), initial_observations=s["initial"], solver=solver, eta=eta,
-                               fmini_over_capacity=q3, log=lg)
+                               fmini_over_capacity=q3, incumbent=incumbent, log=lg)
         wall = time.perf_counter() - t0
     trials_res = []
     for t in range(trials):
@@ -127,14 +146,17 @@ def run_case(key, case, trials, seed, log, solver="sga", eta=0.5, q3=True):
         r = dict(r, initial_best=float(np.min(y[:s["initial"]])))
         trials_res.append(r)
     gcols = our_gap_columns(trials_res, true_minimum, s["budget"])
+    lbs, ubs = testfn.get_bounds()
+    diag = trajectory_diagnostics([r["X"] for r in trials_res], lbs, ubs, s["initial"])
     per_label = {lab: compare(our_column(gcols, lab, myopic), ref_column(case, lab)) for lab in s["labels"]}
     our_times = np.concatenate([r["times"] for r in trials_res])
     ref_times = np.array(case["times"], float)[:, :s["budget"]].ravel()
     ref_times = ref_times[ref_times >= 0]
     return {"case": key, "reference": case["source"], "settings": dict(s, trials=trials, mc_samples=100,
                                                                         sgd_iterations=50, optimize=True, solver=solver,
-                                                                        eta=eta, seed=seed, q3_fmini_over_capacity=q3),
-            "gaps": per_label, "ours_mean_curve": gcols.mean(axis=0).tolist(),
+                                                                        eta=eta, seed=seed, q3_fmini_over_capacity=q3,
+                                                                        incumbent_restart=incumbent),
+            "gaps": per_label, "ours_trajectory_diagnostics": diag, "ours_mean_curve": gcols.mean(axis=0).tolist(),
             "seconds_per_solve": {"ours_median": float(np.median(our_times)), "ref_median": float(np.median(ref_times)),
                                   "ref_note": "reference times from earlier code versions on unstated hardware"},
             "wall_s": wall}
@@ -151,22 +173,24 @@ def main():
     ap.add_argument("--eta", type=float, default=0.0, help="step (default 0.5 for sga, 0.02 box widths for adam)")
     ap.add_argument("--no-q3", action="store_true",
                     help="diagnostic: fmini over the observed points instead of the zero-padded buffer (Q3 off)")
+    ap.add_argument("--no-incumbent", action="store_true",
+                    help="diagnostic: the round-2 solver (no incumbent restart, no no-repeat pick)")
     a = ap.parse_args()
     ref = load_reference()
     log = lambda m: print(m, file=sys.stderr, flush=True)
     for key in (ASSERTED if a.cases == "asserted" else a.cases.split(",")):
         eta = a.eta or (0.5 if a.solver == "sga" else 0.02)
-        row = run_case(key, ref[key], a.trials, a.seed, log, solver=a.solver, eta=eta, q3=not a.no_q3)
+        row = run_case(key, ref[key], a.trials, a.seed, log, solver=a.solver, eta=eta, q3=not a.no_q3, incumbent=not a.no_incumbent)
         line = json.dumps(row)
         print(line, flush=True)
         if a.out:
             with open(a.out, "a") as f:
                 f.write(line + "\n")
         g = row["gaps"][SETTINGS[key]["labels"][-1]]
-        log(f"{key} [{a.solver}{'' if not a.no_q3 else ', Q3 off'}]: final gap ours {g['ours_mean']:.3f}±{g['ours_se']:.3f} ref {g['ref_mean']:.3f}±{g['ref_se']:.3f} "
+        log(f"{key} [{a.solver}{'' if not a.no_q3 else ', Q3 off'}{'' if not a.no_incumbent else ', no incumbent'}]: final gap ours {g['ours_mean']:.3f}±{g['ours_se']:.3f} ref {g['ref_mean']:.3f}±{g['ref_se']:.3f} "
             f"diff {g['diff_mean']:+.3f} [{g['diff_ci95'][0]:+.3f}, {g['diff_ci95'][1]:+.3f}] "
             f"MW p={g['mannwhitney_p']:.3f}; s/solve ours {row['seconds_per_solve']['ours_median']:.3f} "
-            f"ref {row['seconds_per_solve']['ref_median']:.2f}")
+            f"ref {row['seconds_per_solve']['ref_median']:.2f}; diag {row['ours_trajectory_diagnostics']}")
 
 
 if __name__ == "__main__":
