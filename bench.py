@@ -61,6 +61,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--eta", type=float, default=0.01, help="StandardSGA step (optimizers.jl:6-23; default 0.01)")
     ap.add_argument("--dump", default="", help="write the final ETO and x0 (npz) here (rank 0)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="take the multi-rank path (process group, per-step all-gather of the shard moments, "
+                         "MAX all-reduce of the clock) even at one rank: exercises the RCCL exchange on a "
+                         "one-GPU box")
     return ap.parse_args()
 
 
@@ -177,11 +181,15 @@ def main():
     local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     backend = os.environ.get("MRBO_DIST_BACKEND", "nccl")
-    if world > 1:
+    sharded = world > 1 or args.sharded
+    if sharded:
+        # a one-rank --sharded run outside torch.distributed.run has no rendezvous in the env
+        init = {} if "MASTER_ADDR" in os.environ else dict(init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                                                           world_size=1)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), **init)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, **init)
     cfg = configs.CONFIGS[args.config]
     M_local, R, d, h = (args.mc_per_gpu or cfg.M), (args.restarts or cfg.R), cfg.d, cfg.h
     M_total = M_local * world
@@ -215,7 +223,7 @@ def main():
     stream = torch.cuda.current_stream(local)
 
     def step(timed):
-        if world > 1:
+        if sharded:
             dx0.copy_(torch.from_numpy(x0.ravel(order="F")), non_blocking=False)
         if timed:   # HIP events on the launch stream around the rollout launch, read after the loop
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -224,14 +232,14 @@ def main():
         if timed:
             ev[1].record(stream)
             events.append(ev)
-        if world == 1:
+        if not sharded:
             e = plan.eto(out)                           # two-pass mean / std(n-1) on the device
         else:
             e = plan.partial_moments(out, hi - lo)     # this shard's (Σ, M2) rows
         evals_acc.add_(out["evals"])        # also in warmup: no first-use op inside the timed region
         if args.longest_first:
             plan.order_longest_first(out)   # the next step's schedule (same work)
-        if world == 1:
+        if not sharded:
             # eswavs + StandardSGA of every active restart on the device (mrbo_sga_step): x0 and the
             # stop flags stay in HBM, so the next launch follows without a host round trip
             plan.sga_step(e, dx0, dactive, M_total, args.eta)
@@ -246,23 +254,23 @@ def main():
         step(False)
     evals_acc.zero_()
     torch.cuda.synchronize()
-    if world > 1:
+    if sharded:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize()
-    if world > 1:
+    if sharded:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    if world > 1:
+    if sharded:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     kernel_ms = [a.elapsed_time(b) for a, b in events]
-    if world == 1:
+    if not sharded:
         last["eto"] = last["eto_dev"].cpu().numpy().reshape((W, R), order="F")
         x0 = from_device(dx0, (d, R))
         active = dactive.cpu().numpy().astype(bool)
@@ -301,7 +309,7 @@ def main():
                    "lengthscale_source": "optimize! MLE in [0.1, 5]" if mle else ("--ell" if args.ell > 0 else
                                                                                  "ℓ = 1 (SURVEY §8d)"),
                    "rule": rule, "parallelism": f"mc-shard x{world}",
-                   "exchange": "none" if world == 1 else f"all-gather of (Σ, M2) moments, {W * R * 8} B/rank/step",
+                   "exchange": "none" if not sharded else f"all-gather of (Σ, M2) moments, {W * R * 8} B/rank/step",
                    "outer_step": f"eswavs + StandardSGA η={args.eta:g}, no clip (utils.jl:114-123, "
                                  f"optimizers.jl:16-22)",
                    "schedule": "longest first (previous step's work counters)" if args.longest_first else "index order"},
@@ -328,7 +336,7 @@ def main():
         print(json.dumps(res), flush=True)
         if args.dump:
             np.savez(args.dump, eto=last["eto"], x0=x0, active=active)
-    if world > 1:
+    if sharded:
         dist.destroy_process_group()
     return 0
 

@@ -588,8 +588,8 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
   HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * 4, st));
 #ifdef MRBO_STAMPS
   static unsigned long long* dstamps = nullptr;
-  if (!dstamps) HIP_TRY(hipMalloc(&dstamps, sizeof(unsigned long long) * 20));
-  HIP_TRY(hipMemsetAsync(dstamps, 0, sizeof(unsigned long long) * 20, st));
+  if (!dstamps) HIP_TRY(hipMalloc(&dstamps, sizeof(unsigned long long) * NSTAMP_SLOTS));
+  HIP_TRY(hipMemsetAsync(dstamps, 0, sizeof(unsigned long long) * NSTAMP_SLOTS, st));
   kp.stamps = dstamps;
 #endif
   HIP_TRY(hipEventRecord(P->ev0, st));
@@ -614,8 +614,9 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
                                               "adjoint pair", "draw+condition", "resolve+adjoint setup",
                                               "Newton accept/convergence", "Newton direction", "Newton trial point",
                                               "batched start values", "multistart loop (certified starts)",
-                                              "Newton Gershgorin retry", "Newton substitutions"};
-    unsigned long long hs[20];
+                                              "Newton Gershgorin retry", "Newton substitutions",
+                                              "Newton Armijo/accept", "Newton certificates", "Newton projected-gradient test"};
+    unsigned long long hs[NSTAMP_SLOTS];
     HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipMemcpy(hs, dstamps, sizeof(hs), hipMemcpyDeviceToHost));
     double tot = 0;
@@ -623,7 +624,7 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
     for (int k = 0; k < NSTAMP; ++k)
       fprintf(stderr, "[mrbo stamps] %-40s %6.2f%%  %.3e ticks/traj\n", stamp_names[k], 100.0 * hs[k] / tot,
               (double)hs[k] / (double)T);
-    fprintf(stderr, "[mrbo stamps] Gershgorin retries per trajectory: %.3f\n", (double)hs[19] / (double)T);
+    fprintf(stderr, "[mrbo stamps] Gershgorin retries per trajectory: %.3f\n", (double)hs[STAMP_RETRY] / (double)T);
   }
 #endif
   if (host) {

@@ -19,7 +19,9 @@ namespace mrbo {
 // work counters per trajectory (for the algorithmic-FLOP roofline):
 // evals[NCOUNT·t + k], k = gradient evals, value evals, Hessians, adjoint rich evals, pairs
 constexpr int NCOUNT = 5;
-constexpr int NSTAMP = 19;  // MRBO_STAMPS regions (names in mrbo_api.hip); slot 19 counts Gershgorin retries
+constexpr int NSTAMP = 22;        // MRBO_STAMPS regions (names in mrbo_api.hip)
+constexpr int STAMP_RETRY = 22;   // slot counting Gershgorin retries
+constexpr int NSTAMP_SLOTS = 24;  // accumulator slots per wave (U_STAMP) and in kp.stamps
 #ifndef MRBO_FMAX
 #define MRBO_FMAX 6
 #endif

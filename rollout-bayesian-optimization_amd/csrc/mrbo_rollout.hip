@@ -90,8 +90,8 @@ struct Lay {
   static constexpr int U_LB = U_NP + D;                  // box lower bounds      D
   static constexpr int U_UB = U_LB + D;                  // box upper bounds      D
   static constexpr int U_HF = U_UB + D;                  // fantasy rows: [x - X_r (D), g1, g2]  FMAX×(D+2)
-  static constexpr int U_STAMP = U_HF + FMAX * (D + 2);   // cycle accumulators (MRBO_STAMPS) 20
-  static constexpr int U_KC = U_STAMP + 20;              // launch constants (KC_*), see wave_setup
+  static constexpr int U_STAMP = U_HF + FMAX * (D + 2);   // cycle accumulators (MRBO_STAMPS)
+  static constexpr int U_KC = U_STAMP + NSTAMP_SLOTS;             // launch constants (KC_*), see wave_setup
   static constexpr int U_SIZE = ((U_KC + 13) + 1) & ~1;
   static constexpr int G12 = 3 * NR;                     // per-lane [g1, g2, Y0] of the base rows
   static constexpr int EC = SQ ? (2 * FMAX + 1) * NR : 0;  // E (FMAX×NR) + C ((FMAX+1)×NR) in LDS
@@ -1086,15 +1086,19 @@ __device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL>& W, const KParams& 
 
 // One projected-Newton direction from the state in U (g = U_NG, H = U_H, the free set of the
 // projected-gradient test that just passed in U_SC + SC_FREE).  Writes p to U_NP.
-// The reduced Hessian A0 (identity on the active set) is formed once: the Gershgorin shift's row
+// The reduced Hessian A0 (identity on the active set) is formed once; the Gershgorin shift's row
 // sums run over it directly (its masked entries are exact zeros, so the sums are those over the
-// free columns) and the retry adds τ to its free diagonal -- the same values as forming both
-// from Hα with the free-set tests.  p leaves through lane 0's LDS stores (no per-lane select).
+// free columns).  The two factorisations of the sequential rule -- A0, and on failure A0 + τ on
+// the free diagonal -- run at once in the two half-waves (lanes 0-31 factor A0, lanes 32-63 the
+// shifted matrix; the shift is formed by every lane from A0 alone), and p comes from lane 0 when
+// A0 factored, else from lane 32: the same values as the sequential retry, in the time of one
+// factorisation (the retry is taken at ~80-90 % of C3's directions).
 template <int D, int RPL>
 __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KParams& kp) {
   using Ly = Lay<D, RPL>;
   constexpr int NH = D * (D + 1) / 2;
   double* U = W.U;
+  const int lane = W.ln();
   const int fm = (int)U[Ly::U_SC + SC_FREE];
   bool fr[D];
   double gs[D];
@@ -1113,34 +1117,38 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
       const double h = U[Ly::U_H + i * D + j];
       A0[i * (i + 1) / 2 + j] = (fr[i] && fr[j]) ? -h : ((i == j) ? 1.0 : 0.0);
     }
+  // Gershgorin shift over the free block
+  double tau = 0.0, hmax = 0.0;
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    double off = 0.0;
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+      if (j != i) off += fabs((j < i) ? A0[i * (i + 1) / 2 + j] : A0[j * (j + 1) / 2 + i]);
+    const double hii = A0[i * (i + 1) / 2 + i];
+    tau = fr[i] ? fmax(tau, off - hii) : tau;
+    hmax = fr[i] ? fmax(hmax, fabs(hii)) : hmax;
+  }
+  tau += 1e-8 * (1.0 + hmax);
+  const bool shifted = lane >= WAVE / 2;
   double A[NH], idg[D];
 #pragma unroll
   for (int t = 0; t < NH; ++t) A[t] = A0[t];
-  bool ok = chol_packed<D>(A, idg);
-  STAMP(W, 13);
-  if (!ok) {  // Gershgorin shift over the free block, one retry
-#ifdef MRBO_STAMPS
-    stamp_count(W, 19, 1);   // Gershgorin retries (taken at ~80 % of C3's Newton directions)
-#endif
-    double tau = 0.0, hmax = 0.0;
 #pragma unroll
-    for (int i = 0; i < D; ++i) {
-      double off = 0.0;
-#pragma unroll
-      for (int j = 0; j < D; ++j)
-        if (j != i) off += fabs((j < i) ? A0[i * (i + 1) / 2 + j] : A0[j * (j + 1) / 2 + i]);
-      const double hii = A0[i * (i + 1) / 2 + i];
-      tau = fr[i] ? fmax(tau, off - hii) : tau;
-      hmax = fr[i] ? fmax(hmax, fabs(hii)) : hmax;
-    }
-    tau += 1e-8 * (1.0 + hmax);
-#pragma unroll
-    for (int t = 0; t < NH; ++t) A[t] = A0[t];
-#pragma unroll
-    for (int i = 0; i < D; ++i) A[i * (i + 1) / 2 + i] = fr[i] ? A0[i * (i + 1) / 2 + i] + tau : 1.0;
-    ok = chol_packed<D>(A, idg);
+  for (int i = 0; i < D; ++i) {
+    const int ii = i * (i + 1) / 2 + i;
+    A[ii] = shifted ? (fr[i] ? A0[ii] + tau : 1.0) : A0[ii];
+    idg[i] = 0.0;
   }
+  const bool okl = chol_packed<D>(A, idg);
+  const bool ok0 = __builtin_amdgcn_readlane((int)okl, 0) != 0;
+  const bool ok1 = __builtin_amdgcn_readlane((int)okl, WAVE / 2) != 0;
+  STAMP(W, 13);
+#ifdef MRBO_STAMPS
+  if (!ok0) stamp_count(W, STAMP_RETRY, 1);   // Gershgorin retries (taken at ~80 % of C3's Newton directions)
+#endif
   STAMP(W, 17);
+  const bool ok = ok0 || ok1;
   double p[D];
   if (ok) {
     double t1[D];
@@ -1170,7 +1178,7 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
   const double box = KCV(BOX);
   const double sc = (pn > box) ? box / pn : 1.0;
   wave_sync();
-  if (W.ln() == 0) {
+  if (lane == (ok0 ? 0 : WAVE / 2)) {
 #pragma unroll
     for (int a = 0; a < D; ++a) U[Ly::U_NP + a] = (pn > box) ? p[a] * sc : p[a];
   }
@@ -1354,7 +1362,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
       if (lane < D) U[Ly::U_NG + lane] = -U[Ly::U_GAL + lane];
       wave_sync();
       if (!newton_pg_ok<D, RPL>(W, kp)) break;     // stationary
-      STAMP(W, 12);
+      STAMP(W, 21);
       phase = P_HESS;
       mode = EV_BACK;
       continue;
@@ -1388,6 +1396,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
     } else {
       f = fe;
     }
+    STAMP(W, 19);
     // decision point at x = U_NX (= U_X), whose VALUE evaluation is in U
     if (it >= kp.max_iters) break;
     if (f != f) break;
@@ -1396,7 +1405,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
         tight_certified<D, RPL, true>(W, kp, S, U[Ly::U_SC + SC_GMU], U[Ly::U_SC + SC_GSIG], U[Ly::U_SC + SC_SIG],
                                       U[Ly::U_SC + SC_ISIG], kp.cost ? U[Ly::U_SC + SC_ARAW] : 0.0))
       break;
-    STAMP(W, 12);
+    STAMP(W, 20);
     phase = P_GRAD;
     mode = EV_GRADC;
   }
@@ -2308,7 +2317,7 @@ __global__ void __launch_bounds__((KBounds<D, RPL>::threads), (KBounds<D, RPL>::
   }
 #ifdef MRBO_STAMPS
   if (kp.stamps && W.lane == 0)
-    for (int k = 0; k < 20; ++k)
+    for (int k = 0; k < NSTAMP_SLOTS; ++k)
       atomicAdd(kp.stamps + k, reinterpret_cast<unsigned long long*>(W.U + Lay<D, RPL>::U_STAMP)[k]);
 #endif
 }

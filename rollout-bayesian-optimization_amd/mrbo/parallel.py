@@ -87,10 +87,12 @@ def eto_from_moments(moments, M, d):
 
 def allgather_moments(moments_tensor, group=None):
     """ONE all-gather of every rank's flat (W·R) moments tensor; returns a list, rank order.
-    gloo cannot gather device tensors: they travel through host memory on that backend."""
+    gloo cannot gather device tensors: they travel through host memory on that backend.  Without a
+    process group the tensor is returned as is; with one the collective runs at any world size
+    (bench.py --sharded exercises RCCL at one rank)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1):
+    if not (dist.is_available() and dist.is_initialized()):
         return [moments_tensor]
     src = moments_tensor
     if src.is_cuda and dist.get_backend(group) == "gloo":

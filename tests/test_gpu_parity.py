@@ -136,6 +136,24 @@ def _bench(args, env):
     return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
 
 
+def test_bench_sharded_rccl_one_rank_matches_plain(gpu, tmp_path):
+    """`bench.py --sharded` at one rank runs the multi-rank path over RCCL (backend nccl: a
+    process group, the per-step all-gather of the shard moments on device tensors, the host Chan
+    merge and SGA step, the MAX all-reduce of the clock) -- the exchange the 8-GPU run uses, on
+    the one-GPU box.  Its ETO, x0 and stop flags equal the plain run's (device ETO + device SGA)."""
+    common = ["--steps", "2", "--warmup", "1", "--restarts", "4", "--no-cpu-baseline", "--config", "C2",
+              "--mc-per-gpu", "64", "--eta", "0.5"]
+    env = {k: v for k, v in os.environ.items() if k != "MRBO_DIST_BACKEND"}
+    sh = _bench(common + ["--sharded", "--dump", str(tmp_path / "sh.npz")], env)
+    one = _bench(common + ["--dump", str(tmp_path / "one.npz")], env)
+    assert sh["n_gpus"] == one["n_gpus"] == 1
+    assert sh["config"]["exchange"].startswith("all-gather") and one["config"]["exchange"] == "none"
+    a, b = np.load(tmp_path / "sh.npz"), np.load(tmp_path / "one.npz")
+    np.testing.assert_allclose(a["eto"], b["eto"], rtol=1e-12, atol=1e-16)
+    np.testing.assert_array_equal(a["active"], b["active"])
+    np.testing.assert_allclose(a["x0"], b["x0"], rtol=1e-14)
+
+
 def test_bench_two_ranks_rehearsal_matches_one_rank(gpu, tmp_path):
     """`bench.py --gpus 2` starts its two ranks itself (torch.distributed.run) and exchanges the
     per-restart moments once per step; rehearsed on one GPU over gloo (MRBO_DIST_BACKEND=gloo, both

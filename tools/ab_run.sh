@@ -13,5 +13,5 @@ lines = [l for l in open(f"gpurun_out/ab_{v}.json") if l.startswith("{")]
 d = json.loads(lines[-1])
 print(f"{v:12s} {d['value']:12.0f} traj/s  kernel {d['roofline']['kernel_ms']:.2f} ms  frac {d['roofline']['frac']:.4f}")
 PY
-  grep "mrbo stamps" gpurun_out/ab_$v$AB_TAG.err | head -20
+  grep "mrbo stamps" gpurun_out/ab_$v$AB_TAG.err | head -30
 done

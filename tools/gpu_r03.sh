@@ -47,7 +47,7 @@ for step in "$@"; do
       rc=$? ;;
     ab)
       AB_TAG="" timeout -k 10 400 bash tools/ab_run.sh ${AB_VARIANTS:-old new oldst newst} > "$out/ab.log" 2>&1
-      rc=$?; cp gpurun_out/ab_*.json gpurun_out/ab_*.err "$out/" 2>/dev/null; grep -v "^\[mrbo stamps\] .*0.00%" "$out/ab.log" | tail -60 ;;
+      rc=$?; cp gpurun_out/ab_*.json gpurun_out/ab_*.err "$out/" 2>/dev/null; grep -v "^\[mrbo stamps\] .* 0.00%" "$out/ab.log" | tail -60 ;;
     gpfit)
       timeout -k 10 400 python -u tools/bench_rows.py --rows gp_fit --cpu-seconds 2 > "$out/gpfit_rows.jsonl" 2> "$out/gpfit_rows.err"
       rc=$?; python -c "
