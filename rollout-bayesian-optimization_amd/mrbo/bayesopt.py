@@ -116,7 +116,7 @@ def incumbent_start(sur, lbs, ubs):
     return np.clip(xb + step, lbs, ubs)
 
 
-def rollout_solve(sur, lbs, ubs, horizon, mc_samples, batch_size, starts, sgd_iterations, theta, eta=0.5,
+def rollout_solve(sur, lbs, ubs, horizon, mc_samples, batch_size, starts, sgd_iterations, theta, eta=0.01,
                   device=0, solver="sga", incumbent=True, trace=None):
     """xnext from the rollout acquisition: restarts from a Sobol batch (StandardSGA with step `eta`,
     or BoxAdam with `eta` box widths per step), best final ETO mean.
@@ -157,10 +157,11 @@ def rollout_solve(sur, lbs, ubs, horizon, mc_samples, batch_size, starts, sgd_it
 
 # ---- the experiment loop (nonmyopic_bayesopt.jl:120-300) -------------------------------------
 def run(function_name, output_dir, budget=15, trials=60, starts=16, horizon=0, mc_samples=200, batch_size=8,
-        sgd_iterations=50, optimize=False, seed=1906, device=0, log=print, rules=("ei", "poi", "lcb"), eta=0.5,
+        sgd_iterations=50, optimize=False, seed=1906, device=0, log=print, rules=("ei", "poi", "lcb"), eta=0.01,
         initial_observations=INITIAL_OBSERVATIONS, solver="sga", fmini_over_capacity=True, incumbent=True):
     """The experiment loop; `rules` selects a subset of the reference's three acquisitions (all by
-    default, as nonmyopic_bayesopt.jl), `eta` the StandardSGA step of the build-defined solver,
+    default, as nonmyopic_bayesopt.jl), `eta` the StandardSGA step of the build-defined solver
+    (default 0.01, StandardSGA's own default, optimizers.jl:9),
     `initial_observations` the initial design size (5 in the current script, :131), `solver` "sga"
     (StandardSGA, η = eta) or "adam" (BoxAdam, eta box widths per step); fmini_over_capacity=False
     turns the reference's Q3 off (fmini over the observed points, not the zero-padded buffer),

@@ -121,7 +121,7 @@ def trajectory_diagnostics(Xs, lbs, ubs, initial):
             "trials_with_repeats": float(np.mean(rep))}
 
 
-def run_case(key, case, trials, seed, log, solver="sga", eta=0.5, q3=True, incumbent=True):
+def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incumbent=True):
     from mrbo import bayesopt
     s = SETTINGS[key]
     testfn = bayesopt.TESTFNS[s["fn"]]()
@@ -170,7 +170,8 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--solver", default="sga", choices=["sga", "adam"],
                     help="outer solver of the build-defined rollout acquisition (mrbo/bayesopt.py)")
-    ap.add_argument("--eta", type=float, default=0.0, help="step (default 0.5 for sga, 0.02 box widths for adam)")
+    ap.add_argument("--eta", type=float, default=0.0, help="step (default 0.01 for sga -- StandardSGA's default, optimizers.jl:9 -- and 0.02 box widths "
+                         "for adam)")
     ap.add_argument("--no-q3", action="store_true",
                     help="diagnostic: fmini over the observed points instead of the zero-padded buffer (Q3 off)")
     ap.add_argument("--no-incumbent", action="store_true",
@@ -179,7 +180,7 @@ def main():
     ref = load_reference()
     log = lambda m: print(m, file=sys.stderr, flush=True)
     for key in (ASSERTED if a.cases == "asserted" else a.cases.split(",")):
-        eta = a.eta or (0.5 if a.solver == "sga" else 0.02)
+        eta = a.eta or (0.01 if a.solver == "sga" else 0.02)
         row = run_case(key, ref[key], a.trials, a.seed, log, solver=a.solver, eta=eta, q3=not a.no_q3, incumbent=not a.no_incumbent)
         line = json.dumps(row)
         print(line, flush=True)

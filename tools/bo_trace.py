@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--trial", type=int, default=0)
     ap.add_argument("--initial", type=int, default=1)
     ap.add_argument("--solver", default="sga")
-    ap.add_argument("--eta", type=float, default=0.5)
+    ap.add_argument("--eta", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=1906)
     ap.add_argument("--no-incumbent", action="store_true")
     ap.add_argument("--no-q3", action="store_true", help="fmini over the observed points (Q3 off)")
