@@ -1,7 +1,7 @@
 """The non-myopic BO loop (mrbo/bayesopt.py): CSV formats of utils.jl:155-172
 on the CPU, and a small end-to-end experiment on the GPU.  Parity of BO trajectories with the
-reference is unpinned (its rollout solver is undefined and Julia is absent); the GPU test checks
-the loop's invariants instead."""
+reference is unpinned (its rollout solver is undefined and Julia is absent); the GPU tests check
+the loops' invariants and compare their gap distributions with the reference's recorded runs."""
 import csv
 import os
 
@@ -92,6 +92,31 @@ def test_box_adam_steps_in_box_widths():
     for _ in range(100):
         opt.update(x, np.array([1e4, -1e-3]))
     assert np.all(x >= lbs) and np.all(x <= ubs) and x[0] == 10.0 and x[1] == 0.0
+
+
+def test_incumbent_start_and_trajectory_diagnostics():
+    """rollout_solve's incumbent restart: the best observation moved 1 % of a box width towards the
+    centre per coordinate, clamped to the box; and tools/bo_compare.py's trajectory diagnostics
+    (boundary hits, first step on the boundary, repeated observations) on a hand-made sequence."""
+    import sys
+    from conftest import ROOT
+    from mrbo.bayesopt import INCUMBENT_NUDGE, incumbent_start
+
+    class Sur:
+        def get_active_covariates(self):
+            return np.array([[0.0, 9.0, 4.0], [15.0, 1.0, 7.5]])
+
+        def get_active_observations(self):
+            return np.array([3.0, 1.0, 2.0])
+
+    lbs, ubs = np.array([-5.0, 0.0]), np.array([10.0, 15.0])
+    x = incumbent_start(Sur(), lbs, ubs)
+    np.testing.assert_allclose(x, [9.0 - INCUMBENT_NUDGE * 15.0, 1.0 + INCUMBENT_NUDGE * 15.0])
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bo_compare as B
+    X = np.array([[0.0, -5.0, 3.0, 3.0], [1.0, 7.0, 2.0, 2.0]])      # initial point, then 3 BO steps
+    dg = B.trajectory_diagnostics([X], lbs, ubs, 1)
+    assert dg == {"obs_at_boundary": 1 / 3, "first_step_at_boundary": 1.0, "trials_with_repeats": 1.0}
 
 
 @pytest.mark.gpu
