@@ -73,6 +73,9 @@ struct mrbo_plan {
   size_t esmem = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
+  // MRBO_FLAG_HOST_POINTERS staging: device buffers kept across calls, one slot per staged
+  // argument in call order, grown on demand and freed with the plan
+  std::vector<std::pair<void*, size_t>> stage;
 };
 
 namespace {
@@ -278,26 +281,40 @@ static void fill_common(const mrbo_plan_t* P, KParams& kp) {
   kp.cost_tab = P->dcost;
 }
 
-// staging helper for MRBO_FLAG_HOST_POINTERS
+// staging helper for MRBO_FLAG_HOST_POINTERS: the plan's persistent device buffers (slot k =
+// the k-th staged argument of the call), so a host-pointer call allocates nothing once warm;
+// without a plan (mrbo_gp_fit) the buffers live for the call
 struct Stage {
-  std::vector<void*> bufs;
-  ~Stage() { for (void* b : bufs) (void)hipFree(b); }
+  mrbo_plan_t* P;
+  std::vector<std::pair<void*, size_t>> own;
+  size_t k = 0;
+  explicit Stage(mrbo_plan_t* plan = nullptr) : P(plan) {}
+  ~Stage() { for (auto& b : own) if (b.first) (void)hipFree(b.first); }
+  void* slot(size_t bytes) {
+    auto& pool = P ? P->stage : own;
+    if (pool.size() <= k) pool.resize(k + 1, {nullptr, 0});
+    auto& b = pool[k++];
+    if (b.second < bytes) {
+      if (b.first) (void)hipFree(b.first);
+      b = {nullptr, 0};
+      if (hipMalloc(&b.first, bytes) != hipSuccess) { b.first = nullptr; return nullptr; }
+      b.second = bytes;
+    }
+    return b.first;
+  }
   template <class T>
   int in(const T* h, size_t n, const T** dptr) {
     if (!h) { *dptr = nullptr; return 0; }
-    void* d = nullptr;
-    if (hipMalloc(&d, sizeof(T) * n) != hipSuccess) return -1;
-    bufs.push_back(d);
-    if (hipMemcpy(d, h, sizeof(T) * n, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    void* d = slot(sizeof(T) * n);
+    if (!d || hipMemcpy(d, h, sizeof(T) * n, hipMemcpyHostToDevice) != hipSuccess) return -1;
     *dptr = (const T*)d;
     return 0;
   }
   template <class T>
   int out(size_t n, T* h, T** dptr) {
     if (!h) { *dptr = nullptr; return 0; }
-    void* d = nullptr;
-    if (hipMalloc(&d, sizeof(T) * n) != hipSuccess) return -1;
-    bufs.push_back(d);
+    void* d = slot(sizeof(T) * n);
+    if (!d) return -1;
     *dptr = (T*)d;
     return 0;
   }
@@ -309,7 +326,7 @@ static int reduce_common(mrbo_plan_t* P, const double* values, const double* gra
   hipStream_t st = (hipStream_t)stream;
   const int d = P->d, R = P->p.R, Ms = P->p.M;
   const size_t T = (size_t)Ms * R, W = 2 + 2 * d + 2;
-  Stage sg;
+  Stage sg(P);
   const double *dv = values, *dg = grad_x, *dt = grad_theta;
   double* dout = out;
   if (flags & MRBO_FLAG_HOST_POINTERS) {
@@ -538,6 +555,8 @@ int mrbo_plan_destroy(mrbo_plan_t* P) {
   for (void* b : {(void*)P->dX0, (void*)P->dc0, (void*)P->dLinv, (void*)P->dlbs, (void*)P->dubs, (void*)P->dwork, (void*)P->dytab,
                   (void*)P->dkxb, (void*)P->dgtab, (void*)P->dqueue, (void*)P->dcost})
     if (b) (void)hipFree(b);
+  for (auto& b : P->stage)
+    if (b.first) (void)hipFree(b.first);
   if (P->ev0) (void)hipEventDestroy(P->ev0);
   if (P->ev1) (void)hipEventDestroy(P->ev1);
   delete P;
@@ -563,7 +582,7 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
   fill_common(P, kp);
   kp.with_gradient = with_grad ? 1 : 0;
   kp.T = (long long)T;
-  Stage sg;
+  Stage sg(P);
   const bool host = flags & MRBO_FLAG_HOST_POINTERS;
   double *dvalues = values, *dgx = grad_x, *dgt = grad_theta, *dpol = policy_x, *dobs = obs;
   int32_t* dstatus = status;
@@ -694,7 +713,7 @@ int mrbo_eval_base(mrbo_plan_t* P, int32_t npts, const double* xs, double* out, 
   KParams kp;
   fill_common(P, kp);
   kp.T = npts;
-  Stage sg;
+  Stage sg(P);
   const double* dxs = xs;
   double* dout = out;
   if (flags & MRBO_FLAG_HOST_POINTERS) {
@@ -731,7 +750,7 @@ int mrbo_base_solve(mrbo_plan_t* P, int32_t n, const double* xstarts, double* xm
   kp.with_gradient = 0;
   kp.xs_lds = 0;
   kp.batch = 0;
-  Stage sg;
+  Stage sg(P);
   const double* dxs = xstarts;
   double *dx = xmin, *df = fmin;
   int32_t* dst = status;
@@ -786,9 +805,8 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
   if (sg.in(s->X, (size_t)d * N, &dX) || sg.in(s->y, (size_t)N, &dy)) return fail(MRBO_ERR_NOMEM, "staging X, y");
   GpFitParams q{d, N, s->kernel, s->sigma_n2, dX, dy, nt, dth, s->period, dll_, dgr, (int*)dst, dL, dc, nullptr};
   if (!gpfit_in_regs(q) && !gpfit_in_lds(q)) {   // the register (N ≤ 64) and LDS (N ≤ 128) kernels need none
-    if (hipMalloc(&q.work, sizeof(double) * gpfit_tile_work_doubles(N) * P) != hipSuccess)
-      return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
-    sg.bufs.push_back(q.work);
+    q.work = (double*)sg.slot(sizeof(double) * gpfit_tile_work_doubles(N) * P);
+    if (!q.work) return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
   }
   static hipEvent_t gev[2] = {nullptr, nullptr};
   if (!gev[0]) {
