@@ -10,6 +10,8 @@ generate the synthetic base data of every BASELINE configuration (Gramacy–Lee 
 Hartmann-6 C3/C4, Ackley-8 C5) -- and the BO comparison's functions.
 
 For each function: up to PAIRS distinct pairs, taken evenly over the file's trials and steps.
+Also writes tests/golden/bo_ref_observations.json: for the archived rollout runs the BO comparison
+uses, the first trials' objective values in observation order beside their recorded gap rows.
 Run here, where /root/reference exists; the JSON travels with the repo.
 usage: python tests/golden/make_testfn_ref.py [--reference /root/reference]
 """
@@ -46,6 +48,30 @@ def read_pairs(path, d):
     return pairs
 
 
+ROLLOUT_FNS = ["braninhoo", "gramacylee", "ackley1d", "ackley2d", "ackley3d", "ackley4d", "rosenbrock", "hartmann3d",
+               "sixhump", "goldsteinprice"]
+OBS_TRIALS = 10
+
+
+def read_rows(path):
+    rows = [[float(v) for v in r] for r in list(csv.reader(open(path)))[1:]]
+    return [r for r in rows if not all(v == -1.0 for v in r)]
+
+
+def bo_observations(ref, fn, h, d):
+    """The first OBS_TRIALS trials of an archived rollout run: the objective values in observation
+    order (the initial point, then the 20 BO steps) and the trial's recorded gap row (labels 0..20)."""
+    obs = read_rows(os.path.join(ref, f"{SHORT}/{fn}/rollout_h{h}_observations.csv"))
+    gaps = read_rows(os.path.join(ref, f"{SHORT}/{fn}/rollout_h{h}_gaps.csv"))
+    out = []
+    for t in range(OBS_TRIALS):
+        y = obs[t * (d + 1) + d]
+        g = gaps[t]
+        assert y[0] == g[0]                    # rows led by the same trial id (failed trials are absent)
+        out.append({"trial": int(y[0]), "y": y[1:], "gaps": g[1:]})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
@@ -68,6 +94,14 @@ def main():
     with open(path, "w") as f:
         json.dump(out, f, indent=0)
     print(path, {k: len(v["pairs"]) for k, v in out.items()})
+    # the archived runs' observation values beside their recorded gaps (utils.jl `gap`)
+    bo = {f"rollout_h{h}_{fn}": {"source": f"{SHORT}/{fn}/rollout_h{h}_{{observations,gaps}}.csv",
+                                 "trials": bo_observations(a.reference, fn, h, SOURCES[fn][1])}
+          for fn in ROLLOUT_FNS for h in (0, 1)}
+    path = os.path.join(HERE, "bo_ref_observations.json")
+    with open(path, "w") as f:
+        json.dump(bo, f, indent=0)
+    print(path, len(bo))
 
 
 if __name__ == "__main__":

@@ -80,6 +80,39 @@ def test_reference_bo_fixture_and_comparison_helpers():
     assert abs(c["ours_mean"] - 0.2) < 1e-15 and c["n_ref"] == 4 and 0.0 < c["mannwhitney_p"] <= 1.0
 
 
+def test_gap_and_label_convention_reproduce_archived_runs():
+    """The reference's archived rollout runs recorded each trial's objective values in observation
+    order and its gap row (tests/golden/bo_ref_observations.json, make_testfn_ref.py).  From the
+    values alone, the build's `gap` (utils.jl) with the build's f* = f(xopt) and tools/bo_compare.py's
+    label convention (label k = after k BO observations; run()'s gaps recorded before conditioning,
+    the last label from the final minimum observation) reproduce every recorded row bit for bit --
+    200 trials over 10 functions and h = 0, 1 -- and those rows are the first rows of the
+    comparison's fixture."""
+    import json
+    import sys
+    from conftest import ROOT
+    from mrbo import bayesopt
+    from mrbo.utils import gap
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bo_compare as B
+    with open(os.path.join(ROOT, "tests", "golden", "bo_ref_observations.json")) as f:
+        obs = json.load(f)
+    ref = B.load_reference()
+    assert len(obs) == 20
+    for key, case in obs.items():
+        tf = bayesopt.TESTFNS[key.split("_", 2)[2]]()
+        fstar = float(tf.f(np.asarray(tf.xopt[0], dtype=np.float64)))
+        budget = B.SETTINGS[key]["budget"]
+        for i, t in enumerate(case["trials"]):
+            y = np.array(t["y"])
+            assert y.size == budget + 1 and len(t["gaps"]) == budget + 1
+            res = [dict(gaps=np.array([gap(y[0], float(y[:b + 1].min()), fstar) for b in range(budget)]),
+                        minimum_observations=np.minimum.accumulate(y)[1:], initial_best=float(y[0]))]
+            row = B.our_gap_columns(res, fstar, budget)[0]
+            np.testing.assert_array_equal(row, t["gaps"])
+            np.testing.assert_array_equal(ref[key]["gaps"][i], t["gaps"])
+
+
 def test_box_adam_steps_in_box_widths():
     """BoxAdam: the first Adam step moves every coordinate by η box widths (sign of the gradient),
     whatever the gradient's scale, and the iterate stays in the box."""
