@@ -8,7 +8,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/mrbo.h"
@@ -281,17 +283,59 @@ static void fill_common(const mrbo_plan_t* P, KParams& kp) {
   kp.cost_tab = P->dcost;
 }
 
+// Device buffers of plan-less calls (mrbo_gp_fit: staging and the tile kernel's workspace) are
+// pooled per device across calls -- a hipMalloc + hipFree pair costs ≈ 0.1 ms, the whole N = 128
+// fit 0.4 ms.  A call takes the smallest free buffer that fits (or allocates one) and gives it back
+// when it returns, after its stream has synchronised; concurrent calls never share a buffer.
+struct DevPool {
+  std::mutex m;
+  std::vector<std::tuple<int, void*, size_t>> free;   // (device, pointer, bytes)
+};
+static DevPool g_pool;
+
+static std::pair<void*, size_t> pool_take(size_t bytes) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  {
+    std::lock_guard<std::mutex> lk(g_pool.m);
+    size_t best = g_pool.free.size();
+    for (size_t i = 0; i < g_pool.free.size(); ++i) {
+      const auto& [d, p, n] = g_pool.free[i];
+      if (d == dev && n >= bytes && (best == g_pool.free.size() || n < std::get<2>(g_pool.free[best]))) best = i;
+    }
+    if (best < g_pool.free.size()) {
+      auto r = std::make_pair(std::get<1>(g_pool.free[best]), std::get<2>(g_pool.free[best]));
+      g_pool.free.erase(g_pool.free.begin() + best);
+      return r;
+    }
+  }
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) return {nullptr, 0};
+  return {p, bytes};
+}
+
+static void pool_give(void* p, size_t bytes) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_pool.m);
+  g_pool.free.emplace_back(dev, p, bytes);
+}
+
 // staging helper for MRBO_FLAG_HOST_POINTERS: the plan's persistent device buffers (slot k =
 // the k-th staged argument of the call), so a host-pointer call allocates nothing once warm;
-// without a plan (mrbo_gp_fit) the buffers live for the call
+// without a plan (mrbo_gp_fit) the buffers come from the device pool and return to it
 struct Stage {
   mrbo_plan_t* P;
   std::vector<std::pair<void*, size_t>> own;
   size_t k = 0;
   explicit Stage(mrbo_plan_t* plan = nullptr) : P(plan) {}
-  ~Stage() { for (auto& b : own) if (b.first) (void)hipFree(b.first); }
+  ~Stage() { for (auto& b : own) if (b.first) pool_give(b.first, b.second); }
   void* slot(size_t bytes) {
-    auto& pool = P ? P->stage : own;
+    if (!P) {
+      own.push_back(pool_take(bytes));
+      return own.back().first;
+    }
+    auto& pool = P->stage;
     if (pool.size() <= k) pool.resize(k + 1, {nullptr, 0});
     auto& b = pool[k++];
     if (b.second < bytes) {
@@ -804,7 +848,7 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
   const double *dX = nullptr, *dy = nullptr;
   if (sg.in(s->X, (size_t)d * N, &dX) || sg.in(s->y, (size_t)N, &dy)) return fail(MRBO_ERR_NOMEM, "staging X, y");
   GpFitParams q{d, N, s->kernel, s->sigma_n2, dX, dy, nt, dth, s->period, dll_, dgr, (int*)dst, dL, dc, nullptr};
-  if (!gpfit_in_regs(q) && !gpfit_in_lds(q)) {   // the register (N ≤ 64) and LDS (N ≤ 128) kernels need none
+  if (!gpfit_in_regs(q) && !gpfit_in_lds(q)) {   // the register (N ≤ 64) and LDS (N ≤ 80) kernels need none
     q.work = (double*)sg.slot(sizeof(double) * gpfit_tile_work_doubles(N) * P);
     if (!q.work) return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
   }
@@ -817,7 +861,7 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
   launch_gpfit(np, st, q);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(gev[1], st));
-  // the staging buffers and the workspace are freed on return: finish the launch first
+  // the staging buffers and the workspace go back to the pool on return: finish the launch first
   HIP_TRY(hipStreamSynchronize(st));
   {
     float ms = -1.f;

@@ -71,7 +71,7 @@ struct GpFitParams {
   double* c_out;         // optional N×P
   double* work;          // gpfit_tile_work_doubles(N)·P (the tile kernel only)
 };
-// 128 < N ≤ 512 (or factor outputs at N > 128): gpfit_tile_kernel's workspace per candidate
+// MRBO_GPFIT_LDS_MAX < N ≤ 512: gpfit_tile_kernel's workspace per candidate
 size_t gpfit_tile_work_doubles(int N);
 void launch_gpfit(int P, hipStream_t st, const GpFitParams& q);
 // N ≤ 64, d ≤ 16 and no factor / coefficient outputs: the one-wave-per-candidate register kernel
@@ -79,9 +79,15 @@ void launch_gpfit(int P, hipStream_t st, const GpFitParams& q);
 inline bool gpfit_in_regs(const GpFitParams& q) {
   return q.N <= 64 && q.d <= 16 && !q.L_out && !q.c_out;
 }
-// 64 < N ≤ 128 (and N ≤ 64 with factor outputs): gpfit_lds_kernel, no global workspace
+// 64 < N ≤ 80 (and N ≤ 64 with factor outputs): gpfit_lds_kernel, no global workspace.  The
+// ceiling is measured: the tile kernel pads N to a multiple of 32 and overtakes
+// the LDS kernel above N ≈ 80 (N = 96: 0.28 vs 0.36 ms, N = 128: 0.40 vs 0.60 ms per 256
+// candidates; N = 72: 0.27 vs 0.22 ms)
+#ifndef MRBO_GPFIT_LDS_MAX
+#define MRBO_GPFIT_LDS_MAX 80
+#endif
 inline bool gpfit_in_lds(const GpFitParams& q) {
-  return q.N <= 128 && q.d <= 16 && !gpfit_in_regs(q);
+  return q.N <= MRBO_GPFIT_LDS_MAX && q.d <= 16 && !gpfit_in_regs(q);
 }
 
 }  // namespace mrbo

@@ -17,7 +17,8 @@
 // readlane broadcasts; V = L⁻¹ by columns (lane j = column j) and K⁻¹ = VᵀV with the same DPP
 // broadcasts; tr(K⁻¹δK) and cᵀδKc from K⁻¹.  K and δK are evaluated once per pair j ≤ i.  The
 // reference's operations (chol, then triangular solves); summation orders differ (tolerance).
-// 64 < N ≤ 128, or N ≤ 64 with L / c requested: gpfit_lds_kernel (below; everything in LDS).
+// 64 < N ≤ MRBO_GPFIT_LDS_MAX (80), or N ≤ 64 with L / c requested: gpfit_lds_kernel (below;
+// everything in LDS; it holds candidates up to N = 128, but the tile kernel is faster above 80).
 // 128 < N ≤ 512: gpfit_tile_kernel (below): one workgroup per candidate, the blocked algorithm on
 // 32 × 32 tiles in a global workspace with the tile products on the fp64 matrix cores.
 #include <hip/hip_runtime.h>
@@ -361,7 +362,7 @@ __global__ void __launch_bounds__(64 * GR_WAVES) gpfit_reg_kernel(GpFitParams q,
 #endif
 }
 
-// ---- 64 < N ≤ 128: one workgroup per candidate, the factor and its inverse in LDS ----------
+// ---- 64 < N ≤ 128 (dispatched up to 80): one workgroup per candidate, factor and inverse in LDS
 // S (128 × 129 doubles, column-major r + LD·c, odd LD: row and column walks conflict free) holds
 // K → L in its lower triangle and V = L⁻¹ transposed in its strict upper triangle (V[i][j], i > j,
 // at j + LD·i); L's diagonal in ld_, V's (1/L_ii) in dv.  Four waves:

@@ -157,12 +157,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", default="ghq,gp_fit")
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
+    ap.add_argument("--gpfit-n", default="64,128,256,384,512", help="gp_fit rows: comma list of N")
     args = ap.parse_args()
     rows = args.rows.split(",")
     if "ghq" in rows:
         print(json.dumps(row_ghq(args)), flush=True)
     if "gp_fit" in rows:
-        for N in (64, 128, 256, 384, 512):
+        for N in (int(n) for n in args.gpfit_n.split(",")):
             print(json.dumps(row_gp_fit(args, N)), flush=True)
 
 
