@@ -308,6 +308,13 @@ static std::pair<void*, size_t> pool_take(size_t bytes) {
       g_pool.free.erase(g_pool.free.begin() + best);
       return r;
     }
+    // nothing fits: the free buffers of this device are smaller than what calls now ask for (a
+    // BO loop's N grows by one per step), so release them instead of letting the pool grow
+    for (size_t i = g_pool.free.size(); i-- > 0;)
+      if (std::get<0>(g_pool.free[i]) == dev) {
+        (void)hipFree(std::get<1>(g_pool.free[i]));
+        g_pool.free.erase(g_pool.free.begin() + i);
+      }
   }
   void* p = nullptr;
   if (hipMalloc(&p, bytes) != hipSuccess) return {nullptr, 0};
