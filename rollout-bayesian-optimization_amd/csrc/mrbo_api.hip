@@ -859,10 +859,25 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
     q.work = (double*)sg.slot(sizeof(double) * gpfit_tile_work_doubles(N) * P);
     if (!q.work) return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
   }
-  static hipEvent_t gev[2] = {nullptr, nullptr};
-  if (!gev[0]) {
-    HIP_TRY(hipEventCreate(&gev[0]));
-    HIP_TRY(hipEventCreate(&gev[1]));
+  // timing events per device (an event records only on streams of the device it was created on)
+  static std::mutex gev_m;
+  static std::vector<std::pair<hipEvent_t, hipEvent_t>> gevs;
+  hipEvent_t gev[2];
+  {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(gev_m);
+    if ((int)gevs.size() <= dev) gevs.resize(dev + 1, {nullptr, nullptr});
+    if (!gevs[dev].first) {
+      hipEvent_t a = nullptr, b = nullptr;
+      if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+        if (a) (void)hipEventDestroy(a);
+        return fail(MRBO_ERR_HIP, "gp_fit: hipEventCreate");
+      }
+      gevs[dev] = {a, b};
+    }
+    gev[0] = gevs[dev].first;
+    gev[1] = gevs[dev].second;
   }
   HIP_TRY(hipEventRecord(gev[0], st));
   launch_gpfit(np, st, q);
