@@ -35,6 +35,15 @@ def test_full_size_c3_vs_oracle(gpu, oracle):
     _end_to_end(oracle, "C3 full (1024 x 64, l=1)", g, 1024)
 
 
+@pytest.mark.parametrize("name,M,R,kind", [("C1", 32, 4, "forward"), ("C2", 256, 16, "full")])
+def test_full_size_c1_c2_vs_oracle(gpu, oracle, name, M, R, kind):
+    """BASELINE's configurations 0 and 1 at their full launch sizes, exhaustively: C1 (32 MC × 4
+    restarts; d = 1, where every inner maximum meets the reference's det(H) < 1e-4 test, Q4, so its
+    adjoint zeroes the x-duals and the case is forward-only) and C2 (256 × 16, the whole launch)."""
+    g = _problem_arrays(name, M, R)
+    _end_to_end(oracle, f"{name} full ({M} x {R}, l=1, {kind})", g, M, kind=kind)
+
+
 def _mle_arrays(name, M, R):
     """base data of `name` with the lengthscale fitted by optimize! (radial_basis_surrogates.jl:805-829,
     bounds [0.1, 5] as nonmyopic_bayesopt.jl:230) on the device"""
