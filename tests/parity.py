@@ -51,16 +51,23 @@ def _plan(g, M=None, R=None, h=None, nstarts=None, kernel=0, theta=0.0, **opts):
                        **opts)
 
 
-def _run(plan, g, dual=None, replay=None, want_policy=True, with_gradient=True, rn=None, x0s=None):
+def _run(plan, g, dual=None, replay=None, want_policy=True, with_gradient=True, rn=None, x0s=None, ghq=None):
+    """One launch through libmrbo.so: Monte-Carlo draws from g's rnstream (or `rn`), or the
+    Gauss–Hermite estimator when ghq = (nodes, weights) (mrbo_simulate_ghq)."""
     import torch
     from mrbo.engine import from_device, to_device
     dev = "cuda:0"
     out = plan.alloc_outputs(with_gradient=with_gradient, want_policy=want_policy, want_obs=True)
-    plan.simulate(to_device(g["x0s"] if x0s is None else x0s, dev),
-                  to_device(g["rnstream"] if rn is None else rn, dev),
-                  to_device(g["xstarts"], dev), out,
-                  dual_y_dx=None if dual is None else to_device(dual, dev),
-                  replay_x=None if replay is None else to_device(replay, dev))
+    x0d = to_device(g["x0s"] if x0s is None else x0s, dev)
+    if ghq is not None:
+        plan.simulate_ghq(x0d, to_device(ghq[0], dev), to_device(ghq[1], dev), to_device(g["xstarts"], dev), out,
+                          dual_y_dx=None if dual is None else to_device(dual, dev),
+                          replay_x=None if replay is None else to_device(replay, dev))
+    else:
+        plan.simulate(x0d, to_device(g["rnstream"] if rn is None else rn, dev),
+                      to_device(g["xstarts"], dev), out,
+                      dual_y_dx=None if dual is None else to_device(dual, dev),
+                      replay_x=None if replay is None else to_device(replay, dev))
     eto = plan.eto(out)
     torch.cuda.synchronize()
     d, M, R, h = plan.d, plan.M, plan.R, plan.h
@@ -219,17 +226,26 @@ def _compare(key, g, r, o, o_replay, M, kind="full"):
     return stats
 
 
-def _end_to_end(oracle, key, g, M, cost=None, plan_opts=None, kind="full", htol=1e-4):
+def _end_to_end(oracle, key, g, M, cost=None, plan_opts=None, kind="full", htol=1e-4, rule="EI", theta=0.0,
+                ghq=None):
+    """GPU launch, the oracle on the same inputs, the oracle's replay of the GPU's policy points, then
+    _compare.  rule / theta: the base decision rule (EI, POI, LCB); ghq = (nodes, weights): the
+    Gauss–Hermite estimator instead of Monte-Carlo draws (M = the number of node vectors)."""
     opts = dict(plan_opts or {})
     if htol != 1e-4:
         opts["htol"] = htol
-    r = _run(_plan(g, **opts), g)
+    rid = {"EI": 0, "POI": 1, "LCB": 2}[rule]
+    if ghq is not None:
+        opts["M"] = ghq[0].shape[0]
+    r = _run(_plan(g, theta=theta, rule=rid, **opts), g, ghq=ghq)
     nt = _threads()
-    kw = dict(nthreads=nt, cost=cost, htol=htol)
-    o = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
-                           **kw)
+    kw = dict(nthreads=nt, cost=cost, htol=htol, theta=theta, rule=rule)
+    rn = None if ghq is not None else g["rnstream"]
+    if ghq is not None:
+        kw["ghq"] = ghq
+    o = oracle.simulate_mc(_osur(oracle, g), g["x0s"], rn, g["xstarts"], g["lbs"], g["ubs"], int(g["h"]), **kw)
     rp = np.asfortranarray(r["policy_x"][:, 1:])
-    o2 = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
+    o2 = oracle.simulate_mc(_osur(oracle, g), g["x0s"], rn, g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
                             replay_x=rp, want_policy=False, want_kappa=True, **kw)
     return _compare(key, g, r, o, o2, M, kind=kind)
 

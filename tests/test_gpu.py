@@ -58,68 +58,28 @@ def test_end_to_end_vs_oracle(gpu, oracle, name, M, R, ell, kind):
 @pytest.mark.parametrize("rule,rid,theta", [("POI", 1, 0.0), ("POI", 1, 0.05), ("LCB", 2, 2.0)])
 def test_other_rules_vs_oracle(gpu, oracle, rule, rid, theta):
     """POI / LCB base rules (decision_rules.jl:101-127): primitives, then full rollouts with the
-    inner Newton solves on both sides, and a replay of the GPU's policy points."""
-    g = _problem_arrays("C2", 32, 4)
+    inner Newton solves on both sides and the oracle's replay of the GPU's policy points, under the
+    same T2 / T3 bounds and non-vacuity guard as EI (tests/parity.py)."""
+    g = _problem_arrays("C2", 64, 4)
     p = _plan(g, theta=theta, rule=rid)
     osur = _osur(oracle, g)
     pts = np.asfortranarray(g["xstarts"][:, :8] * 0.9 + 0.05)
     np.testing.assert_allclose(p.eval_base(pts), oracle.eval_base(osur, pts, theta=theta, rule=rule),
                                rtol=1e-9, atol=1e-12)
-    r = _run(p, g)
-    o = oracle.simulate_mc(osur, g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
-                           theta=theta, rule=rule, nthreads=8)
-    assert (r["status"] == o["status"]).all()
-    ok = r["status"] == 0
-    same = ok & np.all(np.abs(r["policy_x"] - o["policy_x"]) <= 1e-6 * (1 + np.abs(o["policy_x"])), axis=(0, 1))
-    assert same.sum() >= 0.97 * ok.sum(), (same.sum(), ok.sum())
-    np.testing.assert_allclose(r["values"][same], o["values"][same], rtol=1e-8, atol=1e-11)
-    _assert_grads_close(r["grad_x"][:, same], o["grad_x"][:, same], rtol=1e-5)
-    np.testing.assert_array_equal(r["evals"][:3][:, same], o["evals"][:, same])
-    rp = np.asfortranarray(r["policy_x"][:, 1:])
-    o2 = oracle.simulate_mc(osur, g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
-                            theta=theta, rule=rule, replay_x=rp, nthreads=8)
-    np.testing.assert_allclose(r["values"][ok], o2["values"][ok], rtol=1e-8, atol=1e-11)
-    _assert_grads_close(r["grad_x"][:, ok], o2["grad_x"][:, ok], rtol=1e-5)
-    _assert_grads_close(r["grad_theta"][:, ok], o2["grad_theta"][:, ok], rtol=1e-5)
+    _end_to_end(oracle, f"C2 {rule} theta={theta} (64 x 4)", g, 64, rule=rule, theta=theta)
 
 
 def test_ghq_vs_oracle(gpu, oracle):
-    """Gauss–Hermite estimator (rollout.jl:409-467): h = 2, 5 nodes → 125 node vectors × 2 restarts,
-    full rollouts with inner solves on both sides, then a replay of the GPU's policy points."""
-    import torch
-    from mrbo.engine import from_device, to_device
+    """Gauss–Hermite estimator (rollout.jl:409-467): h = 2, 5 nodes → 125 node vectors × 4 restarts,
+    full rollouts with inner solves on both sides and the oracle's replay of the GPU's policy
+    points, under the T2 / T3 bounds and non-vacuity guard of tests/parity.py."""
     from mrbo.rollout import ghq_node_arrays
     from mrbo.utils import gauss_hermite, generate_indices
-    g = _problem_arrays("C2", 8, 2)
-    h = int(g["h"])
+    g = _problem_arrays("C2", 8, 4)
     t, w = gauss_hermite(5)
-    nodes, weights = ghq_node_arrays(t, w, generate_indices(5, h + 1))
-    M = nodes.shape[0]
-    p = _plan(g, M=M)
-    dev = "cuda:0"
-    out = p.alloc_outputs(with_gradient=True, want_policy=True, want_obs=True)
-    p.simulate_ghq(to_device(g["x0s"], dev), to_device(nodes, dev), to_device(weights, dev),
-                   to_device(g["xstarts"], dev), out)
-    torch.cuda.synchronize()
-    d, R = p.d, p.R
-    r = dict(values=from_device(out["values"], (M, R)), status=from_device(out["status"], (M, R)),
-             grad_x=from_device(out["grad_x"], (d, M, R)), grad_theta=from_device(out["grad_theta"], (1, M, R)),
-             policy_x=from_device(out["policy_x"], (d, h + 1, M, R)), evals=from_device(out["evals"], (5, M, R)))
-    osur = _osur(oracle, g)
-    o = oracle.simulate_mc(osur, g["x0s"], None, g["xstarts"], g["lbs"], g["ubs"], h, ghq=(nodes, weights),
-                           nthreads=8)
-    assert (r["status"] == o["status"]).all()
-    ok = r["status"] == 0
-    same = ok & np.all(np.abs(r["policy_x"] - o["policy_x"]) <= 1e-6 * (1 + np.abs(o["policy_x"])), axis=(0, 1))
-    assert same.sum() >= 0.97 * ok.sum(), (same.sum(), ok.sum())
-    np.testing.assert_allclose(r["values"][same], o["values"][same], rtol=1e-8, atol=1e-13)
-    _assert_grads_close(r["grad_x"][:, same], o["grad_x"][:, same], rtol=1e-5)
-    np.testing.assert_array_equal(r["evals"][:3][:, same], o["evals"][:, same])
-    rp = np.asfortranarray(r["policy_x"][:, 1:])
-    o2 = oracle.simulate_mc(osur, g["x0s"], None, g["xstarts"], g["lbs"], g["ubs"], h, ghq=(nodes, weights),
-                            replay_x=rp, nthreads=8)
-    np.testing.assert_allclose(r["values"][ok], o2["values"][ok], rtol=1e-8, atol=1e-13)
-    _assert_grads_close(r["grad_x"][:, ok], o2["grad_x"][:, ok], rtol=1e-5)
+    nodes, weights = ghq_node_arrays(t, w, generate_indices(5, int(g["h"]) + 1))
+    _end_to_end(oracle, f"C2 Gauss-Hermite ({nodes.shape[0]} node vectors x 4)", g, nodes.shape[0],
+                ghq=(np.asfortranarray(nodes), np.asfortranarray(weights)))
 
 
 @pytest.mark.parametrize("kernel,kid", [("matern32", 1), ("matern12", 2), ("se", 3), ("periodic", 4)])
