@@ -226,6 +226,24 @@ def _compare(key, g, r, o, o_replay, M, kind="full"):
     return stats
 
 
+def _replay_t2(g, r, o, ok=None):
+    """T2 on a replay run alone (the oracle replayed the GPU's policy points, want_kappa=True):
+    every trajectory in `ok` has e_val ≤ 1e-9 and e_grad ≤ max(1e-9, n·u·κ(t)) (module docstring).
+    Returns (max e_val, max e_grad / tol)."""
+    ok = np.ones(r["values"].shape, dtype=bool) if ok is None else ok
+    m = ok.ravel(order="F")
+    if not m.any():
+        return 0.0, 0.0
+    gscale = max(float(np.abs(o["grad_x"][:, ok]).max()), 1e-300)
+    ev, eg = _errs(r, o, gscale)
+    d, N = g["X"].shape
+    tol = grad_tolerance(o["kappa"].ravel(order="F"), N + int(g["h"]))
+    ratio = eg[m] / tol[m]
+    assert ev[m].max() <= 1e-9, (ev[m].max(), int((ev[m] > 1e-9).sum()))
+    assert ratio.max() <= 1.0, (float(ratio.max()), int((ratio > 1).sum()), float(tol[m].max()))
+    return float(ev[m].max()), float(ratio.max())
+
+
 def _end_to_end(oracle, key, g, M, cost=None, plan_opts=None, kind="full", htol=1e-4, rule="EI", theta=0.0,
                 ghq=None):
     """GPU launch, the oracle on the same inputs, the oracle's replay of the GPU's policy points, then

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN_CASES, load_golden
-from parity import _assert_grads_close, _end_to_end, _osur, _plan, _problem_arrays, _run
+from parity import _assert_grads_close, _end_to_end, _osur, _plan, _problem_arrays, _replay_t2, _run
 
 pytestmark = pytest.mark.gpu
 
@@ -92,13 +92,11 @@ def test_other_kernels_replay_vs_oracle(gpu, oracle, kernel, kid):
     r = _run(p, g)
     rp = np.asfortranarray(r["policy_x"][:, 1:])
     o = oracle.simulate_mc(_osur(oracle, g, kernel), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"],
-                           int(g["h"]), replay_x=rp, nthreads=8)
+                           int(g["h"]), replay_x=rp, nthreads=8, want_kappa=True)
     assert (r["status"] == o["status"]).all()
     if kernel == "matern12":  # ψ''(0) > 0: Dk(0) is indefinite, gp_draw's cholesky fails (PosDefException)
         assert (r["status"] & 2).all()
-    ok = r["status"] == 0
-    np.testing.assert_allclose(r["values"][ok], o["values"][ok], rtol=1e-8, atol=1e-11)
-    _assert_grads_close(r["grad_x"][:, ok], o["grad_x"][:, ok], rtol=1e-5)
+    _replay_t2(g, r, o, r["status"] == 0)
 
 
 @pytest.mark.parametrize("d,N,h", [(1, 12, 2), (3, 24, 2), (4, 40, 3), (5, 30, 2), (7, 48, 2), (8, 64, 3), (3, 96, 2),
@@ -121,9 +119,8 @@ def test_dimensions_and_sizes_replay_vs_oracle(gpu, oracle, d, N, h):
     assert (r["status"] == 0).all()
     rp = np.asfortranarray(r["policy_x"][:, 1:])
     o = oracle.simulate_mc(_osur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], h,
-                           replay_x=rp, nthreads=8)
-    np.testing.assert_allclose(r["values"], o["values"], rtol=1e-8, atol=1e-11)
-    _assert_grads_close(r["grad_x"], o["grad_x"], rtol=1e-5)
+                           replay_x=rp, nthreads=8, want_kappa=True)
+    _replay_t2(g, r, o)
 
 
 def test_full_size_c3_properties(gpu):
