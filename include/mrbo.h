@@ -254,7 +254,10 @@ int mrbo_plan_info(const mrbo_plan_t* plan, int32_t* info, int32_t n);
  * counterpart; scheduling only, results do not depend on it): `order` is a DEVICE array of n =
  * M×R int32 trajectory indices (m + M·r), a permutation, handed to the persistent waves in that
  * order -- e.g. longest first by the previous launch's work counters, which shortens the launch's
- * tail.  Caller-owned; it must stay valid while launches use it.  NULL restores the identity. */
+ * tail.  Caller-owned; it must stay valid while launches use it.  NULL restores the identity.
+ * n != M×R: MRBO_ERR_ARG.  An entry outside [0, M×R) runs the trajectory of its own queue index
+ * (no write outside the outputs); tests/test_gpu_schedule.py holds every output bit-identical
+ * under permuted, out-of-range and longest-first orders. */
 int mrbo_plan_set_order(mrbo_plan_t* plan, const int32_t* order, int64_t n);
 
 #ifdef __cplusplus
