@@ -55,9 +55,12 @@ def parse():
                     help="cost-weighted EI with NonUniformCost (cost_functions.jl:5-20; build-defined, "
                          "parity unpinned)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--longest-first", action="store_true",
-                    help="hand trajectories to the waves longest first by the previous step's work "
-                         "counters (default: index order; measured 1 %% slower at C3, DESIGN.md §9)")
+    ap.add_argument("--schedule", choices=("auto", "index", "longest-first"), default="index",
+                    help="order in which the persistent waves take the trajectories: index order "
+                         "(default), or longest first by the first step's work counters; auto = longest "
+                         "first when the launch is at most two rounds of the resident waves deep (C2: "
+                         "kernel 0.56 -> 0.53 ms; at C3's 32 rounds it measured 1 %% slower; DESIGN.md §9)")
+    ap.add_argument("--longest-first", action="store_true", help="same as --schedule longest-first")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--eta", type=float, default=0.01, help="StandardSGA step (optimizers.jl:6-23; default 0.01)")
     ap.add_argument("--dump", default="", help="write the final ETO and x0 (npz) here (rank 0)")
@@ -207,6 +210,9 @@ def main():
     T = pb.T
     plan = _plan_for(T.s, h, hi - lo, R, pb.es.get_starts().shape[1], pb.lbs, pb.ubs, T.θ[0], local,
                      dict(sample_offset=lo, samples_total=M_total, **pb.plan_opts()))
+    geo = plan.info()   # resident persistent waves: workgroups x waves per workgroup
+    longest_first = args.longest_first or args.schedule == "longest-first" or (
+        args.schedule == "auto" and (hi - lo) * R <= 2 * geo["blocks"] * geo["waves_per_group"])
     dev = f"cuda:{local}"
     drn = to_device(np.asfortranarray(pb.tp.rnstream_sequence[lo:hi]), dev)   # resident in HBM
     dxs = to_device(pb.es.get_starts(), dev)
@@ -237,8 +243,12 @@ def main():
         else:
             e = plan.partial_moments(out, hi - lo)     # this shard's (Σ, M2) rows
         evals_acc.add_(out["evals"])        # also in warmup: no first-use op inside the timed region
-        if args.longest_first:
-            plan.order_longest_first(out)   # the next step's schedule (same work)
+        if longest_first and "ordered" not in last:
+            # the schedule of every later step, from this (first) step's work counters: an SGA step
+            # moves x0 a little and the MC streams repeat, so a trajectory's work repeats closely;
+            # re-sorting every step costs more (≈ 0.09 ms at C2) than it gains
+            plan.order_longest_first(out)
+            last["ordered"] = True
         if not sharded:
             # eswavs + StandardSGA of every active restart on the device (mrbo_sga_step): x0 and the
             # stop flags stay in HBM, so the next launch follows without a host round trip
@@ -312,7 +322,7 @@ def main():
                    "exchange": "none" if not sharded else f"all-gather of (Σ, M2) moments, {W * R * 8} B/rank/step",
                    "outer_step": f"eswavs + StandardSGA η={args.eta:g}, no clip (utils.jl:114-123, "
                                  f"optimizers.jl:16-22)",
-                   "schedule": "longest first (previous step's work counters)" if args.longest_first else "index order"},
+                   "schedule": "longest first (first step's work counters)" if longest_first else "index order"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": f"rollout_kernel<{d},{info['rpl']},{info['spec']}>", "kernel_ms": kms, "flops_per_launch": fl,
