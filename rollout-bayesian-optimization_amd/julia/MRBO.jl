@@ -1,21 +1,45 @@
 # MRBO.jl -- Julia binding of libmrbo.so (include/mrbo.h) for the reference package.
 #
-# Include after `rollout_bayesian_optimization.jl`; it adds a GPU method of
-# `simulate_trajectory_mc` (rollout.jl:279-340) selected by a trailing `MrboBackend()` argument,
-# keeping the reference's keyword contract: caller-owned containers overwritten in place, an
-# ExpectedTrajectoryOutput returned, T.x0 set from tp (T.θ kept, Q12), exceptions on failure.
+# The reference is not a package: rollout_bayesian_optimization.jl:1-30 `include`s its files into
+# `Main`, so its types (Surrogate, Trajectory, TrajectoryParameters, ...) and generic functions
+# (simulate_trajectory_mc, simulate_trajectory_ghq, the get_* accessors) are bindings of `Main`.
+# This module therefore takes every reference name it uses from `Main` explicitly, and
+# `import`s the two generic functions it adds methods to, so that the methods below extend the
+# reference's own `simulate_trajectory_mc` (rollout.jl:279-340) and `simulate_trajectory_ghq`
+# (rollout.jl:409-467) rather than defining new functions:
 #
-# Not executed in this repository's CI (no julia in the image); the same ABI is exercised by the
-# Python ctypes harness (rollout-bayesian-optimization_amd/mrbo/_lib.py) and tests/test_gpu.py.
+#     include("rollout_bayesian_optimization.jl")
+#     include("path/to/rollout-bayesian-optimization_amd/julia/MRBO.jl"); using .MRBO
+#     eto = simulate_trajectory_mc(T, tp, MrboBackend(0); inner_solve_xstarts=..., resolutions=..., ...)
+#
+# The GPU methods keep the reference's keyword contract: caller-owned containers overwritten in
+# place, an ExpectedTrajectoryOutput returned, T.x0 set from tp (T.θ kept, Q12), an exception on a
+# failed trajectory.  The trailing `MrboBackend` positional argument selects them; it is not an
+# AbstractObservable, so the reference's observable overload (rollout.jl:342) is not ambiguous.
+#
+# julia is not installed in this image, so the file is never executed here.  What can be checked
+# without julia is checked by tests/test_julia_binding.py: the struct mirrors against the C
+# structs of include/mrbo.h (field order, types, offsets), every ccall against its C prototype,
+# and every reference name used here against the names this module brings into scope from Main.
 module MRBO
 
-export MrboBackend, MrboPlan, mrbo_simulate!, mrbo_log_likelihood, mrbo_multistart_base_solve!
+# the reference's generic functions this module adds methods to (must be `import`ed to extend)
+import Main: simulate_trajectory_mc, simulate_trajectory_ghq
+# the reference's types, constructors and accessors used below (Main-level bindings)
+using Main: Surrogate, Trajectory, TrajectoryParameters, ExpectedTrajectoryOutput,
+            Matern52, Matern32, Matern12, SquaredExponential, Periodic,
+            get_observed, get_active_covariates, get_active_cholesky, get_active_coefficients,
+            get_active_observations, get_observations, get_kernel, get_decision_rule, get_name,
+            get_spatial_bounds, get_starting_point, get_base_surrogate, set_start!
+import Distributions
+
+export MrboBackend, MrboPlan, mrbo_multistart_base_solve!, mrbo_log_likelihood
 
 const libmrbo = joinpath(@__DIR__, "..", "mrbo", "libmrbo.so")
 const MRBO_FLAG_HOST_POINTERS = UInt32(1)
 const MRBO_FLAG_NO_GRADIENT = UInt32(2)
 
-# mirrors mrbo_surrogate_t (C layout: three Int32, then Float64 fields)
+# mirrors mrbo_surrogate_t (include/mrbo.h; Julia isbits structs use the C layout)
 struct MrboSurrogateC
     d::Int32
     N::Int32
@@ -69,44 +93,60 @@ mutable struct MrboPlan
     h::Int
 end
 
-kernel_id(ψ) = ψ.constructor === Matern52 ? 0 : ψ.constructor === Matern32 ? 1 :
-               ψ.constructor === Matern12 ? 2 : ψ.constructor === SquaredExponential ? 3 :
-               ψ.constructor === Periodic ? 4 : error("kernel not compiled into libmrbo")
-kernel_period(ψ) = ψ.constructor === Periodic ? ψ.θ[2] : 1.0
+mrbo_kernel_id(ψ) = ψ.constructor === Matern52 ? Int32(0) : ψ.constructor === Matern32 ? Int32(1) :
+                    ψ.constructor === Matern12 ? Int32(2) : ψ.constructor === SquaredExponential ? Int32(3) :
+                    ψ.constructor === Periodic ? Int32(4) : error("kernel not compiled into libmrbo")
+mrbo_kernel_period(ψ) = ψ.constructor === Periodic ? Float64(ψ.θ[2]) : 1.0
 
-function check(rc)
-    rc == 0 && return
+function mrbo_check(rc)
+    rc == 0 && return nothing
     msg = unsafe_string(ccall((:mrbo_last_error, libmrbo), Cstring, ()))
     error("libmrbo error $rc: $msg")
 end
 
-rule_id(g) = get_name(g) == "EI" ? 0 : get_name(g) == "POI" ? 1 : get_name(g) == "LCB" ? 2 :
-             error("decision rule not compiled into libmrbo")
+mrbo_rule_id(g) = get_name(g) == "EI" ? Int32(0) : get_name(g) == "POI" ? Int32(1) :
+                  get_name(g) == "LCB" ? Int32(2) : error("decision rule not compiled into libmrbo")
 
+# The device state of simulate_trajectory_mc's setup: FantasySurrogate(s, h) over the base
+# surrogate (radial_basis_surrogates.jl:345-381) + TrajectoryParameters (trajectory.jl:43-94).
 function MrboPlan(s::Surrogate, tp::TrajectoryParameters, θ::Vector{Float64}, nstarts::Int;
                   device::Int = 0, max_iters = 50, max_ls = 20, seed = 1906, M::Int = tp.mc_iters)
     N = get_observed(s)
-    X = Matrix(get_active_covariates(s))
-    L = Matrix(get_active_cholesky(s))
-    c = Vector(get_active_coefficients(s))
-    y = Vector(get_active_observations(s))
+    X = Matrix{Float64}(get_active_covariates(s))
+    L = Matrix{Float64}(get_active_cholesky(s))
+    c = Vector{Float64}(get_active_coefficients(s))
+    y = Vector{Float64}(get_active_observations(s))
     fmini = minimum(get_observations(s))                 # over the capacity buffer (Q3)
     lbs, ubs = get_spatial_bounds(tp)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
     GC.@preserve X L c y lbs ubs begin
-        sd = MrboSurrogateC(size(X, 1), N, kernel_id(get_kernel(s)), get_kernel(s).θ[1], s.σn2, fmini,
-                            pointer(X), pointer(L), N, pointer(c), pointer(y), kernel_period(get_kernel(s)))
-        pd = MrboParamsC(tp.horizon, M, 1, nstarts, rule_id(get_decision_rule(s)), θ[1], pointer(lbs), pointer(ubs),
-                         max_iters, max_ls, 1e-3, 1e-3, 1e-8, 1e-4, 1e-8, seed, 0, 0, 0, 1.0, C_NULL)
-        h = Ref{Ptr{Cvoid}}(C_NULL)
-        check(ccall((:mrbo_plan_create, libmrbo), Cint,
-                    (Ref{MrboSurrogateC}, Ref{MrboParamsC}, Cint, Ref{Ptr{Cvoid}}), sd, pd, device, h))
+        sd = MrboSurrogateC(Int32(size(X, 1)), Int32(N), mrbo_kernel_id(get_kernel(s)), get_kernel(s).θ[1], s.σn2,
+                            fmini, pointer(X), pointer(L), Int32(N), pointer(c), pointer(y),
+                            mrbo_kernel_period(get_kernel(s)))
+        pd = MrboParamsC(Int32(tp.horizon), Int32(M), Int32(1), Int32(nstarts), mrbo_rule_id(get_decision_rule(s)),
+                         θ[1], pointer(lbs), pointer(ubs), Int32(max_iters), Int32(max_ls), 1e-3, 1e-3, 1e-8,
+                         1e-4, 1e-8, UInt64(seed), Int32(0), Int32(0), Int32(0), 1.0, Ptr{Float64}(C_NULL))
+        mrbo_check(ccall((:mrbo_plan_create, libmrbo), Cint,
+                         (Ref{MrboSurrogateC}, Ref{MrboParamsC}, Cint, Ref{Ptr{Cvoid}}), sd, pd, device, h))
     end
     plan = MrboPlan(h[], size(X, 1), M, 1, tp.horizon)
     finalizer(p -> ccall((:mrbo_plan_destroy, libmrbo), Cint, (Ptr{Cvoid},), p.handle), plan)
     return plan
 end
 
-# The GPU method of rollout.jl:279-340.
+# ExpectedTrajectoryOutput tail of rollout.jl:328-339 (the reference's own reductions)
+function mrbo_eto(resolutions, gx, gθ)
+    μxθ = Distributions.mean(resolutions)
+    σ_μxθ = Distributions.std(resolutions, mean=μxθ)
+    (isnothing(gx) || isnothing(gθ)) && return ExpectedTrajectoryOutput(μxθ=μxθ, σ_μxθ=σ_μxθ)
+    ∇μx = vec(Distributions.mean(gx, dims=2))
+    σ_∇μx = vec(Distributions.std(gx, dims=2, mean=∇μx))
+    ∇μθ = vec(Distributions.mean(gθ, dims=2))
+    σ_∇μθ = vec(Distributions.std(gθ, dims=2, mean=∇μθ))
+    return ExpectedTrajectoryOutput(μxθ=μxθ, σ_μxθ=σ_μxθ, ∇μx=∇μx, σ_∇μx=σ_∇μx, ∇μθ=∇μθ, σ_∇μθ=σ_∇μθ)
+end
+
+# The GPU method of the reference's simulate_trajectory_mc (rollout.jl:279-340).
 function simulate_trajectory_mc(T::Trajectory, tp::TrajectoryParameters, backend::MrboBackend;
                                 inner_solve_xstarts::Matrix{Float64}, resolutions::Vector{Float64},
                                 spatial_gradients_container::Union{Nothing, Matrix{Float64}} = nothing,
@@ -117,24 +157,20 @@ function simulate_trajectory_mc(T::Trajectory, tp::TrajectoryParameters, backend
     x0 = copy(T.x0)
     rns = tp.rnstream_sequence
     status = zeros(Int32, tp.mc_iters)
-    gx = with_grad ? spatial_gradients_container : C_NULL
-    gθ = with_grad ? hyperparameter_gradients_container : C_NULL
+    gx = with_grad ? spatial_gradients_container : Matrix{Float64}(undef, 0, 0)
+    gθ = with_grad ? hyperparameter_gradients_container : Matrix{Float64}(undef, 0, 0)
     flags = MRBO_FLAG_HOST_POINTERS | (with_grad ? UInt32(0) : MRBO_FLAG_NO_GRADIENT)
-    check(ccall((:mrbo_simulate_mc, libmrbo), Cint,
-                (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Ptr{Float64},
-                 Ptr{Int64}, UInt32, Ptr{Cvoid}),
-                plan.handle, x0, rns, inner_solve_xstarts, C_NULL, C_NULL, resolutions, gx, gθ, status,
-                C_NULL, C_NULL, C_NULL, flags, C_NULL))
+    GC.@preserve x0 rns inner_solve_xstarts resolutions gx gθ status begin
+        mrbo_check(ccall((:mrbo_simulate_mc, libmrbo), Cint,
+                         (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                          Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Ptr{Float64},
+                          Ptr{Int64}, UInt32, Ptr{Cvoid}),
+                         plan.handle, x0, rns, inner_solve_xstarts, C_NULL, C_NULL, resolutions,
+                         with_grad ? pointer(gx) : C_NULL, with_grad ? pointer(gθ) : C_NULL, status,
+                         C_NULL, C_NULL, C_NULL, flags, C_NULL))
+    end
     any(!=(0), status) && throw(ErrorException("rollout failed on $(count(!=(0), status)) trajectories (status bits $(reduce(|, status)))"))
-    μxθ = Distributions.mean(resolutions)
-    σ_μxθ = Distributions.std(resolutions, mean=μxθ)
-    with_grad || return ExpectedTrajectoryOutput(μxθ=μxθ, σ_μxθ=σ_μxθ)
-    ∇μx = vec(Distributions.mean(spatial_gradients_container, dims=2))
-    σ_∇μx = vec(Distributions.std(spatial_gradients_container, dims=2, mean=∇μx))
-    ∇μθ = vec(Distributions.mean(hyperparameter_gradients_container, dims=2))
-    σ_∇μθ = vec(Distributions.std(hyperparameter_gradients_container, dims=2, mean=∇μθ))
-    return ExpectedTrajectoryOutput(μxθ=μxθ, σ_μxθ=σ_μxθ, ∇μx=∇μx, σ_∇μx=σ_∇μx, ∇μθ=∇μθ, σ_∇μθ=σ_∇μθ)
+    return mrbo_eto(resolutions, with_grad ? gx : nothing, with_grad ? gθ : nothing)
 end
 
 # The GPU method of simulate_trajectory_ghq (rollout.jl:409-467): node vectors nodes[indices[m]]
@@ -149,32 +185,28 @@ function simulate_trajectory_ghq(T::Trajectory, tp::TrajectoryParameters, backen
     depth = length(first(indices))
     tn = Matrix{Float64}(undef, M, depth)
     tw = Matrix{Float64}(undef, M, depth)
-    for m in 1:M
-        tn[m, :] .= nodes[indices[m]]
-        tw[m, :] .= weights[indices[m]]
+    for (m, idx) in enumerate(indices)
+        tn[m, :] .= nodes[collect(idx)]
+        tw[m, :] .= weights[collect(idx)]
     end
     plan = MrboPlan(get_base_surrogate(T), tp, T.θ, size(inner_solve_xstarts, 2); device = backend.device, M = M)
     with_grad = !isnothing(spatial_gradients_container) && !isnothing(hyperparameter_gradients_container)
     x0 = copy(T.x0)
     status = zeros(Int32, M)
-    gx = with_grad ? spatial_gradients_container : C_NULL
-    gθ = with_grad ? hyperparameter_gradients_container : C_NULL
+    gx = with_grad ? spatial_gradients_container : Matrix{Float64}(undef, 0, 0)
+    gθ = with_grad ? hyperparameter_gradients_container : Matrix{Float64}(undef, 0, 0)
     flags = MRBO_FLAG_HOST_POINTERS | (with_grad ? UInt32(0) : MRBO_FLAG_NO_GRADIENT)
-    check(ccall((:mrbo_simulate_ghq, libmrbo), Cint,
-                (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Ptr{Float64},
-                 Ptr{Int64}, UInt32, Ptr{Cvoid}),
-                plan.handle, x0, tn, tw, inner_solve_xstarts, C_NULL, C_NULL, resolutions, gx, gθ, status,
-                C_NULL, C_NULL, C_NULL, flags, C_NULL))
+    GC.@preserve x0 tn tw inner_solve_xstarts resolutions gx gθ status begin
+        mrbo_check(ccall((:mrbo_simulate_ghq, libmrbo), Cint,
+                         (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                          Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64},
+                          Ptr{Float64}, Ptr{Int64}, UInt32, Ptr{Cvoid}),
+                         plan.handle, x0, tn, tw, inner_solve_xstarts, C_NULL, C_NULL, resolutions,
+                         with_grad ? pointer(gx) : C_NULL, with_grad ? pointer(gθ) : C_NULL, status,
+                         C_NULL, C_NULL, C_NULL, flags, C_NULL))
+    end
     any(!=(0), status) && throw(ErrorException("rollout failed on $(count(!=(0), status)) trajectories"))
-    μxθ = Distributions.mean(resolutions)
-    σ_μxθ = Distributions.std(resolutions, mean=μxθ)
-    with_grad || return ExpectedTrajectoryOutput(μxθ=μxθ, σ_μxθ=σ_μxθ)
-    ∇μx = vec(Distributions.mean(spatial_gradients_container, dims=2))
-    σ_∇μx = vec(Distributions.std(spatial_gradients_container, dims=2, mean=∇μx))
-    ∇μθ = vec(Distributions.mean(hyperparameter_gradients_container, dims=2))
-    σ_∇μθ = vec(Distributions.std(hyperparameter_gradients_container, dims=2, mean=∇μθ))
-    return ExpectedTrajectoryOutput(μxθ=μxθ, σ_μxθ=σ_μxθ, ∇μx=∇μx, σ_∇μx=σ_∇μx, ∇μθ=∇μθ, σ_∇μθ=σ_∇μθ)
+    return mrbo_eto(resolutions, with_grad ? gx : nothing, with_grad ? gθ : nothing)
 end
 
 
@@ -190,26 +222,30 @@ function mrbo_multistart_base_solve!(s::Surrogate, xfinal::Vector{Float64}; spat
         return nothing
     end
     N = get_observed(s)
-    X = Matrix(get_active_covariates(s))
-    L = Matrix(get_active_cholesky(s))
-    c = Vector(get_active_coefficients(s))
-    y = Vector(get_active_observations(s))
+    X = Matrix{Float64}(get_active_covariates(s))
+    L = Matrix{Float64}(get_active_cholesky(s))
+    c = Vector{Float64}(get_active_coefficients(s))
+    y = Vector{Float64}(get_active_observations(s))
     d, n = size(guesses)
     h = Ref{Ptr{Cvoid}}(C_NULL)
     GC.@preserve X L c y spatial_lbs spatial_ubs begin
-        sd = MrboSurrogateC(d, N, kernel_id(get_kernel(s)), get_kernel(s).θ[1], s.σn2, minimum(get_observations(s)),
-                            pointer(X), pointer(L), N, pointer(c), pointer(y), kernel_period(get_kernel(s)))
-        pd = MrboParamsC(0, 1, 1, 1, rule_id(get_decision_rule(s)), θfixed[1], pointer(spatial_lbs),
-                         pointer(spatial_ubs), 50, 20, 1e-3, 1e-3, 1e-8, 1e-4, 1e-8, 1906, 0, 0, 0, 1.0, C_NULL)
-        check(ccall((:mrbo_plan_create, libmrbo), Cint,
-                    (Ref{MrboSurrogateC}, Ref{MrboParamsC}, Cint, Ref{Ptr{Cvoid}}), sd, pd, device, h))
+        sd = MrboSurrogateC(Int32(d), Int32(N), mrbo_kernel_id(get_kernel(s)), get_kernel(s).θ[1], s.σn2,
+                            minimum(get_observations(s)), pointer(X), pointer(L), Int32(N), pointer(c), pointer(y),
+                            mrbo_kernel_period(get_kernel(s)))
+        pd = MrboParamsC(Int32(0), Int32(1), Int32(1), Int32(1), mrbo_rule_id(get_decision_rule(s)), θfixed[1],
+                         pointer(spatial_lbs), pointer(spatial_ubs), Int32(50), Int32(20), 1e-3, 1e-3, 1e-8, 1e-4,
+                         1e-8, UInt64(1906), Int32(0), Int32(0), Int32(0), 1.0, Ptr{Float64}(C_NULL))
+        mrbo_check(ccall((:mrbo_plan_create, libmrbo), Cint,
+                         (Ref{MrboSurrogateC}, Ref{MrboParamsC}, Cint, Ref{Ptr{Cvoid}}), sd, pd, device, h))
     end
     xs, fs, st = zeros(d, n), zeros(n), zeros(Int32, n)
     try
-        check(ccall((:mrbo_base_solve, libmrbo), Cint,
-                    (Ptr{Cvoid}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int64}, UInt32,
-                     Ptr{Cvoid}),
-                    h[], n, guesses, xs, fs, st, C_NULL, MRBO_FLAG_HOST_POINTERS, C_NULL))
+        GC.@preserve guesses xs fs st begin
+            mrbo_check(ccall((:mrbo_base_solve, libmrbo), Cint,
+                             (Ptr{Cvoid}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int64},
+                              UInt32, Ptr{Cvoid}),
+                             h[], n, guesses, xs, fs, st, C_NULL, MRBO_FLAG_HOST_POINTERS, C_NULL))
+        end
     finally
         ccall((:mrbo_plan_destroy, libmrbo), Cint, (Ptr{Cvoid},), h[])
     end
@@ -228,18 +264,18 @@ end
 # from its fg! closure (one launch evaluates every trial lengthscale of a line search).
 function mrbo_log_likelihood(s::Surrogate, ells::Vector{Float64})
     N = get_observed(s)
-    X = Matrix(get_active_covariates(s))
-    y = Vector(get_active_observations(s))
+    X = Matrix{Float64}(get_active_covariates(s))
+    y = Vector{Float64}(get_active_observations(s))
     P = length(ells)
     ll, dll, st = zeros(P), zeros(P), zeros(Int32, P)
     GC.@preserve X y ells ll dll st begin
-        sd = MrboSurrogateC(size(X, 1), N, kernel_id(get_kernel(s)), get_kernel(s).θ[1], s.σn2,
-                            minimum(get_observations(s)), pointer(X), C_NULL, N, C_NULL, pointer(y),
-                            kernel_period(get_kernel(s)))
-        check(ccall((:mrbo_gp_fit, libmrbo), Cint,
-                    (Ref{MrboSurrogateC}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32},
-                     Ptr{Float64}, Ptr{Float64}, UInt32, Ptr{Cvoid}),
-                    sd, P, ells, ll, dll, st, C_NULL, C_NULL, MRBO_FLAG_HOST_POINTERS, C_NULL))
+        sd = MrboSurrogateC(Int32(size(X, 1)), Int32(N), mrbo_kernel_id(get_kernel(s)), get_kernel(s).θ[1], s.σn2,
+                            minimum(get_observations(s)), pointer(X), Ptr{Float64}(C_NULL), Int32(N),
+                            Ptr{Float64}(C_NULL), pointer(y), mrbo_kernel_period(get_kernel(s)))
+        mrbo_check(ccall((:mrbo_gp_fit, libmrbo), Cint,
+                         (Ref{MrboSurrogateC}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32},
+                          Ptr{Float64}, Ptr{Float64}, UInt32, Ptr{Cvoid}),
+                         sd, P, ells, ll, dll, st, C_NULL, C_NULL, MRBO_FLAG_HOST_POINTERS, C_NULL))
     end
     return ll, dll, st
 end
