@@ -158,14 +158,19 @@ def rollout_solve(sur, lbs, ubs, horizon, mc_samples, batch_size, starts, sgd_it
 # ---- the experiment loop (nonmyopic_bayesopt.jl:120-300) -------------------------------------
 def run(function_name, output_dir, budget=15, trials=60, starts=16, horizon=0, mc_samples=200, batch_size=8,
         sgd_iterations=50, optimize=False, seed=1906, device=0, log=print, rules=("ei", "poi", "lcb"), eta=0.01,
-        initial_observations=INITIAL_OBSERVATIONS, solver="sga", fmini_over_capacity=True, incumbent=True):
+        initial_observations=INITIAL_OBSERVATIONS, solver="sga", fmini_over_capacity=True, incumbent=True,
+        reuse_surrogate=True):
     """The experiment loop; `rules` selects a subset of the reference's three acquisitions (all by
     default, as nonmyopic_bayesopt.jl), `eta` the StandardSGA step of the build-defined solver
     (default 0.01, StandardSGA's own default, optimizers.jl:9),
     `initial_observations` the initial design size (5 in the current script, :131), `solver` "sga"
     (StandardSGA, η = eta) or "adam" (BoxAdam, eta box widths per step); fmini_over_capacity=False
     turns the reference's Q3 off (fmini over the observed points, not the zero-padded buffer),
-    incumbent=False drops rollout_solve's incumbent restart and no-repeat pick (the round-2 solver)."""
+    incumbent=False drops rollout_solve's incumbent restart and no-repeat pick (the round-2 solver).
+    reuse_surrogate=True (the reference, :233-235): one surrogate of capacity budget + initial for
+    every rule and trial, reset! per trial -- the kernel carries over between trials, and fmini over
+    the capacity buffer (Q3) sees the stale observations of the previous trial past the initial
+    design; False: a fresh surrogate per trial (the round-3 loop)."""
     testfn = TESTFNS[function_name]()
     lbs, ubs = testfn.get_bounds()
     directory = os.path.join(output_dir, function_name)
@@ -183,14 +188,24 @@ def run(function_name, output_dir, budget=15, trials=60, starts=16, horizon=0, m
                        for _ in range(trials)]
     true_minimum = float(testfn.f(np.asarray(testfn.xopt[0], dtype=np.float64)))
     results = {}
+    sur = None
+    if reuse_surrogate:    # :233 "Preallocate entire surrogate object and reuse"
+        sur = Surrogate(Matern52(), np.zeros((testfn.dim, 1)), np.zeros(1), capacity=budget + initial_observations,
+                        σn2=1e-6)
     for acq, rule, theta in zip(acquisitions, rules, dr_hypers):
+        if reuse_surrogate:
+            sur.set_decision_rule(rule)                                   # :241
         log(f"Conducting experiments with acquisition = {acq}")
         for trial in range(trials):
             Xinit = initial_samples[trial]
             yinit = testfn(Xinit)
-            sur = Surrogate(Matern52(), Xinit, yinit, capacity=budget + initial_observations, decision_rule=rule,
-                            σn2=1e-6)
+            if reuse_surrogate:
+                sur.reset(Xinit, yinit)                                   # :253
+            else:
+                sur = Surrogate(Matern52(), Xinit, yinit, capacity=budget + initial_observations, decision_rule=rule,
+                                σn2=1e-6)
             sur.fmini_over_capacity = fmini_over_capacity
+            ell_start = float(sur.ψ.lengthscale)
             initial_best = float(np.min(yinit))
             times, gaps, allocs, regrets, minobs = (np.zeros(budget) for _ in range(5))
             for b in range(budget):
@@ -210,7 +225,8 @@ def run(function_name, output_dir, budget=15, trials=60, starts=16, horizon=0, m
             for metric, data in zip(METRICS, (times, gaps, allocs, regrets, minobs)):
                 write_to_csv(os.path.join(directory, f"{acq}_{metric}"), data)
             results[(acq, trial)] = dict(times=times, gaps=gaps, simple_regret=regrets, minimum_observations=minobs,
-                                         X=sur.get_active_covariates().copy(), y=sur.get_active_observations().copy())
+                                         X=sur.get_active_covariates().copy(), y=sur.get_active_observations().copy(),
+                                         ell_start=ell_start, ell_end=float(sur.ψ.lengthscale))
     return results
 
 
@@ -219,12 +235,20 @@ MYOPIC_RULES = {"ei": (EI, 0.0), "poi": (POI, 0.0), "lcb": (LCB, 2.0)}   # :151-
 
 
 def run_myopic(function_name, output_dir, budget=100, trials=60, starts=64, seed=1906, device=0, log=print,
-               rules=("ei", "poi", "lcb"), optimize=True, initial_observations=INITIAL_OBSERVATIONS):
+               rules=("ei", "poi", "lcb"), optimize=True, initial_observations=INITIAL_OBSERVATIONS,
+               reuse_surrogate=True, capacity=None):
     """myopic_bayesopt.jl's loop: per budget step xnext = multistart_base_solve!(sur, …; guesses =
     generate_initial_guesses(starts, lbs, ubs), θfixed) -- the deterministic multistart local solve of
     the analytic acquisition on the base surrogate (:224-233), here mrbo_base_solve on the device --
     then the metrics before conditioning (:234-245), condition!, optimize! (lengthscale MLE, bounds
-    [0.1, 5], :248-249) and the minimum observation.  CSVs `<acq>_<metric>.csv` as the reference."""
+    [0.1, 5], :248-249) and the minimum observation.  CSVs `<acq>_<metric>.csv` as the reference.
+
+    reuse_surrogate=True (the reference): ONE surrogate, built once with capacity = budget (:205),
+    serves every rule (set_decision_rule!, :208) and every trial (reset!(sur, Xinit, yinit), :217).
+    reset! keeps the kernel, so each trial starts from the lengthscale the previous trial's last
+    optimize! left (only the very first trial starts at Matern52()'s ℓ = 1), and past `capacity`
+    observations condition! conditions a discarded resized copy (Surrogate.condition).  False: a
+    fresh surrogate with ℓ = 1 and capacity budget + initial per trial (the round-3 loop)."""
     from .rbf_optim import multistart_base_solve
     from .utils import generate_initial_guesses
     testfn = TESTFNS[function_name]()
@@ -241,14 +265,23 @@ def run_myopic(function_name, output_dir, budget=100, trials=60, starts=64, seed
                        for _ in range(trials)]                              # :187
     true_minimum = float(testfn.f(np.asarray(testfn.xopt[0], dtype=np.float64)))
     results = {}
+    sur = None
+    if reuse_surrogate:    # :205 "Preallocate entire surrogate object and reuse"
+        sur = Surrogate(Matern52(), np.zeros((testfn.dim, 1)), np.zeros(1), capacity=capacity or budget, σn2=1e-6)
     for acq in rules:
         make_rule, theta = MYOPIC_RULES[acq]
+        if reuse_surrogate:
+            sur.set_decision_rule(make_rule())                            # :208
         log(f"Conducting experiments with acquisition = {acq}")
         for trial in range(trials):
             Xinit = initial_samples[trial]
             yinit = testfn(Xinit)
-            sur = Surrogate(Matern52(), Xinit, yinit, capacity=budget + initial_observations, decision_rule=make_rule(),
-                            σn2=1e-6)
+            if reuse_surrogate:
+                sur.reset(Xinit, yinit)                                   # :217
+            else:
+                sur = Surrogate(Matern52(), Xinit, yinit, capacity=capacity or budget + initial_observations,
+                                decision_rule=make_rule(), σn2=1e-6)
+            ell_start = float(sur.ψ.lengthscale)
             initial_best = float(np.min(yinit))
             times, gaps, allocs, regrets, minobs = (np.zeros(budget) for _ in range(5))
             xnext = np.zeros(testfn.dim)
@@ -268,7 +301,8 @@ def run_myopic(function_name, output_dir, budget=100, trials=60, starts=64, seed
             for metric, data in zip(METRICS, (times, gaps, allocs, regrets, minobs)):
                 write_to_csv(os.path.join(directory, f"{acq}_{metric}"), data)
             results[(acq, trial)] = dict(times=times, gaps=gaps, simple_regret=regrets, minimum_observations=minobs,
-                                         X=sur.get_active_covariates().copy(), y=sur.get_active_observations().copy())
+                                         X=sur.get_active_covariates().copy(), y=sur.get_active_observations().copy(),
+                                         ell_start=ell_start, ell_end=float(sur.ψ.lengthscale))
     return results
 
 

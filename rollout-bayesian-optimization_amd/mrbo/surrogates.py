@@ -84,7 +84,9 @@ class Surrogate:
         return float(np.min(self.y))
 
     def reset(self, X, y):
-        """reset!(s, X, y) :147-164"""
+        """reset!(s, X, y) :147-164: refit on (X, y) with s's CURRENT kernel (a lengthscale set by
+        an earlier optimize! carries over) and leave the buffers past N as they are (y[N+1:cap]
+        keeps earlier observations, which fmini over the capacity buffer, Q3, then sees)."""
         self._fit(np.asarray(X, dtype=np.float64), np.asarray(y, dtype=np.float64).ravel())
 
     def set_kernel(self, kernel):
@@ -92,10 +94,21 @@ class Surrogate:
         self.ψ = kernel
         self._fit(self.get_active_covariates().copy(), self.get_active_observations().copy())
 
+    def resize(self):
+        """resize(s) :137-145: a NEW surrogate of twice the capacity refit on the whole buffers
+        (get_covariates / get_observations, all `capacity` columns), with s's kernel and rule."""
+        return Surrogate(self.ψ, self.X.copy(), self.y.copy(), capacity=2 * self.capacity, decision_rule=self.g,
+                         σn2=self.σn2)
+
     def condition(self, xnew, ynew):
-        """condition!(s, x, y) :214-222 (rank-1 Cholesky append, full coefficient re-solve)."""
+        """condition!(s, x, y) :214-222 (rank-1 Cholesky append, full coefficient re-solve).
+        Returns the conditioned surrogate, like the reference.  On a full surrogate the reference
+        rebinds its LOCAL `s = resize(s)` (:215) and conditions that new object: the caller's
+        surrogate is left unchanged and the observation reaches only the returned copy (the loops
+        of experiments/*_bayesopt.jl ignore the return value, so past capacity they stop learning).
+        This mirror does the same."""
         if self.observed == self.capacity:
-            raise NotImplementedError("resize(s) beyond capacity (radial_basis_surrogates.jl:137-145)")
+            return self.resize().condition(xnew, ynew)
         n = self.observed
         x = np.asarray(xnew, dtype=np.float64).ravel()
         self.X[:, n] = x

@@ -109,6 +109,49 @@ def test_surrogate_fit_and_condition_match_dense_refit():
     assert s.fmini() == min(0.0, y2.min())  # Q3: zero padding of the capacity buffer
 
 
+def test_surrogate_reuse_semantics_of_the_experiment_loops():
+    """What experiments/*_bayesopt.jl rely on when they reuse one surrogate: reset!(s, X, y)
+    (r_b_s.jl:147-164) refits with the CURRENT kernel and keeps the buffers past N; condition! on a
+    full surrogate (:214-222) rebinds a local `s = resize(s)` (:137-145), so the caller's surrogate
+    is unchanged and only the returned copy holds the new point."""
+    from mrbo import EI, Matern52, Surrogate
+    from mrbo.kernels import set_hyperparameters
+    rng = np.random.default_rng(1)
+    s = Surrogate(Matern52(), np.zeros((2, 1)), np.zeros(1), capacity=6, decision_rule=EI(), σn2=1e-6)
+    X, y = rng.uniform(size=(2, 4)), rng.normal(size=4) + 5.0
+    s.reset(X, y)
+    s.condition(rng.uniform(size=2), -3.0)
+    s.set_kernel(set_hyperparameters(s.ψ, np.array([0.4])))           # what optimize! leaves
+    X2, y2 = rng.uniform(size=(2, 3)), rng.normal(size=3) + 5.0
+    s.reset(X2, y2)
+    assert s.ψ.lengthscale == 0.4 and s.observed == 3
+    assert s.y[4] == -3.0 and s.fmini() == -3.0                         # stale tail seen by Q3
+    s.condition(rng.uniform(size=2), 1.0)
+    s.condition(rng.uniform(size=2), 2.0)
+    s.condition(rng.uniform(size=2), 3.0)
+    assert s.observed == 6 == s.capacity
+    before = (s.X.copy(), s.y.copy(), s.L.copy(), s.c.copy())
+    r = s.condition(rng.uniform(size=2), 4.0)
+    assert r is not s and r.capacity == 12 and r.observed == 7 and r.y[6] == 4.0
+    for a, b in zip(before, (s.X, s.y, s.L, s.c)):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_reference_myopic_runs_show_the_carried_lengthscale():
+    """The evidence behind the myopic loop's reuse_surrogate default: in the
+    reference's recorded Ackley-5 runs (tests/golden/bo_ref_gaps.json, from
+    experiments/myopic/ackley5d/*_gaps.csv) the first trial -- the only one that starts from
+    Matern52()'s ℓ = 1 -- observes the box centre (Ackley's minimiser, the first Sobol start) at
+    once, as the round-3 loop did in every trial, while the later trials, which start from the
+    previous trial's optimised lengthscale, mostly do not."""
+    import json
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "bo_ref_gaps.json")))
+    g = np.array(ref["myopic_ackley5d_ei"]["gaps"])
+    assert ref["myopic_ackley5d_ei"]["budget_labels"][1] == "2"
+    assert g[0, 1] == 1.0 and g[0, 29] == 1.0
+    assert g[1:, 29].mean() < 0.2 and (g[1:, 1] == 1.0).mean() < 0.1
+
+
 def test_trajectory_parameters_contract():
     from mrbo import TrajectoryParameters
     tp = TrajectoryParameters(start=[0.1, 0.2], hypers=[0.0], horizon=2, mc_iterations=8,

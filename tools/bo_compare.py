@@ -38,8 +38,11 @@ FIXTURE = os.path.join(ROOT, "tests", "golden", "bo_ref_gaps.json")
 MYOPIC_FNS = ["braninhoo", "hartmann6d", "ackley5d", "goldsteinprice", "sixhump", "griewank3d", "levy10d"]
 ROLLOUT_FNS = ["braninhoo", "gramacylee", "ackley1d", "ackley2d", "ackley3d", "ackley4d", "rosenbrock", "hartmann3d",
                "sixhump", "goldsteinprice"]
-SETTINGS = {f"myopic_{fn}_{rule}": dict(fn=fn, rule=rule, horizon=0, budget=30, initial=5, starts=64, batch=0,
-                                        labels=["10", "20", "30"])
+# myopic: the reference ran budget 100 with one surrogate of capacity 100 reused over the trials
+# (myopic_bayesopt.jl:205-217); each trial starts from the lengthscale the previous trial's 100th
+# optimize! left, so the loop runs the same 100 steps (run_budget) and compares the first 30 labels
+SETTINGS = {f"myopic_{fn}_{rule}": dict(fn=fn, rule=rule, horizon=0, budget=30, run_budget=100, capacity=100, initial=5,
+                                        starts=64, batch=0, labels=["10", "20", "30"])
             for fn in MYOPIC_FNS for rule in ("ei", "poi", "lcb")}
 SETTINGS.update({f"rollout_h{h}_{fn}": dict(fn=fn, rule="ei", horizon=h, budget=20, initial=1, starts=8, batch=8,
                                             labels=["5", "10", "20"])
@@ -102,6 +105,14 @@ def compare(a, b):
     return out
 
 
+def detected(cmp, alpha=0.05):
+    """Two-sided verdict beside the one-sided assertion: 'none' when the two-sided Mann–Whitney test
+    finds no difference at level alpha, else which side closes more of the gap."""
+    if not cmp["mannwhitney_p"] < alpha:
+        return "none"
+    return "ours closes more" if cmp["diff_mean"] > 0 else "ours closes less"
+
+
 def trajectory_diagnostics(Xs, lbs, ubs, initial):
     """Shape of the BO observation sequences (same statistics as for the reference's archived
     observation CSVs in DESIGN.md §10): the fraction of BO observations with a coordinate on the box
@@ -121,7 +132,7 @@ def trajectory_diagnostics(Xs, lbs, ubs, initial):
             "trials_with_repeats": float(np.mean(rep))}
 
 
-def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incumbent=True):
+def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incumbent=True, reuse=True):
     from mrbo import bayesopt
     s = SETTINGS[key]
     testfn = bayesopt.TESTFNS[s["fn"]]()
@@ -131,13 +142,15 @@ def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incu
         t0 = time.perf_counter()
         lg = lambda *m: log(f"[{key}] " + " ".join(map(str, m)))
         if myopic:
-            res = bayesopt.run_myopic(s["fn"], tmp, budget=s["budget"], trials=trials, starts=s["starts"], seed=seed,
-                                      rules=(s["rule"],), initial_observations=s["initial"], log=lg)
+            rb = s["run_budget"] if reuse else s["budget"]
+            res = bayesopt.run_myopic(s["fn"], tmp, budget=rb, trials=trials, starts=s["starts"], seed=seed,
+                                      rules=(s["rule"],), initial_observations=s["initial"], log=lg,
+                                      reuse_surrogate=reuse, capacity=s["capacity"] if reuse else None)
         else:
             res = bayesopt.run(s["fn"], tmp, budget=s["budget"], trials=trials, starts=s["starts"], horizon=s["horizon"],
                                mc_samples=100, batch_size=s["batch"], sgd_iterations=50, optimize=True, seed=seed,
                                rules=("ei",), initial_observations=s["initial"], solver=solver, eta=eta,
-                               fmini_over_capacity=q3, incumbent=incumbent, log=lg)
+                               fmini_over_capacity=q3, incumbent=incumbent, reuse_surrogate=reuse, log=lg)
         wall = time.perf_counter() - t0
     trials_res = []
     for t in range(trials):
@@ -145,7 +158,7 @@ def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incu
         y = r["y"]
         r = dict(r, initial_best=float(np.min(y[:s["initial"]])))
         trials_res.append(r)
-    gcols = our_gap_columns(trials_res, true_minimum, s["budget"])
+    gcols = our_gap_columns(trials_res, true_minimum, len(trials_res[0]["gaps"]))
     lbs, ubs = testfn.get_bounds()
     diag = trajectory_diagnostics([r["X"] for r in trials_res], lbs, ubs, s["initial"])
     per_label = {lab: compare(our_column(gcols, lab, myopic), ref_column(case, lab)) for lab in s["labels"]}
@@ -155,8 +168,13 @@ def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incu
     return {"case": key, "reference": case["source"], "settings": dict(s, trials=trials, mc_samples=100,
                                                                         sgd_iterations=50, optimize=True, solver=solver,
                                                                         eta=eta, seed=seed, q3_fmini_over_capacity=q3,
-                                                                        incumbent_restart=incumbent),
-            "gaps": per_label, "ours_trajectory_diagnostics": diag, "ours_mean_curve": gcols.mean(axis=0).tolist(),
+                                                                        incumbent_restart=incumbent,
+                                                                        reuse_surrogate=reuse),
+            "gaps": per_label, "difference_detected": {lab: detected(v) for lab, v in per_label.items()},
+            "ours_lengthscale": {"start_median": float(np.median([r["ell_start"] for r in trials_res])),
+                                 "end_median": float(np.median([r["ell_end"] for r in trials_res])),
+                                 "start_first_trials": [r["ell_start"] for r in trials_res[:5]]},
+            "ours_trajectory_diagnostics": diag, "ours_mean_curve": gcols.mean(axis=0).tolist(),
             "seconds_per_solve": {"ours_median": float(np.median(our_times)), "ref_median": float(np.median(ref_times)),
                                   "ref_note": "reference times from earlier code versions on unstated hardware"},
             "wall_s": wall}
@@ -174,6 +192,9 @@ def main():
                          "for adam)")
     ap.add_argument("--no-q3", action="store_true",
                     help="diagnostic: fmini over the observed points instead of the zero-padded buffer (Q3 off)")
+    ap.add_argument("--no-reuse", action="store_true",
+                    help="diagnostic: a fresh surrogate (ℓ = 1) per trial instead of the reference's one reused "
+                         "surrogate whose lengthscale carries over between trials (the round-3 loops)")
     ap.add_argument("--no-incumbent", action="store_true",
                     help="diagnostic: the round-2 solver (no incumbent restart, no no-repeat pick)")
     a = ap.parse_args()
@@ -181,7 +202,8 @@ def main():
     log = lambda m: print(m, file=sys.stderr, flush=True)
     for key in (ASSERTED if a.cases == "asserted" else a.cases.split(",")):
         eta = a.eta or (0.01 if a.solver == "sga" else 0.02)
-        row = run_case(key, ref[key], a.trials, a.seed, log, solver=a.solver, eta=eta, q3=not a.no_q3, incumbent=not a.no_incumbent)
+        row = run_case(key, ref[key], a.trials, a.seed, log, solver=a.solver, eta=eta, q3=not a.no_q3, incumbent=not a.no_incumbent,
+                       reuse=not a.no_reuse)
         line = json.dumps(row)
         print(line, flush=True)
         if a.out:
@@ -190,7 +212,7 @@ def main():
         g = row["gaps"][SETTINGS[key]["labels"][-1]]
         log(f"{key} [{a.solver}{'' if not a.no_q3 else ', Q3 off'}{'' if not a.no_incumbent else ', no incumbent'}]: final gap ours {g['ours_mean']:.3f}±{g['ours_se']:.3f} ref {g['ref_mean']:.3f}±{g['ref_se']:.3f} "
             f"diff {g['diff_mean']:+.3f} [{g['diff_ci95'][0]:+.3f}, {g['diff_ci95'][1]:+.3f}] "
-            f"MW p={g['mannwhitney_p']:.3f}; s/solve ours {row['seconds_per_solve']['ours_median']:.3f} "
+            f"MW p={g['mannwhitney_p']:.3f} ({row['difference_detected'][SETTINGS[key]['labels'][-1]]}); s/solve ours {row['seconds_per_solve']['ours_median']:.3f} "
             f"ref {row['seconds_per_solve']['ref_median']:.2f}; diag {row['ours_trajectory_diagnostics']}")
 
 
