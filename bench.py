@@ -138,6 +138,13 @@ def cpu_baseline(pb, M_full, R_full, budget_s, cost=None):
                       nthreads=nt, want_policy=False, cost=cost)
         return time.perf_counter() - t
 
+    def bounded(nt, seconds):
+        """trajectories/s of nt threads over a sample of about `seconds` of this leg's work"""
+        m = min(M_full, max(nt * 4, 32))
+        t = run(m, 1, nt)
+        m = min(M_full, max(m, int(m / t * seconds)))
+        return m, run(m, 1, nt)
+
     Ms = min(M_full, max(nthreads * 4, 32))
     dt = run(Ms, 1, nthreads)
     rate = Ms / dt
@@ -150,13 +157,27 @@ def cpu_baseline(pb, M_full, R_full, budget_s, cost=None):
     dt1 = run(M1, 1, 1)
     M1 = min(M_full, max(M1, int(M1 / dt1 * budget_s * 0.3)))
     dt1 = run(M1, 1, 1)
+    # every CPU of this process's affinity set, whatever OMP_NUM_THREADS says
+    # (it only sets the default; nthreads is passed to omp_set_num_threads for this leg alone)
+    Ma, dta = bounded(aff, 3.0)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     O.use_library(None)
     return dict(value=Ms * Rs / dt, unit="trajectories/s", cores=nthreads, kind="port",
                 sample=f"{pb.cfg.name} workload, first {Rs} restart(s) x {Ms} MC samples "
                        f"({Ms * Rs} trajectories, {dt:.1f} s), oracle/rbo_oracle.c OpenMP x{nthreads}",
                 build=flags, host_cpus=os.cpu_count(), affinity_cpus=aff, reference=julia_probe(),
                 single_thread={"value": M1 / dt1, "cores": 1,
-                               "sample": f"first restart x {M1} MC samples ({dt1:.1f} s), 1 thread"})
+                               "sample": f"first restart x {M1} MC samples ({dt1:.1f} s), 1 thread"},
+                all_cores={"value": Ma / dta, "cores": aff,
+                           "sample": f"first restart x {Ma} MC samples ({dta:.1f} s), {aff} threads = the "
+                                     f"process's whole affinity set",
+                           "cgroup_cpu_quota": quota})
 
 
 def main():
@@ -176,7 +197,6 @@ def main():
     from mrbo import configs, flops, parallel
     from mrbo.engine import from_device, to_device
     from mrbo.rollout import _plan_for
-    from mrbo.utils import sga_step_batch
 
     # one process per GPU; MRBO_DIST_BACKEND=gloo + device wrap-around only for rehearsing the
     # multi-rank path on a box with fewer GPUs than ranks
@@ -216,32 +236,23 @@ def main():
     dev = f"cuda:{local}"
     drn = to_device(np.asfortranarray(pb.tp.rnstream_sequence[lo:hi]), dev)   # resident in HBM
     dxs = to_device(pb.es.get_starts(), dev)
-    x0 = np.array(pb.x0s, dtype=np.float64)
-    dx0 = to_device(x0, dev)
+    dx0 = to_device(np.array(pb.x0s, dtype=np.float64), dev)
     out = plan.alloc_outputs(with_gradient=True)
     evals_acc = torch.zeros_like(out["evals"])
-    active = np.ones(R, dtype=bool)
     dactive = torch.ones(R, dtype=torch.int32, device=dev)
     W = parallel.width(d)
-    kernel_ms = []
-    events = []
     last = {}
-    stream = torch.cuda.current_stream(local)
 
-    def step(timed):
-        if sharded:
-            dx0.copy_(torch.from_numpy(x0.ravel(order="F")), non_blocking=False)
-        if timed:   # HIP events on the launch stream around the rollout launch, read after the loop
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record(stream)
-        plan.simulate(dx0, drn, dxs, out)
-        if timed:
-            ev[1].record(stream)
-            events.append(ev)
+    shard_sizes = [b - a for a, b in shards]
+
+    def step():
+        plan.simulate(dx0, drn, dxs, out)   # the library records HIP events around the rollout kernel
         if not sharded:
             e = plan.eto(out)                           # two-pass mean / std(n-1) on the device
         else:
-            e = plan.partial_moments(out, hi - lo)     # this shard's (Σ, M2) rows
+            # this shard's (Σ, M2) rows, ONE all-gather of the device tensors, Chan merge + ETO on
+            # the device (mrbo_merge_moments): the same host profile as the one-GPU step
+            e = parallel.sharded_eto_device(plan, plan.partial_moments(out, hi - lo), shard_sizes)
         evals_acc.add_(out["evals"])        # also in warmup: no first-use op inside the timed region
         if longest_first and "ordered" not in last:
             # the schedule of every later step, from this (first) step's work counters: an SGA step
@@ -249,19 +260,13 @@ def main():
             # re-sorting every step costs more (≈ 0.09 ms at C2) than it gains
             plan.order_longest_first(out)
             last["ordered"] = True
-        if not sharded:
-            # eswavs + StandardSGA of every active restart on the device (mrbo_sga_step): x0 and the
-            # stop flags stay in HBM, so the next launch follows without a host round trip
-            plan.sga_step(e, dx0, dactive, M_total, args.eta)
-            last["eto_dev"] = e
-        else:
-            eto = parallel.sharded_eto(e, [b - a for a, b in shards], d)
-            last["eto"] = eto
-            # eswavs + StandardSGA of every active restart at once (utils.jl:114-123, optimizers.jl:16-22)
-            sga_step_batch(x0, active, eto[2:2 + d], eto[2 + d:2 + 2 * d], M_total, args.eta)
+        # eswavs + StandardSGA of every active restart on the device (mrbo_sga_step): x0 and the
+        # stop flags stay in HBM, so the next launch follows without a host round trip
+        plan.sga_step(e, dx0, dactive, M_total, args.eta)
+        last["eto_dev"] = e
 
     for _ in range(args.warmup):
-        step(False)
+        step()
     evals_acc.zero_()
     torch.cuda.synchronize()
     if sharded:
@@ -269,7 +274,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        step()
     torch.cuda.synchronize()
     if sharded:
         dist.barrier()
@@ -279,11 +284,11 @@ def main():
     if sharded:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    kernel_ms = [a.elapsed_time(b) for a, b in events]
-    if not sharded:
-        last["eto"] = last["eto_dev"].cpu().numpy().reshape((W, R), order="F")
-        x0 = from_device(dx0, (d, R))
-        active = dactive.cpu().numpy().astype(bool)
+    # HIP events around each timed step's rollout kernel alone, on its launch stream (mrbo_kernel_times)
+    kernel_ms = plan.kernel_times(args.steps) if args.steps > 0 else []
+    last["eto"] = last["eto_dev"].cpu().numpy().reshape((W, R), order="F")
+    x0 = from_device(dx0, (d, R))
+    active = dactive.cpu().numpy().astype(bool)
 
     st = out["status"].cpu().numpy()
     ev = evals_acc.cpu().numpy().reshape((flops.NCOUNTERS, hi - lo, R), order="F") / max(args.steps, 1)

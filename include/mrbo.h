@@ -197,6 +197,16 @@ int mrbo_sga_step(mrbo_plan_t* plan, const double* eto, double* x0s, int32_t* ac
 int mrbo_partial_moments(mrbo_plan_t* plan, const double* values, const double* grad_x, const double* grad_theta,
                          int32_t M_local, double* moments, uint32_t flags, void* stream);
 
+/* The exchange's merge on the device (no host round trip per SGA step): moments = the nshards
+ * ranks' mrbo_partial_moments blocks concatenated in rank order (nshards × R×W, what one
+ * all-gather of the flat blocks produces), counts = their sample counts (HOST int64[nshards],
+ * the shard sizes every rank knows; 1 ≤ nshards ≤ 64, a zero-count shard is skipped).  Chan's
+ * pairwise merge left to right, then the ETO rows (mrbo_eto_reduce's layout, std n−1, Q14) into
+ * eto (device, R×W) -- the same operations in the same order as mrbo/parallel.py merge_moments +
+ * eto_from_moments.  Device pointers only; asynchronous on `stream`.                       */
+int mrbo_merge_moments(mrbo_plan_t* plan, int32_t nshards, const double* moments, const int64_t* counts, double* eto,
+                       uint32_t flags, void* stream);
+
 /* eval(s, x, θ) of the base surrogate at P points xs (d×P); out stride 3+4d+d²:
  * [μ, σ, α, ∇μ(d), ∇σ(d), ∇α(d), Hα(d×d col-major), d2α/dxdθ(d)].                       */
 int mrbo_eval_base(mrbo_plan_t* plan, int32_t P, const double* xs, double* out, uint32_t flags, void* stream);
@@ -238,8 +248,13 @@ int mrbo_rnstream(int32_t M, int32_t d, int32_t H, double* out);                
 int mrbo_initial_guesses(int32_t n, int32_t d, const double* lbs, const double* ubs, double* out); /* d×(n+2) */
 double mrbo_dual_uniform(uint64_t seed, int64_t traj, int32_t j, int32_t k);
 
-/* Timing of the last mrbo_simulate_mc kernel on its stream (HIP events), milliseconds. */
+/* Timing of the last mrbo_simulate_mc / _ghq rollout kernel on its stream (HIP events around the
+ * kernel launch alone), milliseconds; -1 before the first launch.  Waits for that launch.      */
 double mrbo_last_kernel_ms(mrbo_plan_t* plan);
+
+/* The same for the plan's last min(n, launches, 64) launches, oldest first, into ms[]; returns the
+ * number written (≥ 0) or a negative mrbo_err_t.  Waits for those launches.                    */
+int mrbo_kernel_times(mrbo_plan_t* plan, int32_t n, double* ms);
 
 /* Kernel time of the last mrbo_gp_fit launch (HIP events around it), milliseconds; -1 before
  * the first call.  Process-wide (the last call on any stream). */
@@ -257,7 +272,10 @@ int mrbo_plan_info(const mrbo_plan_t* plan, int32_t* info, int32_t n);
  * tail.  Caller-owned; it must stay valid while launches use it.  NULL restores the identity.
  * n != M×R: MRBO_ERR_ARG.  An entry outside [0, M×R) runs the trajectory of its own queue index
  * (no write outside the outputs); tests/test_gpu_schedule.py holds every output bit-identical
- * under permuted, out-of-range and longest-first orders. */
+ * under permuted, out-of-range and longest-first orders.  The library does not check that the
+ * order is a permutation: with a duplicated index (or a mix of out-of-range entries and valid
+ * ones that name the same trajectory) one trajectory runs on two waves at once and another never
+ * runs -- its outputs are left undefined.  The Python mirror (RolloutPlan.set_order) checks. */
 int mrbo_plan_set_order(mrbo_plan_t* plan, const int32_t* order, int64_t n);
 
 #ifdef __cplusplus

@@ -73,8 +73,11 @@ struct mrbo_plan {
   int batch = 0;            // batched start-point values (start tables in LDS)
   int ewpg = 4, eblocks = 0;
   size_t esmem = 0;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool timed = false;
+  // HIP events around every rollout kernel launch (the kernel alone: after the queue memset and
+  // the packed layouts' start-table kernel), a ring of the last NEV launches (mrbo_kernel_times)
+  static constexpr int NEV = 64;
+  hipEvent_t ev[2 * NEV] = {};
+  long long nlaunch = 0;
   // MRBO_FLAG_HOST_POINTERS staging: device buffers kept across calls, one slot per staged
   // argument in call order, grown on demand and freed with the plan
   std::vector<std::pair<void*, size_t>> stage;
@@ -227,6 +230,43 @@ __global__ void __launch_bounds__(64) sga_kernel(const double* eto, double* x0s,
   for (int a = 0; a < d; ++a) x0s[(size_t)d * r + a] = x0s[(size_t)d * r + a] + eta * e[2 + a];
 }
 
+// ---- multi-GPU exchange on the device: Chan merge of the all-gathered shard moments ---------
+// One thread per (restart r, component c of [α, ∇x (d), ∇θ]): the shards' (Σ, M2) are merged
+// left to right in rank order with Chan et al.'s pairwise formula and turned into the ETO row
+// (mean, std(n−1), rollout.jl:328-339) -- the same operations, in the same order and without
+// contraction, as mrbo/parallel.py merge_moments + eto_from_moments.
+constexpr int MERGE_MAX_SHARDS = 64;
+struct MergeCounts { long long n[MERGE_MAX_SHARDS]; };
+
+__global__ void __launch_bounds__(64) merge_kernel(const double* moments, int nshards, MergeCounts cnt, int R, int d,
+                                                   double* eto) {
+#pragma clang fp contract(off)
+  const int W = 2 + 2 * d + 2;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= R * (d + 2)) return;
+  const int r = idx / (d + 2), comp = idx % (d + 2);
+  int c0, c1;
+  if (comp == 0) { c0 = 0; c1 = 1; }
+  else if (comp <= d) { c0 = 2 + (comp - 1); c1 = 2 + d + (comp - 1); }
+  else { c0 = 2 + 2 * d; c1 = 3 + 2 * d; }
+  double n = 0.0, sm = 0.0, q = 0.0;
+  bool any = false;
+  for (int k = 0; k < nshards; ++k) {
+    const double nk = (double)cnt.n[k];
+    if (cnt.n[k] == 0) continue;
+    const double* blk = moments + (size_t)k * W * R + (size_t)W * r;
+    const double sk = blk[c0], qk = blk[c1];
+    if (!any) { n = nk; sm = sk; q = qk; any = true; continue; }
+    const double delta = sk / nk - sm / n;
+    q = q + qk + delta * delta * (n * nk / (n + nk));
+    sm = sm + sk;
+    n = n + nk;
+  }
+  double* e = eto + (size_t)W * r;
+  e[c0] = sm / n;
+  e[c1] = n > 1.0 ? sqrt(q / (n - 1.0)) : __builtin_nan("");
+}
+
 // ---- host Sobol (Joe-Kuo directions, Gray code, zero point skipped) ---------------------
 struct Sobol {
   int dim;
@@ -337,6 +377,8 @@ struct Stage {
   size_t k = 0;
   explicit Stage(mrbo_plan_t* plan = nullptr) : P(plan) {}
   ~Stage() { for (auto& b : own) if (b.first) pool_give(b.first, b.second); }
+  // a launch that may still be running after an error: keep its buffers out of the pool (leaked)
+  void abandon() { own.clear(); }
   void* slot(size_t bytes) {
     if (!P) {
       own.push_back(pool_take(bytes));
@@ -591,8 +633,8 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
        hipMemcpy(P->dLinv, packed.data(), sizeof(double) * packed.size(), hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(P->dlbs, P->lbs.data(), sizeof(double) * d, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(P->dubs, P->ubs.data(), sizeof(double) * d, hipMemcpyHostToDevice) == hipSuccess &&
-       hipMemset(P->dwork, 0, sizeof(double) * (size_t)slots * P->work_stride) == hipSuccess &&
-       hipEventCreate(&P->ev0) == hipSuccess && hipEventCreate(&P->ev1) == hipSuccess;
+       hipMemset(P->dwork, 0, sizeof(double) * (size_t)slots * P->work_stride) == hipSuccess;
+  for (int k = 0; ok && k < 2 * mrbo_plan::NEV; ++k) ok = hipEventCreate(&P->ev[k]) == hipSuccess;
   if (!ok) {
     mrbo_plan_destroy(P);
     return fail(MRBO_ERR_NOMEM, "device allocation failed");
@@ -608,8 +650,8 @@ int mrbo_plan_destroy(mrbo_plan_t* P) {
     if (b) (void)hipFree(b);
   for (auto& b : P->stage)
     if (b.first) (void)hipFree(b.first);
-  if (P->ev0) (void)hipEventDestroy(P->ev0);
-  if (P->ev1) (void)hipEventDestroy(P->ev1);
+  for (hipEvent_t e : P->ev)
+    if (e) (void)hipEventDestroy(e);
   delete P;
   return MRBO_OK;
 }
@@ -662,7 +704,6 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
   HIP_TRY(hipMemsetAsync(dstamps, 0, sizeof(unsigned long long) * NSTAMP_SLOTS, st));
   kp.stamps = dstamps;
 #endif
-  HIP_TRY(hipEventRecord(P->ev0, st));
   kp.xs_lds = P->xs_lds;
   kp.batch = P->batch;
   if (P->batch && P->RPL > 1) {   // packed layouts: global start tables for this launch's xstarts
@@ -671,10 +712,12 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
     launch_tables(d, P->RPL, P->fx, P->p.nstarts, st, kp);
     HIP_TRY(hipGetLastError());
   }
+  const int slot = (int)(P->nlaunch % mrbo_plan::NEV);
+  HIP_TRY(hipEventRecord(P->ev[2 * slot], st));
   launch_rollout(d, P->RPL, P->fx, P->spec, dim3(P->blocks), dim3(P->wpg * WAVE), P->smem, st, kp);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(P->ev1, st));
-  P->timed = true;
+  HIP_TRY(hipEventRecord(P->ev[2 * slot + 1], st));
+  ++P->nlaunch;
 #ifdef MRBO_STAMPS
   {
     // region names follow the STAMP(W, k) sites in mrbo_rollout.hip
@@ -751,6 +794,28 @@ int mrbo_sga_step(mrbo_plan_t* P, const double* eto, double* x0s, int32_t* activ
   const int R = P->p.R;
   hipLaunchKernelGGL(sga_kernel, dim3((R + 63) / 64), dim3(64), 0, (hipStream_t)stream, eto, x0s, (int*)active, R, P->d,
                      sample_size, eta);
+  HIP_TRY(hipGetLastError());
+  return MRBO_OK;
+}
+
+int mrbo_merge_moments(mrbo_plan_t* P, int32_t nshards, const double* moments, const int64_t* counts, double* eto,
+                       uint32_t flags, void* stream) {
+  if (!P || !moments || !counts || !eto) return fail(MRBO_ERR_ARG, "null argument");
+  if (flags & MRBO_FLAG_HOST_POINTERS) return fail(MRBO_ERR_ARG, "mrbo_merge_moments takes device moments / eto");
+  if (nshards < 1 || nshards > MERGE_MAX_SHARDS)
+    return fail(MRBO_ERR_ARG, "nshards=%d outside [1, %d]", nshards, MERGE_MAX_SHARDS);
+  MergeCounts cnt{};
+  long long tot = 0;
+  for (int k = 0; k < nshards; ++k) {
+    if (counts[k] < 0) return fail(MRBO_ERR_ARG, "negative shard count %lld", (long long)counts[k]);
+    cnt.n[k] = counts[k];
+    tot += counts[k];
+  }
+  if (tot < 1) return fail(MRBO_ERR_ARG, "no samples in any shard");
+  if (hipSetDevice(P->device) != hipSuccess) return fail(MRBO_ERR_HIP, "hipSetDevice");
+  const int R = P->p.R, d = P->d, nthr = R * (d + 2);
+  hipLaunchKernelGGL(merge_kernel, dim3((nthr + 63) / 64), dim3(64), 0, (hipStream_t)stream, moments, (int)nshards, cnt,
+                     R, d, eto);
   HIP_TRY(hipGetLastError());
   return MRBO_OK;
 }
@@ -855,6 +920,15 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
   const double *dX = nullptr, *dy = nullptr;
   if (sg.in(s->X, (size_t)d * N, &dX) || sg.in(s->y, (size_t)N, &dy)) return fail(MRBO_ERR_NOMEM, "staging X, y");
   GpFitParams q{d, N, s->kernel, s->sigma_n2, dX, dy, nt, dth, s->period, dll_, dgr, (int*)dst, dL, dc, nullptr};
+  {
+    int dev = 0, lds_max = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    HIP_TRY(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+    const size_t need = gpfit_launch_lds(q);
+    if (need > (size_t)lds_max)
+      return fail(MRBO_ERR_UNSUPPORTED, "gp_fit: d=%d N=%d needs %zu B of LDS per workgroup, the device has %d", d, N,
+                  need, lds_max);
+  }
   if (!gpfit_in_regs(q) && !gpfit_in_lds(q)) {   // the register (N ≤ 64) and LDS (N ≤ 80) kernels need none
     q.work = (double*)sg.slot(sizeof(double) * gpfit_tile_work_doubles(N) * P);
     if (!q.work) return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
@@ -881,10 +955,20 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
   }
   HIP_TRY(hipEventRecord(gev[0], st));
   launch_gpfit(np, st, q);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(gev[1], st));
-  // the staging buffers and the workspace go back to the pool on return: finish the launch first
-  HIP_TRY(hipStreamSynchronize(st));
+  // the staging buffers and the workspace go back to the pool on return: once the launch is
+  // issued, every path synchronises the stream first (an error after the launch must not hand
+  // memory a running kernel still uses to another call), and keeps them out of the pool when
+  // even that fails
+  {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipEventRecord(gev[1], st);
+    const hipError_t es = hipStreamSynchronize(st);
+    if (es != hipSuccess) {
+      sg.abandon();
+      return fail(MRBO_ERR_HIP, "gp_fit: hipStreamSynchronize: %s", hipGetErrorString(es));
+    }
+    if (e != hipSuccess) return fail(MRBO_ERR_HIP, "gp_fit launch: %s", hipGetErrorString(e));
+  }
   {
     float ms = -1.f;
     if (hipEventElapsedTime(&ms, gev[0], gev[1]) == hipSuccess) g_gpfit_ms = ms;
@@ -920,12 +1004,27 @@ int mrbo_plan_info(const mrbo_plan_t* P, int32_t* info, int32_t n) {
   return MRBO_OK;
 }
 
-double mrbo_last_kernel_ms(mrbo_plan_t* P) {
-  if (!P || !P->timed) return -1.0;
+static double launch_ms(mrbo_plan_t* P, long long launch) {
+  const int slot = (int)(launch % mrbo_plan::NEV);
   float ms = -1.f;
-  if (hipEventSynchronize(P->ev1) != hipSuccess) return -1.0;
-  if (hipEventElapsedTime(&ms, P->ev0, P->ev1) != hipSuccess) return -1.0;
+  if (hipEventSynchronize(P->ev[2 * slot + 1]) != hipSuccess) return -1.0;
+  if (hipEventElapsedTime(&ms, P->ev[2 * slot], P->ev[2 * slot + 1]) != hipSuccess) return -1.0;
   return ms;
+}
+
+double mrbo_last_kernel_ms(mrbo_plan_t* P) {
+  if (!P || P->nlaunch == 0) return -1.0;
+  return launch_ms(P, P->nlaunch - 1);
+}
+
+int mrbo_kernel_times(mrbo_plan_t* P, int32_t n, double* ms) {
+  if (!P || !ms || n < 0) return fail(MRBO_ERR_ARG, "bad arguments");
+  const long long k = std::min<long long>({(long long)n, P->nlaunch, (long long)mrbo_plan::NEV});
+  for (long long i = 0; i < k; ++i) {
+    ms[i] = launch_ms(P, P->nlaunch - k + i);
+    if (ms[i] < 0) return fail(MRBO_ERR_HIP, "hipEventElapsedTime");
+  }
+  return (int)k;
 }
 
 // utils.jl:4-74 -- Sobol uniforms → Box–Muller with log10 (Q1) → column-major reshape (Q2)

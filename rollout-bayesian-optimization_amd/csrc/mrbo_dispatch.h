@@ -73,6 +73,9 @@ struct GpFitParams {
 };
 // MRBO_GPFIT_LDS_MAX < N ≤ 512: gpfit_tile_kernel's workspace per candidate
 size_t gpfit_tile_work_doubles(int N);
+// LDS bytes per workgroup of the kernel launch_gpfit selects for q (the tile kernel stages X:
+// d·⌈N/32⌉·32 doubles, so large d can exceed the CU's 160 KB)
+size_t gpfit_launch_lds(const GpFitParams& q);
 void launch_gpfit(int P, hipStream_t st, const GpFitParams& q);
 // N ≤ 64, d ≤ 16 and no factor / coefficient outputs: the one-wave-per-candidate register kernel
 // (no workspace)

@@ -966,6 +966,12 @@ size_t gpfit_lds_bytes() { return sizeof(double) * ((size_t)GL_N * GL_LD + 16 * 
 
 size_t gpfit_reg_lds(int nt) { return sizeof(double) * ((size_t)(1 + nt) * 64 * GR_LD + 64 + 16 * 64); }
 
+size_t gpfit_launch_lds(const GpFitParams& q) {
+  if (gpfit_in_regs(q)) return gpfit_reg_lds(q.nt);
+  if (gpfit_in_lds(q)) return gpfit_lds_bytes();
+  return gpfit_tile_lds(q.d, q.N);
+}
+
 void launch_gpfit(int P, hipStream_t st, const GpFitParams& q) {
   if (gpfit_in_regs(q)) {
     if (q.nt == 2)

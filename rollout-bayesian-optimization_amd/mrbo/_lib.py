@@ -35,6 +35,7 @@ EXPORTS = [
     "mrbo_simulate_mc", "mrbo_simulate_ghq", "mrbo_eto_reduce", "mrbo_partial_moments", "mrbo_eval_base", "mrbo_rnstream",
     "mrbo_initial_guesses", "mrbo_dual_uniform", "mrbo_last_kernel_ms", "mrbo_gp_fit", "mrbo_gp_fit_theta",
     "mrbo_plan_info", "mrbo_last_gp_fit_ms", "mrbo_plan_set_order", "mrbo_base_solve", "mrbo_sga_step",
+    "mrbo_kernel_times", "mrbo_merge_moments",
 ]
 
 
@@ -100,6 +101,9 @@ def load():
     L.mrbo_last_kernel_ms.argtypes = [_vp]
     L.mrbo_last_kernel_ms.restype = ctypes.c_double
     L.mrbo_plan_info.argtypes = [_vp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]
+    L.mrbo_kernel_times.argtypes = [_vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]
+    L.mrbo_merge_moments.argtypes = [_vp, ctypes.c_int32, _vp, ctypes.POINTER(ctypes.c_int64), _vp, ctypes.c_uint32,
+                                     _vp]
     L.mrbo_plan_set_order.argtypes = [_vp, _vp, ctypes.c_int64]
     L.mrbo_last_gp_fit_ms.restype = ctypes.c_double
     _lib = L

@@ -144,6 +144,22 @@ class RolloutPlan:
                                               ctypes.c_void_p(st.cuda_stream)))
         return e
 
+    def merge_moments(self, gathered, counts, stream=None):
+        """mrbo_merge_moments: gathered = the ranks' partial_moments blocks concatenated in rank
+        order (one flat device tensor of len(counts)·W·R), counts = their sample counts; returns
+        the merged ETO rows (device tensor, eto()'s layout)."""
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        W = 2 + 2 * self.d + 2
+        n = len(counts)
+        if gathered.numel() != n * W * self.R or not gathered.is_cuda:
+            raise ValueError(f"gathered must be a device tensor of {n}·{W}·{self.R} moments")
+        e = torch.empty(W * self.R, dtype=torch.float64, device=f"cuda:{self.device}")
+        c = (ctypes.c_int64 * n)(*[int(k) for k in counts])
+        _lib.check(self.lib.mrbo_merge_moments(self.handle, n, ctypes.c_void_p(gathered.data_ptr()), c,
+                                               ctypes.c_void_p(e.data_ptr()), 0, ctypes.c_void_p(st.cuda_stream)))
+        return e
+
     def sga_step(self, eto, x0s, active, sample_size, eta, stream=None):
         """mrbo_sga_step: eswavs + StandardSGA for every active restart, in place on the device
         tensors x0s (d·R, column-major) and active (R, int32); eto from `eto()`."""
@@ -170,13 +186,24 @@ class RolloutPlan:
     def last_kernel_ms(self):
         return self.lib.mrbo_last_kernel_ms(self.handle)
 
+    def kernel_times(self, n):
+        """mrbo_kernel_times: HIP-event durations (ms) of the rollout kernel alone in the plan's
+        last min(n, launches, 64) mrbo_simulate_mc / _ghq launches, oldest first (waits for them)."""
+        buf = (ctypes.c_double * max(int(n), 1))()
+        k = self.lib.mrbo_kernel_times(self.handle, int(n), buf)
+        _lib.check(min(k, 0))
+        return [buf[i] for i in range(k)]
+
     # relative cost of one unit of each work counter (grad, value, hess, rich, pairs), in value
     # evaluations -- only the ORDER of the work depends on these, never a result
     ORDER_WEIGHTS = (2.5, 1.0, 3.0, 5.0, 3.0)
 
-    def set_order(self, order):
+    def set_order(self, order, check=True):
         """mrbo_plan_set_order: an int32 device tensor holding a permutation of the M×R trajectory
-        indices (m + M·r), or None for the identity.  The plan keeps a reference."""
+        indices (m + M·r), or None for the identity.  The plan keeps a reference.  check=True
+        refuses anything but a permutation (a duplicated index would run one trajectory on two waves
+        at once and leave another unrun, its outputs undefined); check=False passes any order of the
+        right length to the library (tests: the all-out-of-range guard)."""
         if order is None:
             _lib.check(self.lib.mrbo_plan_set_order(self.handle, None, 0))
             self._order = None
@@ -184,6 +211,9 @@ class RolloutPlan:
         torch = _torch()
         if order.dtype != torch.int32 or not order.is_cuda or order.numel() != self.M * self.R:
             raise ValueError("order must be an int32 device tensor of M*R trajectory indices")
+        if check and not torch.equal(torch.sort(order.to(torch.int64)).values,
+                                     torch.arange(order.numel(), dtype=torch.int64, device=order.device)):
+            raise ValueError("order is not a permutation of 0..M*R-1")
         self._order = order.contiguous()
         _lib.check(self.lib.mrbo_plan_set_order(self.handle, ctypes.c_void_p(self._order.data_ptr()),
                                                 self._order.numel()))

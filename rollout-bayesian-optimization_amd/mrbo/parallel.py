@@ -102,6 +102,32 @@ def allgather_moments(moments_tensor, group=None):
     return outs
 
 
+def allgather_moments_device(moments_tensor, group=None):
+    """ONE all-gather of every rank's flat (W·R) device moments into one flat device tensor, rank
+    order (RCCL gathers device tensors in place; gloo, the CPU rehearsal backend, goes through host
+    memory and the result is copied back to the device)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return moments_tensor
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "gloo":
+        outs = [torch.empty_like(moments_tensor, device="cpu") for _ in range(world)]
+        dist.all_gather(outs, moments_tensor.cpu(), group=group)
+        return torch.cat(outs).to(moments_tensor.device)
+    out = torch.empty(world * moments_tensor.numel(), dtype=moments_tensor.dtype, device=moments_tensor.device)
+    dist.all_gather_into_tensor(out, moments_tensor, group=group)
+    return out
+
+
+def sharded_eto_device(plan, moments_tensor, shard_sizes, group=None):
+    """The per-SGA-step exchange kept on the device: all-gather (device tensors) + Chan merge and
+    ETO in mrbo_merge_moments.  Returns the ETO rows as a device tensor (plan.eto()'s layout), for
+    plan.sga_step -- the same host profile as the one-GPU step (no .cpu() per step)."""
+    gathered = allgather_moments_device(moments_tensor, group)
+    return plan.merge_moments(gathered, shard_sizes)
+
+
 def sharded_eto(moments_tensor, shard_sizes, d, group=None):
     """all-gather + Chan merge + ETO: the per-SGA-step exchange of the sharded rollout."""
     gathered = allgather_moments(moments_tensor, group)

@@ -138,6 +138,42 @@ def test_device_moments_merge_equals_eto_reduce(gpu):
     np.testing.assert_allclose(mom[2:2 + d], gx.sum(1), rtol=1e-10, atol=1e-14)
 
 
+def test_merge_moments_on_device_equals_host_merge(gpu):
+    """mrbo_merge_moments (the exchange's Chan merge + ETO on the device) equals the host
+    restatement mrbo/parallel.py merge_moments + eto_from_moments bit for bit: same operations, same
+    order, no contraction.  Shards of unequal size, one empty shard, mean ≫ spread (the case a
+    one-pass formula loses), and the one-sample NaN std (Q14)."""
+    import torch
+    from mrbo import configs
+    from mrbo.parallel import eto_from_moments, local_moments, merge_moments, width
+    from mrbo.rollout import _plan_for
+    cfg = configs.CONFIGS["C2"]
+    pb = configs.problem("C2", M=16, R=3)
+    d, R = cfg.d, 3
+    plan = _plan_for(pb.T.s, cfg.h, 16, R, pb.es.get_starts().shape[1], pb.lbs, pb.ubs, pb.T.θ[0], 0, pb.plan_opts())
+    rng = np.random.default_rng(3)
+    for sizes in ([5, 0, 11, 3], [1], [7, 9]):
+        parts = []
+        for n in sizes:
+            if n == 0:
+                parts.append((0, np.full((width(d), R), np.nan)))     # never read
+                continue
+            v = 1e6 + rng.normal(size=(n, R))
+            gx = rng.normal(size=(d, n, R)) * 1e-3 + 5.0
+            gt = rng.normal(size=(n, R))
+            parts.append((n, local_moments(v, gx, gt)))
+        ntot, merged = merge_moments(parts, d)
+        host = eto_from_moments(merged, ntot, d)
+        flat = np.concatenate([b.ravel(order="F") for _, b in parts])
+        dev = plan.merge_moments(torch.from_numpy(flat).to("cuda:0"), [n for n, _ in parts])
+        torch.cuda.synchronize()
+        got = dev.cpu().numpy().reshape((width(d), R), order="F")
+        np.testing.assert_array_equal(np.isnan(got), np.isnan(host))
+        np.testing.assert_array_equal(got[~np.isnan(got)], host[~np.isnan(host)])
+    with pytest.raises(Exception):
+        plan.merge_moments(torch.zeros(width(d) * R, dtype=torch.float64, device="cuda:0"), [0])
+
+
 def _bench(args, env):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
                        timeout=110, env=env, cwd=ROOT)
@@ -147,9 +183,10 @@ def _bench(args, env):
 
 def test_bench_sharded_rccl_one_rank_matches_plain(gpu, tmp_path):
     """`bench.py --sharded` at one rank runs the multi-rank path over RCCL (backend nccl: a
-    process group, the per-step all-gather of the shard moments on device tensors, the host Chan
-    merge and SGA step, the MAX all-reduce of the clock) -- the exchange the 8-GPU run uses, on
-    the one-GPU box.  Its ETO, x0 and stop flags equal the plain run's (device ETO + device SGA)."""
+    process group, the per-step all-gather of the shard moments as device tensors, the Chan merge
+    and ETO on the device (mrbo_merge_moments), the device SGA step, the MAX all-reduce of the
+    clock) -- the exchange the 8-GPU run uses, on the one-GPU box.  Its ETO, x0 and stop flags
+    equal the plain run's (device ETO + device SGA)."""
     common = ["--steps", "2", "--warmup", "1", "--restarts", "4", "--no-cpu-baseline", "--config", "C2",
               "--mc-per-gpu", "64", "--eta", "0.5"]
     env = {k: v for k, v in os.environ.items() if k != "MRBO_DIST_BACKEND"}

@@ -59,7 +59,7 @@ def test_results_independent_of_schedule(gpu, name, M, R):
     }
     try:
         for oname, order in orders.items():
-            plan.set_order(order)
+            plan.set_order(order, check=oname != "out_of_range")
             out = _launch(torch, plan, args)
             for k, v in ref.items():
                 assert torch.equal(out[k], v), f"{name} order {oname}: output {k} differs"
@@ -75,5 +75,8 @@ def test_set_order_rejects_wrong_length(gpu):
     bad = torch.arange(63, dtype=torch.int32, device="cuda:0")
     with pytest.raises(ValueError):
         plan.set_order(bad)
+    dup = torch.zeros(64, dtype=torch.int32, device="cuda:0")     # right length, not a permutation
+    with pytest.raises(ValueError, match="permutation"):
+        plan.set_order(dup)
     rc = plan.lib.mrbo_plan_set_order(plan.handle, ctypes.c_void_p(bad.data_ptr()), bad.numel())
     assert rc == -1   # MRBO_ERR_ARG

@@ -148,6 +148,28 @@ def test_gp_fit_vs_oracle(gpu, oracle, kernel, d, N):
 
 
 @pytest.mark.gpu
+def test_gp_fit_wide_inputs_and_lds_limit(gpu, oracle):
+    """d > 16 runs the tile kernel, whose LDS holds X (d·⌈N/32⌉·32 doubles): d = 24 at N = 100 fits
+    and matches the oracle; d = 40 at N = 512 needs more than the CU's 160 KB, and the call fails
+    with MRBO_ERR_UNSUPPORTED before any launch instead of a HIP launch error."""
+    from mrbo import _lib
+    from mrbo.mle import gp_fit_batch
+    X, y = _data(24, 100, seed=5)
+    s = _surrogate(X, y, "matern52", 1.0)
+    ells = np.array([2.0, 5.0])
+    r = gp_fit_batch(s, ells)
+    for p, ell in enumerate(ells):
+        ll, dll = oracle.log_likelihood(X, y, "matern52", ell, 1e-6)
+        assert r["status"][p] == 0
+        assert r["ll"][p] == pytest.approx(ll, rel=1e-10, abs=1e-9)
+        assert r["dll"][p] == pytest.approx(dll, rel=1e-8, abs=1e-8 * (1 + abs(ll)))
+    X, y = _data(40, 512, seed=6)
+    s = _surrogate(X, y, "matern52", 5.0)
+    with pytest.raises(_lib.MrboError, match="LDS"):
+        gp_fit_batch(s, [5.0])
+
+
+@pytest.mark.gpu
 def test_gp_fit_posdef_failure(gpu):
     from mrbo.mle import gp_fit_batch
     X, y = _data(2, 10)
