@@ -94,13 +94,22 @@ static void run_case(int testfn, int d, int N, int h, int M, int R, double lo, d
   rbo_params p = {h, M, R, S, 0.0, lbs, ubs, 50, 20, 1e-3, 1e-3, 1e-8, 1e-4, 1e-8, 1906, 0, 0, 1, 1, RBO_RULE_EI,
                   cost, 1.0, w};
   double* kap = malloc(sizeof(double) * T);
+  double* vb = malloc(sizeof(double) * T);
+  double* yl = malloc(sizeof(double) * T);
   p.kappa = kap;
+  p.vbound = vb;
+  p.ylip = yl;
   CHECK(rbo_simulate_mc(&s, &p, x0s, rn, xs, NULL, NULL, values, gx, gt, st, pol, obs, eto, ev) == 0, "mc d=%d", d);
   p.kappa = NULL;
+  p.vbound = NULL;
+  p.ylip = NULL;
   int ok = 0;
-  for (int64_t t = 0; t < T; ++t) ok += (st[t] == 0) && isfinite(values[t]) && kap[t] >= 1.0;
+  for (int64_t t = 0; t < T; ++t)
+    ok += (st[t] == 0) && isfinite(values[t]) && kap[t] >= 1.0 && vb[t] > 0.0 && isfinite(vb[t]) && yl[t] >= 0.0;
   CHECK(ok == T, "mc d=%d: %d of %lld trajectories ok", d, ok, (long long)T);
   free(kap);
+  free(vb);
+  free(yl);
   /* replay the policy points just found: same values */
   if (h > 0) {
     double* rp = malloc(sizeof(double) * d * h * T);

@@ -37,7 +37,8 @@ class Params(ctypes.Structure):
                 ("htol", ctypes.c_double), ("sigma_tol", ctypes.c_double), ("seed", ctypes.c_uint64),
                 ("sample_offset", ctypes.c_int32), ("samples_total", ctypes.c_int32),
                 ("with_gradient", ctypes.c_int32), ("nthreads", ctypes.c_int32), ("rule", ctypes.c_int32),
-                ("cost", ctypes.c_int32), ("cost_c0", ctypes.c_double), ("cost_w", _dp), ("kappa", _dp)]
+                ("cost", ctypes.c_int32), ("cost_c0", ctypes.c_double), ("cost_w", _dp), ("kappa", _dp),
+                ("vbound", _dp), ("ylip", _dp)]
 
 
 def build():
@@ -202,7 +203,9 @@ def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=
     of the rnstream draws (rnstream is then only used for its M).
     cost=(kind, c0, w): NonUniformCost weighting of the inner-solve rule (rbo_oracle.h RBO_COST_*).
     want_kappa: also return "kappa" (M×R), each trajectory's largest cond₁ of the acquisition
-    Hessians its adjoint solved with (rbo_params.kappa; 1 when none)."""
+    Hessians its adjoint solved with (rbo_params.kappa; 1 when none), "vbound" (M×R) the first-order
+    bound on the rounding difference of its value and "ylip" (M×R) max_k ‖∂y_k/∂x_k‖₁
+    (rbo_params.vbound / ylip)."""
     x0s, xstarts = _f64(x0s), _f64(xstarts)
     lbs, ubs = _f64(lbs), _f64(ubs)
     d, R = x0s.shape
@@ -225,7 +228,9 @@ def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=
                  htol, sigma_tol, seed, sample_offset, samples_total, 1 if with_gradient else 0, nthreads,
                  RULES[rule], ck, c0, _p(cw))
     kappa = np.zeros((M, R), order="F") if want_kappa else None
-    prm.kappa = _p(kappa)
+    vbound = np.zeros((M, R), order="F") if want_kappa else None
+    ylip = np.zeros((M, R), order="F") if want_kappa else None
+    prm.kappa, prm.vbound, prm.ylip = _p(kappa), _p(vbound), _p(ylip)
     values = np.zeros((M, R), order="F")
     grad_x = np.zeros((d, M, R), order="F")
     grad_t = np.zeros((1, M, R), order="F")
@@ -248,7 +253,7 @@ def simulate_mc(osur, x0s, rnstream, xstarts, lbs, ubs, h, theta=0.0, dual_y_dx=
                                    evals.ctypes.data_as(_lp))
     assert rc == 0, rc
     return dict(values=values, grad_x=grad_x, grad_theta=grad_t, status=status, policy_x=policy, obs=obs,
-                eto=eto, evals=evals, kappa=kappa)
+                eto=eto, evals=evals, kappa=kappa, vbound=vbound, ylip=ylip)
 
 
 def base_solve(osur, xstarts, lbs, ubs, theta=0.0, rule="EI", max_iters=50, max_ls=20, x_tol=1e-3, f_tol=1e-3,

@@ -981,10 +981,13 @@ typedef struct {
 
 static int run_trajectory(const traj_in* in, int r, int m, const double* x0, fsur_t* fs, scratch_t* sc,
                           double* value, double* gx, double* gth, double* pol, double* obs_out, int64_t* evals,
-                          double* kappa) {
+                          double* kappa, double* vbound, double* ylip, double kappa_L) {
   const rbo_params* p = in->p;
   const int d = fs->d, h = p->h, M = p->M, D1 = d + 1;
-  double obs[64] = {0}, grads[64 * 16], z[17], xnext[16];
+  double obs[64] = {0}, grads[64 * 16], z[17], xnext[16], dy[64] = {0};
+  double wmax = 0.0;
+  const double nu = (double)(fs->N + h) * 0x1p-53;
+  if (ylip) *ylip = 0.0;
   sx_t sx;
   int st = 0;
   fsur_reset(fs);
@@ -1015,11 +1018,25 @@ static int run_trajectory(const traj_in* in, int r, int m, const double* x0, fsu
       st |= sx.status;
       obs[k] = sx.mu + SQRT2 * sx.sigma * tk;
       for (int a = 0; a < d; ++a) grads[a + d * k] = wk * (sx.gmu[a] + SQRT2 * sx.gsig[a] * tk);
+      z[0] = SQRT2 * tk;
+      wmax = fmax(wmax, wk);
     } else {
       for (int a = 0; a < D1; ++a) z[a] = in->rnstream[(int64_t)m + (int64_t)M * a + (int64_t)M * D1 * k];
       st |= fsur_draw(fs, xk, p->theta, p->sigma_tol, k - 1, z, &obs[k], grads + d * k, &sx, sc, kappa);
     }
     if (st) break;
+    if (vbound || ylip) {   /* the value bound's terms (rbo_params.vbound / ylip) */
+      const int n = fs->N + k;
+      const double* cv = fs->cs + (int64_t)k * fs->cap;
+      double smu = 0.0, skw = 0.0, yl = 0.0;
+      for (int j = 0; j < n; ++j) { smu += fabs(sc->kx[j] * cv[j]); skw += fabs(sc->kx[j] * sc->w[j]); }
+      dy[k] = nu * kappa_L * (smu + fabs(z[0]) * (k_psi(&fs->k, 0.0) + skw) / (2.0 * sx.sigma));
+      for (int i = 0; i < k; ++i) dy[k] += fabs(sc->w[fs->N + i]) * dy[i];
+      if (ylip) {
+        for (int a = 0; a < d; ++a) yl += fabs(sx.gmu[a] + z[0] * sx.gsig[a]);
+        *ylip = fmax(*ylip, yl);
+      }
+    }
     st |= fsur_condition(fs, xk, obs[k], sc->tmp);
     if (st) break;
   }
@@ -1031,7 +1048,13 @@ static int run_trajectory(const traj_in* in, int r, int m, const double* x0, fsu
     *value = NAN;
     for (int a = 0; a < d; ++a) gx[a] = NAN;
     *gth = NAN;
+    if (vbound) *vbound = NAN;
     return st;
+  }
+  if (vbound) {
+    double mx = 0.0;
+    for (int k = 0; k <= h; ++k) mx = fmax(mx, dy[k]);
+    *vbound = 2.0 * mx * (in->ghq_w ? wmax / SQRTPI : 1.0);
   }
   /* resolve (observables.jl:12-14) with fmini over the capacity buffer (Q3) */
   double bo = obs[0];
@@ -1162,6 +1185,29 @@ static int simulate_impl(const rbo_surrogate* s, const rbo_params* p, const doub
   const int d = s->d, M = p->M, R = p->R, h = p->h;
   const int64_t T = (int64_t)M * R;
   traj_in in = {s, p, rnstream, xstarts, dual_y_dx, replay_x, ghq_nodes, ghq_w};
+  /* κ_L = ‖L0‖₁‖L0⁻¹‖₁ of the base factor, for the value bound (rbo_params.vbound) */
+  double kappa_L = 1.0;
+  if (p->vbound) {
+    const int N = s->N;
+    double* Li = (double*)calloc((size_t)N * N, sizeof(double));
+    double nL = 0.0, nLi = 0.0;
+    for (int j = 0; j < N; ++j) {   /* column j of L0⁻¹ by forward substitution */
+      Li[j + (int64_t)N * j] = 1.0 / s->L[j + (int64_t)N * j];
+      for (int i = j + 1; i < N; ++i) {
+        double t = 0.0;
+        for (int q = j; q < i; ++q) t -= s->L[i + (int64_t)N * q] * Li[q + (int64_t)N * j];
+        Li[i + (int64_t)N * j] = t / s->L[i + (int64_t)N * i];
+      }
+    }
+    for (int j = 0; j < N; ++j) {
+      double a = 0.0, b = 0.0;
+      for (int i = j; i < N; ++i) { a += fabs(s->L[i + (int64_t)N * j]); b += fabs(Li[i + (int64_t)N * j]); }
+      nL = fmax(nL, a);
+      nLi = fmax(nLi, b);
+    }
+    kappa_L = nL * nLi;
+    free(Li);
+  }
 #ifdef _OPENMP
   if (p->nthreads > 0) omp_set_num_threads(p->nthreads);
 #endif
@@ -1178,7 +1224,8 @@ static int simulate_impl(const rbo_surrogate* s, const rbo_params* p, const doub
       double* kap = p->kappa ? p->kappa + tr : NULL;
       if (kap) *kap = 1.0;
       const int st = run_trajectory(&in, r, m, x0s + (int64_t)d * r, &fs, &sc, values + tr, grad_x + (int64_t)d * tr,
-                                    grad_theta + tr, policy_x, obs ? obs + (int64_t)(h + 1) * tr : NULL, ev, kap);
+                                    grad_theta + tr, policy_x, obs ? obs + (int64_t)(h + 1) * tr : NULL, ev, kap,
+                                    p->vbound ? p->vbound + tr : NULL, p->ylip ? p->ylip + tr : NULL, kappa_L);
       status[tr] = st;
       if (evals) for (int k = 0; k < 3; ++k) evals[3 * tr + k] = ev[k];
     }

@@ -79,6 +79,21 @@ typedef struct {
                               ‖Dk(0)‖₁‖σx⁻¹‖₁ over the draws (the cancellation condition of the
                               draw covariance σx = Dk(0) − G); the parity tests scale the
                               gradient tolerance by it                                        */
+  double* vbound;          /* diagnostic output M×R, or NULL: per trajectory a first-order bound on
+                              the absolute rounding difference of its value between two fp64
+                              implementations of the path (the parity tests' T2/T3 value bound):
+                              2·max_k δy_k with, per observation y_k = μ_k + σ_k·z_k,
+                                δy_k = n·u·κ_L·(Σ_j|kx_j c_j| + |z_k|·(ψ(0) + Σ_j|kx_j w_j|)/(2σ_k))
+                                       + Σ_{i<k} |w_k[N+i]|·δy_i,
+                              n = N + h, u = 2⁻⁵³, κ_L = ‖L0‖₁‖L0⁻¹‖₁ of the base factor, w = K⁻¹kx:
+                              the rounding of μ's and σ²'s n-term sums amplified by the base
+                              factor's conditioning (an explicit L0⁻¹ or substitution), σ² → σ
+                              by 1/(2σ), and the earlier fantasy observations' errors through
+                              ∂μ_k/∂y_i = w_k[N+i] (the conditions that feed resolve, rollout.jl:108-111);
+                              Gauss–Hermite: × the largest weight/√π                          */
+  double* ylip;            /* diagnostic output M×R, or NULL: max_k ‖∂y_k/∂x_k‖₁ = ‖∇μ + z_k∇σ‖₁ at the
+                              trajectory's observations (first-order effect of a policy point's
+                              own rounding difference on the value, T3)                       */
 } rbo_params;
 
 /* NonUniformCost (cost_functions.jl:5-20) as closed-form families.  The reference's cost is an

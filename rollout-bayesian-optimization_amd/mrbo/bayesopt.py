@@ -267,7 +267,10 @@ def run_myopic(function_name, output_dir, budget=100, trials=60, starts=64, seed
     results = {}
     sur = None
     if reuse_surrogate:    # :205 "Preallocate entire surrogate object and reuse"
-        sur = Surrogate(Matern52(), np.zeros((testfn.dim, 1)), np.zeros(1), capacity=capacity or budget, σn2=1e-6)
+        # capacity = BUDGET as the reference; it must hold the initial design (a reset! past
+        # capacity is a BoundsError in Julia), so a budget below it gets the design's size
+        sur = Surrogate(Matern52(), np.zeros((testfn.dim, 1)), np.zeros(1),
+                        capacity=capacity or max(budget, initial_observations), σn2=1e-6)
     for acq in rules:
         make_rule, theta = MYOPIC_RULES[acq]
         if reuse_surrogate:

@@ -9,23 +9,35 @@ Per trajectory t, with normwise relative errors
    e_val(t)  = |Δ value| / max(|value|, 1e-12)
    e_grad(t) = ‖Δ ∇x‖∞ / max(‖∇x‖∞, 1e-11·max_t ‖∇x‖∞)
   T2 replay (the oracle replays the GPU's own policy points x_1..x_h; every trajectory):
-     e_val ≤ 1e-9;  e_grad ≤ tol(t) = max(1e-9, n·u·κ(t)), u = 2^-53, n = N + h the largest data
+     |Δ value(t)| ≤ vb(t), the oracle's per-trajectory first-order bound (rbo_params.vbound):
+     2·max_k δy_k over the observations y_k = μ_k + σ_k z_k that feed resolve (rollout.jl:108-111),
+       δy_k = n·u·κ_L·(Σ_j|kx_j c_j| + |z_k|·(ψ(0) + Σ_j|kx_j w_j|)/(2σ_k)) + Σ_{i<k} |w_k[N+i]|·δy_i,
+     κ_L = ‖L0‖₁‖L0⁻¹‖₁ -- the n-term sums of μ and σ² rounded in different orders on the two sides,
+     amplified by the base factor's conditioning (the GPU multiplies by an explicit L0⁻¹, the
+     oracle substitutes) and by 1/(2σ) from σ² to σ, plus the earlier fantasy observations'
+     errors carried into μ_k by ∂μ_k/∂y_i = w_k[N+i] (the conditions, Q13);
+     e_grad ≤ tol(t) = max(1e-9, n·u·κ(t)), u = 2^-53, n = N + h the largest data
      size, κ(t) the oracle's conditioning of that trajectory (rbo_params.kappa): the largest of
      cond₁(H_j) over the adjoint solves H_j'\x̄ and ‖Dk(0)‖₁‖σx⁻¹‖₁ over the draws.  The two
      sides sum the n-term products of the draw covariance σx = Dk(0) − G and of Hα in different
      orders (rounding ≤ n·u relative to Dk(0) and ‖Hα‖); the draw's Cholesky and the adjoint solves
-     amplify that by κ.  No trajectory is exempt.
+     amplify that by κ.  No trajectory is exempt from either bound; the margins (largest error /
+     bound) go to the report.
   T3 end to end (both sides run the inner Newton solve):
      flips (an x_1..x_h differing by > 1e-6·(1+|x|))                  ≤ 0.1 % of trajectories
-     identical paths (policy equal to Δx(t) ≤ 1e-12 relative): e_val ≤ 1e-9 and
+     identical paths (policy equal to Δx(t) ≤ 1e-12 relative): |Δ value| ≤ vb(t) +
+     10·ylip(t)·Δx(t)·(1 + max|x|) -- the T2 bound plus the first-order effect of the policy points'
+     own rounding difference (ylip = max_k ‖∂y_k/∂x_k‖₁, rbo_params.ylip; 10 covers its propagation
+     through the later fantasy steps) -- and
      e_grad ≤ max(tol(t), 10·κ(t)·Δx(t)) -- the T2 bound plus the first-order effect of the
      policy points' own rounding difference Δx on the adjoint (‖∂x̄_j/∂x_j‖ ≤ κ·‖∂H/∂x‖/‖H‖, and
      ‖∂H/∂x‖/‖H‖ ≤ 10 is the kernel's derivative ratio ≈ √5/ℓ at ℓ ≥ 0.5); Newton work per counter
-     (gradient, value, Hessian) summed over them within 1 % of the oracle's.  Per-trajectory
-     equality of the counts is recorded, not asserted: on flat acquisition surfaces the line
-     search of a start that does not win the multistart is rounding-sensitive -- two builds of the
-     ORACLE itself (-ffp-contract=off vs -O3 -march=native) disagree on 56 of 122 identical-path
-     C4 trajectories at ℓ = 0.5 (totals within 0.2 %) and on none at C3 (tests/test_oracle.py)
+     (gradient, value, Hessian) summed over them within 1 % of the oracle's, and equal per
+     trajectory (work_exact, every case but C4's): on flat acquisition surfaces the line search of
+     a start that does not win the multistart is rounding-sensitive -- two builds of the ORACLE
+     itself (-ffp-contract=off vs -O3 -march=native) disagree on 56 of 122 identical-path C4
+     trajectories at ℓ = 0.5 (totals within 0.2 %) and on none at C3 (tests/test_oracle.py), so
+     C4 asserts the totals only
      ETO: no flips → normwise 1e-9 relative per block (mean value, std value, mean ∇x);
      flips → each mean within 3·σ/√M of the oracle's (σ the oracle's std)
   Non-vacuity (every case; a case that only exercises the forward rollout says so with
@@ -167,9 +179,18 @@ def _coverage(r, o):
                 gpu_grad_evals=int(ev[0].sum()), gpu_hessians=int(ev[2].sum()))
 
 
-def _compare(key, g, r, o, o_replay, M, kind="full"):
+def value_bound_stats(dv, vb):
+    """|Δ value| against the per-trajectory bound vb: count over, largest margin (error / bound)"""
+    if dv.size == 0:
+        return dict(over_bound=0, margin_max=0.0, bound_max=0.0, bound_median=0.0, err_max=0.0)
+    return dict(over_bound=int((dv > vb).sum()), margin_max=float((dv / vb).max()), bound_max=float(vb.max()),
+                bound_median=float(np.median(vb)), err_max=float(dv.max()))
+
+
+def _compare(key, g, r, o, o_replay, M, kind="full", work_exact=True):
     """The T2 / T3 assertions above and the non-vacuity guard; records the measured statistics
-    under `key`."""
+    under `key`.  work_exact: assert per-trajectory Newton work equality on the identical paths
+    (all cases but C4's, module docstring)."""
     assert kind in ("full", "forward")
     assert (r["status"] == 0).all() and (o["status"] == 0).all() and (o_replay["status"] == 0).all()
     dx = np.abs(r["policy_x"] - o["policy_x"]) / (1 + np.abs(o["policy_x"]))
@@ -182,6 +203,11 @@ def _compare(key, g, r, o, o_replay, M, kind="full"):
     kap = o_replay["kappa"].ravel(order="F")
     tol = grad_tolerance(kap, N + int(g["h"]))
     tol3 = np.maximum(tol, 10.0 * kap * dxt)
+    vb = o_replay["vbound"].ravel(order="F")
+    xmag = 1.0 + np.abs(o["policy_x"]).max(axis=(0, 1)).ravel(order="F")
+    vb3 = vb + 10.0 * o_replay["ylip"].ravel(order="F") * dxt * xmag
+    dv2 = np.abs(r["values"] - o_replay["values"]).ravel(order="F")
+    dv3 = np.abs(r["values"] - o["values"]).ravel(order="F")
     evals_r = r["evals"][:3].reshape(3, -1, order="F")
     evals_o = o["evals"].reshape(3, -1, order="F")
     e_r, e_o = r["eto"], o["eto"]
@@ -190,7 +216,9 @@ def _compare(key, g, r, o, o_replay, M, kind="full"):
                  drift=int((~flip & ~exact).sum()), identical=int(exact.sum()), flip_fraction=float(flip.mean()),
                  kappa_max=float(o_replay["kappa"].max()), grad_tol_max=float(tol.max()),
                  replay_value=_summ(ev2), replay_grad=_summ(eg2, tol),
+                 replay_value_bound=value_bound_stats(dv2, vb),
                  identical_value=_summ(ev3[exact]), identical_grad=_summ(eg3[exact], tol3[exact]),
+                 identical_value_bound=value_bound_stats(dv3[exact], vb3[exact]),
                  identical_dx_max=float(dxt[exact].max()) if exact.any() else 0.0,
                  work_unequal_identical=int((evals_r[:, exact] != evals_o[:, exact]).any(axis=0).sum()),
                  eto_mean_value_rel=_blocknorm(e_r[0], e_o[0]), eto_std_value_rel=_blocknorm(e_r[1], e_o[1]),
@@ -211,12 +239,14 @@ def _compare(key, g, r, o, o_replay, M, kind="full"):
     if kind == "full":
         assert cov["nonzero_values"] >= 0.25 and cov["t_ge_1"] >= 0.01 and cov["gpu_pairs"] > 0, stats
     # T2
-    assert stats["replay_value"]["max"] <= 1e-9, stats
+    assert stats["replay_value_bound"]["over_bound"] == 0, stats
     assert stats["replay_grad"]["over_tol"] == 0, stats
     # T3
     assert stats["flip_fraction"] <= FLIP_MAX, stats
-    assert stats["identical_value"]["max"] <= 1e-9, stats
+    assert stats["identical_value_bound"]["over_bound"] == 0, stats
     assert stats["identical_grad"]["over_tol"] == 0, stats
+    if work_exact:
+        assert stats["work_unequal_identical"] == 0, stats
     tg, to = np.asarray(stats["work_totals"]["gpu"], float), np.asarray(stats["work_totals"]["oracle"], float)
     assert np.all(np.abs(tg - to) <= 0.01 * np.maximum(to, 1.0)), stats
     if not flip.any():
@@ -228,8 +258,8 @@ def _compare(key, g, r, o, o_replay, M, kind="full"):
 
 def _replay_t2(g, r, o, ok=None):
     """T2 on a replay run alone (the oracle replayed the GPU's policy points, want_kappa=True):
-    every trajectory in `ok` has e_val ≤ 1e-9 and e_grad ≤ max(1e-9, n·u·κ(t)) (module docstring).
-    Returns (max e_val, max e_grad / tol)."""
+    every trajectory in `ok` has |Δ value| ≤ vb(t) and e_grad ≤ max(1e-9, n·u·κ(t)) (module
+    docstring).  Returns (max |Δ value| / vb, max e_grad / tol)."""
     ok = np.ones(r["values"].shape, dtype=bool) if ok is None else ok
     m = ok.ravel(order="F")
     if not m.any():
@@ -239,13 +269,15 @@ def _replay_t2(g, r, o, ok=None):
     d, N = g["X"].shape
     tol = grad_tolerance(o["kappa"].ravel(order="F"), N + int(g["h"]))
     ratio = eg[m] / tol[m]
-    assert ev[m].max() <= 1e-9, (ev[m].max(), int((ev[m] > 1e-9).sum()))
+    dv = np.abs(r["values"] - o["values"]).ravel(order="F")[m]
+    vm = dv / o["vbound"].ravel(order="F")[m]
+    assert vm.max() <= 1.0, (float(vm.max()), int((vm > 1).sum()), float(dv.max()))
     assert ratio.max() <= 1.0, (float(ratio.max()), int((ratio > 1).sum()), float(tol[m].max()))
-    return float(ev[m].max()), float(ratio.max())
+    return float(vm.max()), float(ratio.max())
 
 
 def _end_to_end(oracle, key, g, M, cost=None, plan_opts=None, kind="full", htol=1e-4, rule="EI", theta=0.0,
-                ghq=None):
+                ghq=None, work_exact=True):
     """GPU launch, the oracle on the same inputs, the oracle's replay of the GPU's policy points, then
     _compare.  rule / theta: the base decision rule (EI, POI, LCB); ghq = (nodes, weights): the
     Gauss–Hermite estimator instead of Monte-Carlo draws (M = the number of node vectors)."""
@@ -265,6 +297,6 @@ def _end_to_end(oracle, key, g, M, cost=None, plan_opts=None, kind="full", htol=
     rp = np.asfortranarray(r["policy_x"][:, 1:])
     o2 = oracle.simulate_mc(_osur(oracle, g), g["x0s"], rn, g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
                             replay_x=rp, want_policy=False, want_kappa=True, **kw)
-    return _compare(key, g, r, o, o2, M, kind=kind)
+    return _compare(key, g, r, o, o2, M, kind=kind, work_exact=work_exact)
 
 

@@ -396,3 +396,38 @@ def test_newton_work_rounding_sensitivity(oracle):
         else:
             assert (ea != eb).any(axis=0).sum() > 0          # per-trajectory counts differ ...
             np.testing.assert_allclose(eb.sum(1), ea.sum(1), rtol=0.01)   # ... the totals do not
+
+
+def test_value_bound_covers_two_oracle_builds(oracle):
+    """The T2 value bound (rbo_params.vbound, tests/parity.py) on a pair of fp64 implementations
+    the CPU suite can run: the -ffp-contract=off checker and the -O3 -march=native (FMA-contracted)
+    timing build of the oracle, replaying the same policy points.  Every trajectory's value
+    difference lies within its bound, the bound is finite and positive, and the values do differ
+    (the check is not vacuous)."""
+    from parity import _problem_arrays
+    from parity import _osur as posur
+    fast = os.path.join(ROOT, "oracle", "build", "librbo_oracle_fast.so")
+    if not os.path.exists(fast):
+        pytest.skip("timing build of the oracle not built")
+    nz = 0
+    for name, M, R, ell in [("C2", 64, 4, None), ("C3", 32, 4, None), ("C4", 16, 2, 0.5)]:
+        g = _problem_arrays(name, M, R, ell=ell)
+        base = oracle.simulate_mc(posur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"],
+                                  int(g["h"]), nthreads=8)
+        rp = np.asfortranarray(base["policy_x"][:, 1:])
+        runs = []
+        try:
+            for lib in (None, fast):
+                oracle.use_library(lib)
+                runs.append(oracle.simulate_mc(posur(oracle, g), g["x0s"], g["rnstream"], g["xstarts"], g["lbs"],
+                                               g["ubs"], int(g["h"]), replay_x=rp, nthreads=8, want_kappa=True))
+        finally:
+            oracle.use_library(None)
+        a, b = runs
+        vb = a["vbound"]
+        assert np.isfinite(vb).all() and (vb > 0).all()
+        dv = np.abs(a["values"] - b["values"])
+        assert (dv <= vb).all(), (name, float((dv / vb).max()))
+        nz += int((dv > 0).sum())
+        assert (a["ylip"] >= 0).all()
+    assert nz > 0
