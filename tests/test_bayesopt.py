@@ -157,7 +157,8 @@ def test_myopic_loop_end_to_end(gpu, tmp_path):
     """experiments/myopic_bayesopt.jl's loop (bayesopt.run_myopic): multistart_base_solve! on the
     device per budget step, CSVs per acquisition, the loop's invariants."""
     from mrbo import bayesopt
-    res = bayesopt.run_myopic("braninhoo", str(tmp_path), budget=3, trials=2, starts=16, log=lambda *a: None)
+    res = bayesopt.run_myopic("braninhoo", str(tmp_path), budget=3, trials=2, starts=16, log=lambda *a: None,
+                              capacity=8)
     d = tmp_path / "myopic" / "braninhoo"
     for acq in ("ei", "poi", "lcb"):
         for metric in bayesopt.METRICS:
@@ -169,6 +170,12 @@ def test_myopic_loop_end_to_end(gpu, tmp_path):
             assert (r["X"][0] >= -5.0).all() and (r["X"][0] <= 10.0).all() and (r["X"][1] >= 0.0).all()
             assert np.all(np.diff(r["minimum_observations"]) <= 0)
             assert np.all((r["gaps"] >= 0.0) & (r["gaps"] <= 1.0 + 1e-12))
+    # one surrogate for every rule and trial (myopic_bayesopt.jl:205-217): each trial starts from
+    # the lengthscale the previous one's optimize! left; only the very first starts at ℓ = 1
+    order = [(acq, t) for acq in ("ei", "poi", "lcb") for t in range(2)]
+    assert res[order[0]]["ell_start"] == 1.0
+    for a, b in zip(order, order[1:]):
+        assert res[b]["ell_start"] == res[a]["ell_end"]
 
 
 @pytest.mark.gpu
