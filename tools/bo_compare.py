@@ -132,7 +132,10 @@ def trajectory_diagnostics(Xs, lbs, ubs, initial):
             "trials_with_repeats": float(np.mean(rep))}
 
 
-def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incumbent=True, reuse=True):
+def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incumbent=True, reuse=True,
+             run_budget=None):
+    """One comparison case.  run_budget (myopic cases) overrides the steps each trial runs (default
+    the reference's 100, whose last optimize! sets the next trial's starting lengthscale)."""
     from mrbo import bayesopt
     s = SETTINGS[key]
     testfn = bayesopt.TESTFNS[s["fn"]]()
@@ -142,7 +145,7 @@ def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incu
         t0 = time.perf_counter()
         lg = lambda *m: log(f"[{key}] " + " ".join(map(str, m)))
         if myopic:
-            rb = s["run_budget"] if reuse else s["budget"]
+            rb = (run_budget or s["run_budget"]) if reuse else s["budget"]
             res = bayesopt.run_myopic(s["fn"], tmp, budget=rb, trials=trials, starts=s["starts"], seed=seed,
                                       rules=(s["rule"],), initial_observations=s["initial"], log=lg,
                                       reuse_surrogate=reuse, capacity=s["capacity"] if reuse else None)
