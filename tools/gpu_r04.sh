@@ -65,7 +65,7 @@ for l in open(sys.argv[1]):
     if l.startswith('{'):
         d = json.loads(l); print(d['config']['workload'], round(d['value']), 'fits/s;', round(d['kernel_ms'], 3), 'ms kernel; frac', round(d['roofline']['frac'], 4))" "$out/gpfit_rows.jsonl" ;;
     bo)
-      timeout -k 10 1000 python -u tools/bo_compare.py --trials ${BO_TRIALS:-40} --cases ${BO_CASES:-asserted} ${BO_ARGS:-} \
+      timeout -k 10 ${BO_TIMEOUT:-1000} python -u tools/bo_compare.py --trials ${BO_TRIALS:-40} --cases ${BO_CASES:-asserted} ${BO_ARGS:-} \
         --out "$out/bo_compare.jsonl" > /dev/null 2> "$out/bo_compare.err"
       rc=$?; grep "final gap" "$out/bo_compare.err" ;;
     *) echo "unknown step $step"; rc=2 ;;
