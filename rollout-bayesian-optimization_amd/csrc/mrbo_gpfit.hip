@@ -683,11 +683,28 @@ __device__ __forceinline__ void tile_ij(int q, int& I, int& J) {
   J = q - I * (I + 1) / 2;
 }
 
+// -DMRBO_GPFIT_STAMPS: cycles per phase of candidate 0 (thread 0, after each workgroup barrier):
+// K, then per tile column the diagonal factor + inverse, the panel, the trailing update (summed
+// over k), V by tile rows, c, K⁻¹ + traces
+#ifdef MRBO_GPFIT_STAMPS
+#define TT_STAMP(k)                                                   \
+  do {                                                                \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();     \
+    tt_acc[k] += now_ - tt_last;                                      \
+    tt_last = now_;                                                   \
+  } while (0)
+#else
+#define TT_STAMP(k) ((void)0)
+#endif
+
 template <int NT>
 __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, int P) {
   extern __shared__ __attribute__((aligned(16))) double tsm[];
   const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (p >= P) return;   // whole workgroups
+#ifdef MRBO_GPFIT_STAMPS
+  unsigned long long tt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tt_last = __builtin_amdgcn_s_memtime();
+#endif
   const int N = q.N, d = q.d, T = (N + TT - 1) / TT, NP = T * TT;
   double* XS = tsm;                      // X[u][i] at u·NP + i, zero-padded
   double* Dk = XS + (size_t)d * NP;      // diagonal tile A_kk → L_kk, 32 × 33 column-major
@@ -727,6 +744,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     Lt[e] = v;
   }
   __syncthreads();
+  TT_STAMP(1);
   double lg = 0.0;   // Σ log L_ii (wave 0)
   for (int k = 0; k < T; ++k) {
     if (w == 0) {
@@ -783,6 +801,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       }
     }
     __syncthreads();
+    TT_STAMP(2);
     if (fail) break;
     // panel: L_Ik = A_Ik·L_kk⁻ᵀ by forward substitution, one row per lane (lanes < 32) in the
     // wave's LDS scratch: L_Ik[r][c] = (A_Ik[r][c] − Σ_{m<c} L_Ik[r][m]·L_kk[c][m]) / L_kk[c][c], the
@@ -810,6 +829,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       gr_sync();
     }
     __syncthreads();
+    TT_STAMP(3);
     // trailing update A_IJ −= L_Ik·L_Jkᵀ, k < J ≤ I
     const int m = T - k - 1, npair = m * (m + 1) / 2;
     for (int pi = w; pi < npair; pi += 4) {
@@ -823,6 +843,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       tile_store<false>(c, Lt + tile_at(I, J), lane);
     }
     __syncthreads();
+    TT_STAMP(4);
   }
   if (fail) {
     if (tid == 0) {
@@ -848,6 +869,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       gr_sync();
     }
     __syncthreads();
+    TT_STAMP(5);
   }
   // c = L'\(L\y) by blocked substitution (wave 0; lane i < 32 = row i of the current tile):
   // forward z_I = L_II⁻¹(y_I − Σ_{J<I} L_IJ z_J), backward c_I = L_II⁻ᵀ(z_I − Σ_{J>I} L_JIᵀ c_J);
@@ -894,6 +916,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     if (lane == 0) part[0][2 * NT] = yc;
   }
   __syncthreads();
+  TT_STAMP(6);
   // K⁻¹ tiles and the traces over the strictly lower entries
   double tr[NT], cgc[NT];
 #pragma unroll
@@ -931,6 +954,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     if (lane == 0) { part[w][t] = trs; part[w][NT + t] = cgs; }
   }
   __syncthreads();
+  TT_STAMP(7);
   if (tid == 0) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {   // both triangles: 2·Σ_{j<i}, halved by δlog_likelihood's 1/2
@@ -941,6 +965,11 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     q.ll[p] = -0.5 * part[0][2 * NT] - part[0][2 * NT + 1] - 0.5 * N * log(2.0 * 3.141592653589793);
     q.status[p] = 0;
   }
+#ifdef MRBO_GPFIT_STAMPS
+  if (p == 0 && tid == 0)
+    printf("gpfit_tile N=%d cycles: K %llu  diag %llu  panel %llu  trailing %llu  V %llu  c %llu  traces %llu\n", N,
+           tt_acc[1], tt_acc[2], tt_acc[3], tt_acc[4], tt_acc[5], tt_acc[6], tt_acc[7]);
+#endif
   if (q.L_out) {
     double* Lo = q.L_out + (size_t)N * N * p;
     for (size_t idx = tid; idx < (size_t)N * N; idx += TT_THREADS) {
