@@ -713,6 +713,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   double* Sw = rd + TT;                  // per-wave 32 × 32 scratch (row-major S)
   double* yv = Sw + 4 * TT * TT;         // y, then c
   double* uv = yv + NP;                  // z = L⁻¹y
+  double* rdall = uv + NP;               // 1/L_ii of every row (the substitutions multiply)
   __shared__ double part[TT_THREADS / 64][2 * NT + 2];
   __shared__ int fail;
   double ell, per;
@@ -745,7 +746,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   }
   __syncthreads();
   TT_STAMP(1);
-  double lg = 0.0;   // Σ log L_ii (wave 0)
+  double lgl = 0.0;   // Σ log L_ii: lane i < 32 of wave 0 sums row i of every diagonal tile
   for (int k = 0; k < T; ++k) {
     if (w == 0) {
       // A_kk → L_kk in LDS (right-looking; PosDefException → status 1), then W_k = L_kk⁻¹
@@ -762,31 +763,55 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
         }
         double lcc, rl;
         sqrt_rsqrt(piv, lcc, rl);
-        if (TT * k + c < N) lg += log(lcc);
-        gr_sync();
-        if (h == 0 && i > c) Dk[c * TT_LD + i] *= rl;
+        // column c is scaled on the fly (l_jc = a_jc·rl, the same product as scaling it first):
+        // the update reads column c and writes the columns j > c, so one wave barrier per column
+        // (before the next pivot) suffices, and every lane issues all its loads before its stores
+        if (i > c) {
+          const double lic = Dk[c * TT_LD + i] * rl;
+          double lc[TT / 2], ar[TT / 2];
+#pragma unroll
+          for (int q2 = 0; q2 < TT / 2; ++q2) {
+            const int j = 2 * q2 + h;
+            const bool v = (j > c) & (j <= i);
+            lc[q2] = v ? Dk[c * TT_LD + j] : 0.0;
+            ar[q2] = v ? Dk[j * TT_LD + i] : 0.0;
+          }
+#pragma unroll
+          for (int q2 = 0; q2 < TT / 2; ++q2) {
+            const int j = 2 * q2 + h;
+            if ((j > c) & (j <= i)) Dk[j * TT_LD + i] = fma(-lic, lc[q2] * rl, ar[q2]);
+          }
+          if (h == 0) Dk[c * TT_LD + i] = lic;
+        }
         if (lane == 0) {
           Dk[c * TT_LD + c] = lcc;
           rd[c] = rl;
-        }
-        gr_sync();
-        if (i > c) {
-          const double lic = Dk[c * TT_LD + i];
-          for (int j = c + 1 + h; j <= i; j += 2) Dk[j * TT_LD + i] = fma(-lic, Dk[c * TT_LD + j], Dk[j * TT_LD + i]);
+          rdall[TT * k + c] = rl;
         }
         gr_sync();
       }
       if (bad) {
         if (lane == 0) fail = 1;
       } else {
-        // W column j = lane (< 32): W_ij = (δ_ij − Σ_{m<i} L_im W_mj)/L_ii, rows ascending
-        // (W_mj = 0 for m < j comes out of the same recursion)
+        if (lane < TT && TT * k + lane < N) lgl += log(Dk[lane * TT_LD + lane]);
+        // W column j = lane (< 32): W_ij = (δ_ij − Σ_{m<i} L_im W_mj)/L_ii, rows ascending, the
+        // column in registers (W_mj = 0 for m < j comes out of the same recursion); two partial
+        // sums halve the dependent chain
         if (lane < TT) {
+          double wc[TT];
+#pragma unroll
           for (int r = 0; r < TT; ++r) {
-            double sacc = (r == lane) ? 1.0 : 0.0;
-            for (int m = 0; m < r; ++m) sacc = fma(-Dk[m * TT_LD + r], Wk[lane * TT_LD + m], sacc);
-            Wk[lane * TT_LD + r] = sacc * rd[r];
+            double s0 = (r == lane) ? 1.0 : 0.0, s1 = 0.0;
+#pragma unroll
+            for (int m = 0; m + 1 < r; m += 2) {
+              s0 = fma(-Dk[m * TT_LD + r], wc[m], s0);
+              s1 = fma(-Dk[(m + 1) * TT_LD + r], wc[m + 1], s1);
+            }
+            if (r & 1) s0 = fma(-Dk[(r - 1) * TT_LD + r], wc[r - 1], s0);
+            wc[r] = (s0 + s1) * rd[r];
           }
+#pragma unroll
+          for (int r = 0; r < TT; ++r) Wk[lane * TT_LD + r] = wc[r];
         }
         gr_sync();
         double* Lkk = Lt + tile_at(k, k);
@@ -803,30 +828,28 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     __syncthreads();
     TT_STAMP(2);
     if (fail) break;
-    // panel: L_Ik = A_Ik·L_kk⁻ᵀ by forward substitution, one row per lane (lanes < 32) in the
-    // wave's LDS scratch: L_Ik[r][c] = (A_Ik[r][c] − Σ_{m<c} L_Ik[r][m]·L_kk[c][m]) / L_kk[c][c], the
+    // panel: L_Ik = A_Ik·L_kk⁻ᵀ by forward substitution, one row per lane (lanes < 32), the row in
+    // registers: L_Ik[r][c] = (A_Ik[r][c] − Σ_{m<c} L_Ik[r][m]·L_kk[c][m]) / L_kk[c][c], the
     // factor's own recurrence (a product with the explicit inverse W_k is ≈ κ(L_kk) less accurate)
     for (int I = k + 1 + w; I < T; I += 4) {
       double* A = Lt + tile_at(I, k);
-      double* S = Sw + w * (TT * TT);
-      for (int e = lane; e < TT * TT; e += 64) S[e] = A[e];
-      gr_sync();
       if (lane < TT) {
         const int r = lane;
+        double lrow[TT];
+#pragma unroll
         for (int c = 0; c < TT; ++c) {
-          double v0 = S[c * TT + r], v1 = 0.0;
-          int m = 0;
-          for (; m + 2 <= c; m += 2) {
-            v0 = fma(-S[m * TT + r], Dk[m * TT_LD + c], v0);
-            v1 = fma(-S[(m + 1) * TT + r], Dk[(m + 1) * TT_LD + c], v1);
+          double v0 = A[c * TT + r], v1 = 0.0;
+#pragma unroll
+          for (int m = 0; m + 1 < c; m += 2) {
+            v0 = fma(-lrow[m], Dk[m * TT_LD + c], v0);
+            v1 = fma(-lrow[m + 1], Dk[(m + 1) * TT_LD + c], v1);
           }
-          if (m < c) v0 = fma(-S[m * TT + r], Dk[m * TT_LD + c], v0);
-          S[c * TT + r] = (v0 + v1) * rd[c];
+          if (c & 1) v0 = fma(-lrow[c - 1], Dk[(c - 1) * TT_LD + c], v0);
+          lrow[c] = (v0 + v1) * rd[c];
         }
+#pragma unroll
+        for (int c = 0; c < TT; ++c) A[c * TT + r] = lrow[c];
       }
-      gr_sync();
-      for (int e = lane; e < TT * TT; e += 64) A[e] = S[e];
-      gr_sync();
     }
     __syncthreads();
     TT_STAMP(3);
@@ -853,7 +876,10 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     }
     return;
   }
-  if (tid == 0) part[0][2 * NT + 1] = lg;   // wave 0's sum
+  if (w == 0) {
+    const double lg = gr_sum(lgl);
+    if (lane == 0) part[0][2 * NT + 1] = lg;   // wave 0's sum
+  }
   // V = L⁻¹ below the diagonal tiles, by tile rows
   for (int I = 1; I < T; ++I) {
     for (int J = w; J < I; J += 4) {
@@ -886,7 +912,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       }
       const double* L = Lt + tile_at(I, I);
       for (int m = 0; m < TT; ++m) {
-        const double zm = readlane_d(r, m) / L[m * TT + m];
+        const double zm = readlane_d(r, m) * rdall[TT * I + m];
         if (i == m) r = zm;
         else if (i > m) r = fma(-L[m * TT + i], zm, r);
       }
@@ -901,7 +927,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       }
       const double* L = Lt + tile_at(I, I);
       for (int m = TT - 1; m >= 0; --m) {
-        const double cm = readlane_d(r, m) / L[m * TT + m];
+        const double cm = readlane_d(r, m) * rdall[TT * I + m];
         if (i == m) r = cm;
         else if (i < m) r = fma(-L[i * TT + m], cm, r);
       }
@@ -983,7 +1009,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
 
 size_t gpfit_tile_lds(int d, int N) {
   const int NP = ((N + TT - 1) / TT) * TT;
-  return sizeof(double) * ((size_t)d * NP + 2 * TT * TT_LD + TT + 4 * TT * TT + 2 * (size_t)NP);
+  return sizeof(double) * ((size_t)d * NP + 2 * TT * TT_LD + TT + 4 * TT * TT + 3 * (size_t)NP);
 }
 
 size_t gpfit_tile_work_doubles(int N) {
