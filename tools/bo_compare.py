@@ -132,10 +132,17 @@ def trajectory_diagnostics(Xs, lbs, ubs, initial):
             "trials_with_repeats": float(np.mean(rep))}
 
 
-def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incumbent=True, reuse=True,
+def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incumbent=True, reuse=None,
              run_budget=None):
     """One comparison case.  run_budget (myopic cases) overrides the steps each trial runs (default
-    the reference's 100, whose last optimize! sets the next trial's starting lengthscale)."""
+    the reference's 100, whose last optimize! sets the next trial's starting lengthscale).
+    reuse=None takes the surrogate semantics of the driver that produced the case's records: the
+    myopic records come from experiments/myopic_bayesopt.jl, which reuses ONE surrogate over the
+    trials (:205-217, the lengthscale carries over); the archived rollout records come from the
+    earlier driver experiments/adaptive_bayesopt.jl, which fits a fresh surrogate per trial
+    (`sur = fit_surrogate(ψ, Xinit, yinit)`, :498, ψ defined once at :407)."""
+    if reuse is None:
+        reuse = key.startswith("myopic")
     from mrbo import bayesopt
     s = SETTINGS[key]
     testfn = bayesopt.TESTFNS[s["fn"]]()
@@ -195,9 +202,10 @@ def main():
                          "for adam)")
     ap.add_argument("--no-q3", action="store_true",
                     help="diagnostic: fmini over the observed points instead of the zero-padded buffer (Q3 off)")
-    ap.add_argument("--no-reuse", action="store_true",
-                    help="diagnostic: a fresh surrogate (ℓ = 1) per trial instead of the reference's one reused "
-                         "surrogate whose lengthscale carries over between trials (the round-3 loops)")
+    ap.add_argument("--reuse", choices=("auto", "yes", "no"), default="auto",
+                    help="surrogate reuse over trials: auto = the recording driver's semantics (myopic: reused, "
+                         "myopic_bayesopt.jl:205-217; archived rollout runs: fresh per trial, "
+                         "adaptive_bayesopt.jl:498); yes / no force it (diagnostics)")
     ap.add_argument("--no-incumbent", action="store_true",
                     help="diagnostic: the round-2 solver (no incumbent restart, no no-repeat pick)")
     a = ap.parse_args()
@@ -206,7 +214,7 @@ def main():
     for key in (ASSERTED if a.cases == "asserted" else a.cases.split(",")):
         eta = a.eta or (0.01 if a.solver == "sga" else 0.02)
         row = run_case(key, ref[key], a.trials, a.seed, log, solver=a.solver, eta=eta, q3=not a.no_q3, incumbent=not a.no_incumbent,
-                       reuse=not a.no_reuse)
+                       reuse={"auto": None, "yes": True, "no": False}[a.reuse])
         line = json.dumps(row)
         print(line, flush=True)
         if a.out:
