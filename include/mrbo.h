@@ -235,7 +235,7 @@ int mrbo_base_solve(mrbo_plan_t* plan, int32_t n, const double* xstarts, double*
  * / c_out are device pointers unless MRBO_FLAG_HOST_POINTERS; N ≤ 512 (every N the rollout
  * accepts).  N ≤ 80 runs without workspace (one wave per candidate at N ≤ 64 without L_out /
  * c_out, the candidate in LDS up to N = 80); N > 80 runs the 32 × 32-tile kernel on the fp64
- * matrix cores with (T(T+1) + T)·1024·P doubles of workspace, T = ⌈N/32⌉, allocated for the
+ * matrix cores with ((2 + nt)·T(T+1)/2 + T)·1024·P doubles of workspace, T = ⌈N/32⌉, allocated for the
  * call.  Synchronises the stream before returning.                                          */
 int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t P, int32_t nt, const double* thetas, double* ll,
                       double* grad, int32_t* status, double* L_out, double* c_out, uint32_t flags, void* stream);

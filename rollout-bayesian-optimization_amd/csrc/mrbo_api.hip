@@ -930,7 +930,7 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
                   need, lds_max);
   }
   if (!gpfit_in_regs(q) && !gpfit_in_lds(q)) {   // the register (N ≤ 64) and LDS (N ≤ 80) kernels need none
-    q.work = (double*)sg.slot(sizeof(double) * gpfit_tile_work_doubles(N) * P);
+    q.work = (double*)sg.slot(sizeof(double) * gpfit_tile_work_doubles(N, nt) * P);
     if (!q.work) return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
   }
   // timing events per device (an event records only on streams of the device it was created on)

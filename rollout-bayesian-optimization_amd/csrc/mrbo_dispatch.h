@@ -69,10 +69,10 @@ struct GpFitParams {
   int* status;           // P: 0, or 1 = PosDefException
   double* L_out;         // optional N×N×P
   double* c_out;         // optional N×P
-  double* work;          // gpfit_tile_work_doubles(N)·P (the tile kernel only)
+  double* work;          // gpfit_tile_work_doubles(N, nt)·P (the tile kernel only)
 };
 // MRBO_GPFIT_LDS_MAX < N ≤ 512: gpfit_tile_kernel's workspace per candidate
-size_t gpfit_tile_work_doubles(int N);
+size_t gpfit_tile_work_doubles(int N, int nt);
 // LDS bytes per workgroup of the kernel launch_gpfit selects for q (the tile kernel stages X:
 // d·⌈N/32⌉·32 doubles, so large d can exceed the CU's 160 KB)
 size_t gpfit_launch_lds(const GpFitParams& q);

@@ -607,8 +607,10 @@ __global__ void __launch_bounds__(GL_THREADS) gpfit_lds_kernel(GpFitParams q, in
 // ---- 128 < N ≤ 512: blocked on 32 × 32 tiles, the products on the fp64 matrix cores ----------
 // One workgroup (four waves) per candidate.  Global workspace per candidate (tile_work_doubles):
 // the lower tiles of K → L (column-major), of V = L⁻¹ (row-major) and the diagonal-tile inverses
-// W_k = L_kk⁻¹ (column-major); T = ⌈N/32⌉, rows and columns past N are identity rows of K (their
-// L, V and K⁻¹ rows are identity rows too, and they take no part in the sums).
+// W_k = L_kk⁻¹ (column-major), then the lower tiles of δK_t = ∂K/∂θ_t (the K pass evaluates ψ and
+// ∂ψ/∂θ together; the traces read them back instead of evaluating the radial function again);
+// T = ⌈N/32⌉, rows and columns past N are identity rows of K (their L, V and K⁻¹ rows are identity
+// rows too, and they take no part in the sums).
 //   Cholesky, right-looking by tile columns k: wave 0 factors A_kk and inverts L_kk in LDS; the
 //   panel L_Ik = A_Ik·L_kk⁻ᵀ by substitution (one row per lane); the trailing updates
 //   A_IJ −= L_Ik·L_Jkᵀ are 32³ products spread over the four waves, each 32 v_mfma_f64_16x16x4
@@ -617,7 +619,7 @@ __global__ void __launch_bounds__(GL_THREADS) gpfit_lds_kernel(GpFitParams q, in
 //   column-major Vᵀ the later products read.
 //   c = L'\(L\y) by blocked substitution, and K⁻¹_IJ = Σ_{M≥I} V_MIᵀ V_MJ for I ≥ J, whose tile the
 //   wave holds in registers while it adds K⁻¹_ij·δK_t,ij and c_i c_j·δK_t,ij over the strictly
-//   lower entries (δK on the fly; δK_ii = 0), as the LDS kernel above does.
+//   lower entries (δK stored by the K pass; δK_ii = 0), as the LDS kernel above does.
 // ≈ N³/2 multiply-adds (N³/6 each for L, V and K⁻¹), all but the diagonal tiles' on the MFMA pipe.
 constexpr int TT = 32, TT_THREADS = 256, TT_LD = 33;
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -719,9 +721,10 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   double ell, per;
   cand_theta(q, p, ell, per);
   const size_t ntile = (size_t)T * (T + 1) / 2;
-  double* Lt = q.work + (size_t)p * (2 * ntile + T) * (TT * TT);
+  double* Lt = q.work + (size_t)p * ((2 + NT) * ntile + T) * (TT * TT);
   double* Vt = Lt + ntile * (TT * TT);
   double* Wt = Vt + ntile * (TT * TT);
+  double* Dt = Wt + (size_t)T * (TT * TT);   // δK_t = ∂K/∂θ_t in the tile layout of Lt, kept for the traces
   if (tid == 0) fail = 0;
   for (int idx = tid; idx < d * NP; idx += TT_THREADS) {
     const int u = idx / NP, i = idx % NP;
@@ -735,14 +738,17 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     tile_ij((int)(e >> 10), I, J);
     const int gi = TT * I + (int)(e & 31), gj = TT * J + (int)((e >> 5) & 31);
     double v = (gi == gj) ? 1.0 : 0.0;
+    double dps[2] = {0.0, 0.0};
     if (gi < N && gj < N) {
       double r2 = 0.0;
       for (int u = 0; u < d; ++u) { const double r = XS[u * NP + gi] - XS[u * NP + gj]; r2 = fma(r, r, r2); }
-      double psi, dps[2];
+      double psi;
       psi_dtheta(q.kernel, ell, per, (gi == gj) ? 0.0 : sqrt(r2), psi, dps);
       v = (gi == gj) ? psi + q.sn2 : psi;
     }
     Lt[e] = v;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) Dt[(size_t)t * ntile * (TT * TT) + e] = dps[t];   // the same bits the traces used to recompute
   }
   __syncthreads();
   TT_STAMP(1);
@@ -959,17 +965,15 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int gi = TT * I + 16 * bi + (lane >> 4) + 4 * j, gj = TT * J + 16 * bj + (lane & 15);
+          const int li = 16 * bi + (lane >> 4) + 4 * j, lj = 16 * bj + (lane & 15);
+          const int gi = TT * I + li, gj = TT * J + lj;
           if (gi > gj && gi < N) {
-            double r2 = 0.0;
-            for (int u = 0; u < d; ++u) { const double r = XS[u * NP + gi] - XS[u * NP + gj]; r2 = fma(r, r, r2); }
-            double psi, dps[2];
-            psi_dtheta(q.kernel, ell, per, sqrt(r2), psi, dps);
             const double cc = yv[gi] * yv[gj], kij = c[bi][bj][j];
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-              tr[t] = fma(kij, dps[t], tr[t]);
-              cgc[t] = fma(cc, dps[t], cgc[t]);
+              const double dk = Dt[(size_t)t * ntile * (TT * TT) + tile_at(I, J) + lj * TT + li];   // δK_t,ij from the K pass
+              tr[t] = fma(kij, dk, tr[t]);
+              cgc[t] = fma(cc, dk, cgc[t]);
             }
           }
         }
@@ -1012,9 +1016,9 @@ size_t gpfit_tile_lds(int d, int N) {
   return sizeof(double) * ((size_t)d * NP + 2 * TT * TT_LD + TT + 4 * TT * TT + 3 * (size_t)NP);
 }
 
-size_t gpfit_tile_work_doubles(int N) {
-  const size_t T = (N + TT - 1) / TT;
-  return (T * (T + 1) + T) * TT * TT;
+size_t gpfit_tile_work_doubles(int N, int nt) {
+  const size_t T = (N + TT - 1) / TT, ntile = T * (T + 1) / 2;
+  return ((2 + (size_t)nt) * ntile + T) * TT * TT;
 }
 
 size_t gpfit_lds_bytes() { return sizeof(double) * ((size_t)GL_N * GL_LD + 16 * GL_N + 3 * GL_N); }
