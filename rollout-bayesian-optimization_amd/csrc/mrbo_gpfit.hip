@@ -758,44 +758,49 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       // A_kk → L_kk in LDS (right-looking; PosDefException → status 1), then W_k = L_kk⁻¹
       const int i = lane & 31, h = lane >> 5;
       const double* A = Lt + tile_at(k, k);
-      for (int e = lane; e < TT * TT; e += 64) Dk[(e >> 5) * TT_LD + (e & 31)] = A[e];
-      gr_sync();
+      // A_kk → L_kk with the rows in registers: lane (i, h) holds a_ij for the columns j = 2q + h
+      // (i = lane & 31, h = lane >> 5).  Per column c the pivot comes by readlane, a_ic from the
+      // partner half by one swap, and column c of L reaches every lane through one LDS broadcast;
+      // the rank-1 update is then 16 predicated FMAs per lane on registers.
       bool bad = false;
+      double a[TT / 2];
+#pragma unroll
+      for (int q2 = 0; q2 < TT / 2; ++q2) a[q2] = A[(2 * q2 + h) * TT + i];
+      double* colc = Wk;   // column c of L (32 doubles); W_k is formed after the factorization
+#pragma unroll
       for (int c = 0; c < TT; ++c) {
-        const double piv = Dk[c * TT_LD + c];
+        const int qc = c >> 1, hc = c & 1;
+        const double piv = readlane_d(a[qc], c + 32 * hc);
         if (!(piv > 0.0)) {   // the same value in every lane: a uniform exit
           bad = true;
           break;
         }
         double lcc, rl;
         sqrt_rsqrt(piv, lcc, rl);
-        // column c is scaled on the fly (l_jc = a_jc·rl, the same product as scaling it first):
-        // the update reads column c and writes the columns j > c, so one wave barrier per column
-        // (before the next pivot) suffices, and every lane issues all its loads before its stores
-        if (i > c) {
-          const double lic = Dk[c * TT_LD + i] * rl;
-          double lc[TT / 2], ar[TT / 2];
+        const double other = __shfl_xor(a[qc], 32, 64);
+        const double lic = ((h == hc) ? a[qc] : other) * rl;   // l_ic of this lane's row
+        if (h == 0) colc[i] = lic;
+        gr_sync();
 #pragma unroll
-          for (int q2 = 0; q2 < TT / 2; ++q2) {
+        for (int q2 = 0; q2 < TT / 2; ++q2) {
+          if (2 * q2 + 1 > c) {   // some column j = 2·q2 + h of this slot lies right of c
             const int j = 2 * q2 + h;
-            const bool v = (j > c) & (j <= i);
-            lc[q2] = v ? Dk[c * TT_LD + j] : 0.0;
-            ar[q2] = v ? Dk[j * TT_LD + i] : 0.0;
+            const double ljc = colc[j];
+            if ((j > c) & (j <= i)) a[q2] = fma(-lic, ljc, a[q2]);
           }
-#pragma unroll
-          for (int q2 = 0; q2 < TT / 2; ++q2) {
-            const int j = 2 * q2 + h;
-            if ((j > c) & (j <= i)) Dk[j * TT_LD + i] = fma(-lic, lc[q2] * rl, ar[q2]);
-          }
-          if (h == 0) Dk[c * TT_LD + i] = lic;
         }
+        if (h == hc) a[qc] = (i == c) ? lcc : ((i > c) ? lic : a[qc]);
         if (lane == 0) {
-          Dk[c * TT_LD + c] = lcc;
           rd[c] = rl;
           rdall[TT * k + c] = rl;
         }
         gr_sync();
       }
+      if (!bad) {
+#pragma unroll
+        for (int q2 = 0; q2 < TT / 2; ++q2) Dk[(2 * q2 + h) * TT_LD + i] = a[q2];
+      }
+      gr_sync();
       if (bad) {
         if (lane == 0) fail = 1;
       } else {
@@ -910,32 +915,50 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   if (w == 0) {
     const int i = lane & 31;
     double yc = 0.0;
+    // every tile's L entries are loaded into registers ahead of the dependent FMA chains (fully
+    // unrolled: the workspace loads of a tile issue together instead of one per step)
     for (int I = 0; I < T; ++I) {
       double r = yv[TT * I + i];
+      double lm[TT];
+      const double* LD_ = Lt + tile_at(I, I);
+#pragma unroll
+      for (int m = 0; m < TT; ++m) lm[m] = LD_[m * TT + i];
       for (int J = 0; J < I; ++J) {
         const double* L = Lt + tile_at(I, J);
-        for (int j = 0; j < TT; ++j) r = fma(-L[j * TT + i], uv[TT * J + j], r);
+        double lj[TT];
+#pragma unroll
+        for (int j = 0; j < TT; ++j) lj[j] = L[j * TT + i];
+#pragma unroll
+        for (int j = 0; j < TT; ++j) r = fma(-lj[j], uv[TT * J + j], r);
       }
-      const double* L = Lt + tile_at(I, I);
+#pragma unroll
       for (int m = 0; m < TT; ++m) {
         const double zm = readlane_d(r, m) * rdall[TT * I + m];
         if (i == m) r = zm;
-        else if (i > m) r = fma(-L[m * TT + i], zm, r);
+        else if (i > m) r = fma(-lm[m], zm, r);
       }
       if (lane < TT) uv[TT * I + i] = r;   // z
       gr_sync();
     }
     for (int I = T - 1; I >= 0; --I) {
       double r = uv[TT * I + i];
+      double lm[TT];
+      const double* LD_ = Lt + tile_at(I, I);
+#pragma unroll
+      for (int m = 0; m < TT; ++m) lm[m] = LD_[i * TT + m];
       for (int J = I + 1; J < T; ++J) {
         const double* L = Lt + tile_at(J, I);
-        for (int j = 0; j < TT; ++j) r = fma(-L[i * TT + j], yv[TT * J + j], r);
+        double lj[TT];
+#pragma unroll
+        for (int j = 0; j < TT; ++j) lj[j] = L[i * TT + j];
+#pragma unroll
+        for (int j = 0; j < TT; ++j) r = fma(-lj[j], yv[TT * J + j], r);
       }
-      const double* L = Lt + tile_at(I, I);
+#pragma unroll
       for (int m = TT - 1; m >= 0; --m) {
         const double cm = readlane_d(r, m) * rdall[TT * I + m];
         if (i == m) r = cm;
-        else if (i < m) r = fma(-L[i * TT + m], cm, r);
+        else if (i < m) r = fma(-lm[m], cm, r);
       }
       gr_sync();
       if (lane < TT) {
