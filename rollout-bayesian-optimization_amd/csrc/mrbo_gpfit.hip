@@ -705,7 +705,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (p >= P) return;   // whole workgroups
 #ifdef MRBO_GPFIT_STAMPS
-  unsigned long long tt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tt_last = __builtin_amdgcn_s_memtime();
+  unsigned long long tt_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tt_last = __builtin_amdgcn_s_memtime();
 #endif
   const int N = q.N, d = q.d, T = (N + TT - 1) / TT, NP = T * TT;
   double* XS = tsm;                      // X[u][i] at u·NP + i, zero-padded
@@ -801,6 +801,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
         for (int q2 = 0; q2 < TT / 2; ++q2) Dk[(2 * q2 + h) * TT_LD + i] = a[q2];
       }
       gr_sync();
+      TT_STAMP(8);
       if (bad) {
         if (lane == 0) fail = 1;
       } else {
@@ -825,6 +826,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
           for (int r = 0; r < TT; ++r) Wk[lane * TT_LD + r] = wc[r];
         }
         gr_sync();
+        TT_STAMP(9);
         double* Lkk = Lt + tile_at(k, k);
         double* Vkk = Vt + tile_at(k, k);
         double* Wkk = Wt + (size_t)k * (TT * TT);
@@ -834,6 +836,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
           Wkk[e] = Wk[cc * TT_LD + r];
           Vkk[r * TT + cc] = Wk[cc * TT_LD + r];              // row-major copy: V_kk = W_k
         }
+        TT_STAMP(10);
       }
     }
     __syncthreads();
@@ -1020,8 +1023,9 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   }
 #ifdef MRBO_GPFIT_STAMPS
   if (p == 0 && tid == 0)
-    printf("gpfit_tile N=%d cycles: K %llu  diag %llu  panel %llu  trailing %llu  V %llu  c %llu  traces %llu\n", N,
-           tt_acc[1], tt_acc[2], tt_acc[3], tt_acc[4], tt_acc[5], tt_acc[6], tt_acc[7]);
+    printf("gpfit_tile N=%d cycles: K %llu  diag %llu (factor %llu, W %llu, copy %llu, wait %llu)  panel %llu  trailing %llu  "
+           "V %llu  c %llu  traces %llu\n", N, tt_acc[1], tt_acc[2] + tt_acc[8] + tt_acc[9] + tt_acc[10], tt_acc[8],
+           tt_acc[9], tt_acc[10], tt_acc[2], tt_acc[3], tt_acc[4], tt_acc[5], tt_acc[6], tt_acc[7]);
 #endif
   if (q.L_out) {
     double* Lo = q.L_out + (size_t)N * N * p;
