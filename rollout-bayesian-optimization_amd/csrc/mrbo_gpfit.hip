@@ -758,47 +758,36 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       // A_kk → L_kk in LDS (right-looking; PosDefException → status 1), then W_k = L_kk⁻¹
       const int i = lane & 31, h = lane >> 5;
       const double* A = Lt + tile_at(k, k);
-      // A_kk → L_kk with the rows in registers: lane (i, h) holds a_ij for the columns j = 2q + h
-      // (i = lane & 31, h = lane >> 5).  Per column c the pivot comes by readlane, a_ic from the
-      // partner half by one swap, and column c of L reaches every lane through one LDS broadcast;
-      // the rank-1 update is then 16 predicated FMAs per lane on registers.
+      // A_kk → L_kk with row i of the tile in lane i's registers (lanes 32..63 mirror 0..31).  Per
+      // column c the pivot and then each l_jc (j > c) come from lane j by readlane into scalar
+      // registers, which the FMAs of the rank-1 update take as operands: no LDS round trip and no
+      // wave barrier on the pivot chain.  Entries right of the diagonal are updated too (they are
+      // never read) so that no lane needs a mask.
       bool bad = false;
-      double a[TT / 2];
+      double a[TT];
 #pragma unroll
-      for (int q2 = 0; q2 < TT / 2; ++q2) a[q2] = A[(2 * q2 + h) * TT + i];
-      double* colc = Wk;   // column c of L (32 doubles); W_k is formed after the factorization
+      for (int j = 0; j < TT; ++j) a[j] = A[j * TT + i];
 #pragma unroll
       for (int c = 0; c < TT; ++c) {
-        const int qc = c >> 1, hc = c & 1;
-        const double piv = readlane_d(a[qc], c + 32 * hc);
+        const double piv = readlane_d(a[c], c);
         if (!(piv > 0.0)) {   // the same value in every lane: a uniform exit
           bad = true;
           break;
         }
         double lcc, rl;
         sqrt_rsqrt(piv, lcc, rl);
-        const double other = __shfl_xor(a[qc], 32, 64);
-        const double lic = ((h == hc) ? a[qc] : other) * rl;   // l_ic of this lane's row
-        if (h == 0) colc[i] = lic;
-        gr_sync();
+        const double lic = a[c] * rl;   // l_ic of this lane's row (meaningful for i > c)
 #pragma unroll
-        for (int q2 = 0; q2 < TT / 2; ++q2) {
-          if (2 * q2 + 1 > c) {   // some column j = 2·q2 + h of this slot lies right of c
-            const int j = 2 * q2 + h;
-            const double ljc = colc[j];
-            if ((j > c) & (j <= i)) a[q2] = fma(-lic, ljc, a[q2]);
-          }
-        }
-        if (h == hc) a[qc] = (i == c) ? lcc : ((i > c) ? lic : a[qc]);
+        for (int j = c + 1; j < TT; ++j) a[j] = fma(-lic, readlane_d(lic, j), a[j]);
+        a[c] = (i == c) ? lcc : ((i > c) ? lic : a[c]);
         if (lane == 0) {
           rd[c] = rl;
           rdall[TT * k + c] = rl;
         }
-        gr_sync();
       }
       if (!bad) {
 #pragma unroll
-        for (int q2 = 0; q2 < TT / 2; ++q2) Dk[(2 * q2 + h) * TT_LD + i] = a[q2];
+        for (int j = 0; j < TT; ++j) Dk[j * TT_LD + i] = a[j];
       }
       gr_sync();
       TT_STAMP(8);
