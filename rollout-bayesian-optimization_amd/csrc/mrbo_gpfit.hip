@@ -97,6 +97,13 @@ __device__ __forceinline__ void gr_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// Ordering of one wave's own LDS accesses: the LDS executes a wave's operations in issue order, so
+// a store followed by a load of the same address needs no wait -- only the compiler must not move
+// accesses across this point (no instruction is emitted)
+__device__ __forceinline__ void lds_order() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 
 // a[j/16][j%16] += L[j][k]·m for j = k+1..63: the column (lane j holds L[j][k]) broadcast block by
 // block (replicated by permlane swaps, DPP row_newbcast inside the fused FMAs, gpfit_asm.h)
@@ -758,36 +765,49 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       // A_kk → L_kk in LDS (right-looking; PosDefException → status 1), then W_k = L_kk⁻¹
       const int i = lane & 31, h = lane >> 5;
       const double* A = Lt + tile_at(k, k);
-      // A_kk → L_kk with row i of the tile in lane i's registers (lanes 32..63 mirror 0..31).  Per
-      // column c the pivot and then each l_jc (j > c) come from lane j by readlane into scalar
-      // registers, which the FMAs of the rank-1 update take as operands: no LDS round trip and no
-      // wave barrier on the pivot chain.  Entries right of the diagonal are updated too (they are
-      // never read) so that no lane needs a mask.
+      // A_kk → L_kk with the rows in registers: lane (i, h) holds a_ij for the columns j = 2q + h
+      // (i = lane & 31, h = lane >> 5).  Per column c the pivot comes by readlane, a_ic from the
+      // partner half by one swap, and column c of L reaches every lane through one LDS broadcast;
+      // the rank-1 update is then 16 predicated FMAs per lane on registers.  (Broadcasting every
+      // l_jc by readlane into scalar FMA operands instead measured 2.6x slower: ≈ 500 readlane
+      // pairs per tile, each a VALU-to-SGPR round trip.)
       bool bad = false;
-      double a[TT];
+      double a[TT / 2];
 #pragma unroll
-      for (int j = 0; j < TT; ++j) a[j] = A[j * TT + i];
+      for (int q2 = 0; q2 < TT / 2; ++q2) a[q2] = A[(2 * q2 + h) * TT + i];
+      double* colc = Wk;   // column c of L (32 doubles); W_k is formed after the factorization
 #pragma unroll
       for (int c = 0; c < TT; ++c) {
-        const double piv = readlane_d(a[c], c);
+        const int qc = c >> 1, hc = c & 1;
+        const double piv = readlane_d(a[qc], c + 32 * hc);
         if (!(piv > 0.0)) {   // the same value in every lane: a uniform exit
           bad = true;
           break;
         }
         double lcc, rl;
         sqrt_rsqrt(piv, lcc, rl);
-        const double lic = a[c] * rl;   // l_ic of this lane's row (meaningful for i > c)
+        const double other = __shfl_xor(a[qc], 32, 64);
+        const double lic = ((h == hc) ? a[qc] : other) * rl;   // l_ic of this lane's row
+        if (h == 0) colc[i] = lic;
+        lds_order();   // one wave: its LDS operations execute in issue order, so no wait is needed
 #pragma unroll
-        for (int j = c + 1; j < TT; ++j) a[j] = fma(-lic, readlane_d(lic, j), a[j]);
-        a[c] = (i == c) ? lcc : ((i > c) ? lic : a[c]);
+        for (int q2 = 0; q2 < TT / 2; ++q2) {
+          if (2 * q2 + 1 > c) {   // some column j = 2·q2 + h of this slot lies right of c
+            const int j = 2 * q2 + h;
+            const double ljc = colc[j];
+            if ((j > c) & (j <= i)) a[q2] = fma(-lic, ljc, a[q2]);
+          }
+        }
+        if (h == hc) a[qc] = (i == c) ? lcc : ((i > c) ? lic : a[qc]);
         if (lane == 0) {
           rd[c] = rl;
           rdall[TT * k + c] = rl;
         }
+        lds_order();   // colc is rewritten by the next column after these reads were issued
       }
       if (!bad) {
 #pragma unroll
-        for (int j = 0; j < TT; ++j) Dk[j * TT_LD + i] = a[j];
+        for (int q2 = 0; q2 < TT / 2; ++q2) Dk[(2 * q2 + h) * TT_LD + i] = a[q2];
       }
       gr_sync();
       TT_STAMP(8);
