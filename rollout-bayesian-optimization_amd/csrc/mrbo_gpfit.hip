@@ -740,13 +740,18 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   for (int i = tid; i < NP; i += TT_THREADS) yv[i] = (i < N) ? q.y[i] : 0.0;
   __syncthreads();
   // K (eval_KXX :161-178, ψ(0) + σn2 on the diagonal), every entry of the lower tiles
-  for (size_t e = tid; e < ntile * (TT * TT); e += TT_THREADS) {
-    int I, J;
-    tile_ij((int)(e >> 10), I, J);
-    const int gi = TT * I + (int)(e & 31), gj = TT * J + (int)((e >> 5) & 31);
+  // (tile by tile: the tile's (I, J) once per tile instead of a square root per entry; the
+  // diagonal tiles' strict upper triangles are never read -- the factor, the copy-out and the
+  // traces take the lower part -- so they are zero-filled without a radial evaluation)
+  for (int qt = 0; qt < (int)ntile; ++qt) {
+   int I, J;
+   tile_ij(qt, I, J);
+   for (int el = tid; el < TT * TT; el += TT_THREADS) {
+    const size_t e = (size_t)qt * (TT * TT) + el;
+    const int gi = TT * I + (el & 31), gj = TT * J + (el >> 5);
     double v = (gi == gj) ? 1.0 : 0.0;
     double dps[2] = {0.0, 0.0};
-    if (gi < N && gj < N) {
+    if (gi < N && gj < N && gj <= gi) {
       double r2 = 0.0;
       for (int u = 0; u < d; ++u) { const double r = XS[u * NP + gi] - XS[u * NP + gj]; r2 = fma(r, r, r2); }
       double psi;
@@ -756,6 +761,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     Lt[e] = v;
 #pragma unroll
     for (int t = 0; t < NT; ++t) Dt[(size_t)t * ntile * (TT * TT) + e] = dps[t];   // the same bits the traces used to recompute
+   }
   }
   __syncthreads();
   TT_STAMP(1);
