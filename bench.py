@@ -62,7 +62,11 @@ def parse():
                          "kernel 0.56 -> 0.53 ms; at C3's 32 rounds it measured 1 %% slower; DESIGN.md §9)")
     ap.add_argument("--longest-first", action="store_true", help="same as --schedule longest-first")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--eta", type=float, default=0.01, help="StandardSGA step (optimizers.jl:6-23; default 0.01)")
+    ap.add_argument("--solver", choices=("sga", "adam"), default="sga",
+                    help="outer update!: StandardSGA (default) or Adam (optimizers.jl:25-74), both on the device")
+    ap.add_argument("--eta", type=float, default=0.0,
+                    help="step: default 0.01 for StandardSGA, 0.001 for Adam (the reference's defaults, "
+                         "optimizers.jl:10, 35)")
     ap.add_argument("--dump", default="", help="write the final ETO and x0 (npz) here (rank 0)")
     ap.add_argument("--sharded", action="store_true",
                     help="take the multi-rank path (process group, per-step all-gather of the shard moments, "
@@ -242,6 +246,9 @@ def main():
     dactive = torch.ones(R, dtype=torch.int32, device=dev)
     W = parallel.width(d)
     last = {}
+    eta = args.eta or (0.01 if args.solver == "sga" else 0.001)
+    if args.solver == "adam":   # Adam's moment estimates, resident beside x0 (m = v = 0 before update 1)
+        dm, dv = torch.zeros_like(dx0), torch.zeros_like(dx0)
 
     shard_sizes = [b - a for a, b in shards]
 
@@ -260,9 +267,14 @@ def main():
             # re-sorting every step costs more (≈ 0.09 ms at C2) than it gains
             plan.order_longest_first(out)
             last["ordered"] = True
-        # eswavs + StandardSGA of every active restart on the device (mrbo_sga_step): x0 and the
-        # stop flags stay in HBM, so the next launch follows without a host round trip
-        plan.sga_step(e, dx0, dactive, M_total, args.eta)
+        # eswavs + update! of every active restart on the device (mrbo_sga_step / mrbo_adam_step):
+        # x0, the stop flags and Adam's moments stay in HBM, so the next launch follows without a
+        # host round trip
+        if args.solver == "sga":
+            plan.sga_step(e, dx0, dactive, M_total, eta)
+        else:
+            last["t"] = last.get("t", 0) + 1
+            plan.adam_step(e, dx0, dactive, dm, dv, last["t"], M_total, eta)
         last["eto_dev"] = e
 
     for _ in range(args.warmup):
@@ -325,8 +337,10 @@ def main():
                                                                                  "ℓ = 1 (SURVEY §8d)"),
                    "rule": rule, "parallelism": f"mc-shard x{world}",
                    "exchange": "none" if not sharded else f"all-gather of (Σ, M2) moments, {W * R * 8} B/rank/step",
-                   "outer_step": f"eswavs + StandardSGA η={args.eta:g}, no clip (utils.jl:114-123, "
-                                 f"optimizers.jl:16-22)",
+                   "outer_step": (f"eswavs + StandardSGA η={eta:g}, no clip (utils.jl:114-123, optimizers.jl:16-22)"
+                                  if args.solver == "sga" else
+                                  f"eswavs + Adam η={eta:g} β=(0.9, 0.999) ε=1e-8 (utils.jl:114-123, "
+                                  f"optimizers.jl:49-74)"),
                    "schedule": "longest first (first step's work counters)" if longest_first else "index order"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,

@@ -189,6 +189,15 @@ int mrbo_eto_reduce(mrbo_plan_t* plan, const double* values, const double* grad_
 int mrbo_sga_step(mrbo_plan_t* plan, const double* eto, double* x0s, int32_t* active, double sample_size, double eta,
                   uint32_t flags, void* stream);
 
+/* The same step with Adam update! (optimizers.jl:49-74) in place of StandardSGA: m, v (device,
+ * d×R, zero before the first update) are the restarts' moment estimates, t ≥ 1 the update count
+ * of the active restarts (a restart that eswavs stops never updates again, so the active ones
+ * share it); x0s[:, r] += η·m̂/(√v̂ + ε) with m̂ = m/(1 − β1^t), v̂ = v/(1 − β2^t).  The reference's
+ * defaults: η = 0.001, β1 = 0.9, β2 = 0.999, ε = 1e-8 (optimizers.jl:35-40).                 */
+int mrbo_adam_step(mrbo_plan_t* plan, const double* eto, double* x0s, int32_t* active, double* m, double* v, int32_t t,
+                   double sample_size, double eta, double beta1, double beta2, double eps, uint32_t flags,
+                   void* stream);
+
 /* Shard moments for the multi-GPU exchange: moments R×(2+2d+2) = [Σα, M2α, Σ∇x(d), M2∇x(d), Σ∇θ, M2∇θ]
  * over the first M_local samples of each restart (the outputs keep the plan's M as the restart
  * stride; 1 ≤ M_local ≤ M), M2 = Σ(x − x̄_local)² by two passes.  Ranks all-gather

@@ -210,24 +210,55 @@ __global__ void __launch_bounds__(256) reduce_kernel(const double* values, const
 
 // ---- outer ascent step on the device (stochastic_solve utils.jl:235-265): per active restart r,
 // eswavs (utils.jl:114-123) on the ETO's ∇μx and σ_∇μx -- stop when 1 − (M/d)·Σ_a ∇_a²/σ_a² > 0 (a
-// NaN ratio keeps iterating, as in Julia) -- else StandardSGA update! x += η·∇ (optimizers.jl:16-22).
-// One thread per restart; the x0 batch never leaves the device between launches.
-__global__ void __launch_bounds__(64) sga_kernel(const double* eto, double* x0s, int* active, int R, int d,
-                                                 double sample_size, double eta) {
+// NaN ratio keeps iterating, as in Julia) -- else the optimizer's update! of x (StandardSGA
+// optimizers.jl:16-22 or Adam :49-74).  One thread per restart; the x0 batch and the Adam moments
+// never leave the device between launches.
+__device__ __forceinline__ bool eswavs_stops(const double* e, int d, double sample_size) {
 #pragma clang fp contract(off)   // the host mirror's (numpy) roundings: no fused multiply-adds
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R || !active[r]) return;
-  const double* e = eto + (size_t)(2 + 2 * d + 2) * r;
   double ratio = 0.0;
   for (int a = 0; a < d; ++a) {
     const double g = e[2 + a], s = e[2 + d + a];
     ratio += (g * g) / (s * s);
   }
-  if (1.0 - (sample_size / d) * ratio > 0.0) {
+  return 1.0 - (sample_size / d) * ratio > 0.0;
+}
+
+__global__ void __launch_bounds__(64) sga_kernel(const double* eto, double* x0s, int* active, int R, int d,
+                                                 double sample_size, double eta) {
+#pragma clang fp contract(off)
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R || !active[r]) return;
+  const double* e = eto + (size_t)(2 + 2 * d + 2) * r;
+  if (eswavs_stops(e, d, sample_size)) {
     active[r] = 0;
     return;
   }
   for (int a = 0; a < d; ++a) x0s[(size_t)d * r + a] = x0s[(size_t)d * r + a] + eta * e[2 + a];
+}
+
+// Adam update! (optimizers.jl:49-74) with its moments m, v (d×R) kept on the device: m ← β1·m +
+// (1−β1)·∇, v ← β2·v + (1−β2)·∇², x += η·(m/c1) / (√(v/c2) + ε), c1 = 1 − β1^t and c2 = 1 − β2^t
+// formed on the host (the same pow as the host mirror's).  sqrt and division are IEEE-rounded.
+__global__ void __launch_bounds__(64) adam_kernel(const double* eto, double* x0s, int* active, double* m, double* v,
+                                                  int R, int d, double sample_size, double eta, double b1, double b2,
+                                                  double eps, double c1, double c2) {
+#pragma clang fp contract(off)
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R || !active[r]) return;
+  const double* e = eto + (size_t)(2 + 2 * d + 2) * r;
+  if (eswavs_stops(e, d, sample_size)) {
+    active[r] = 0;
+    return;
+  }
+  for (int a = 0; a < d; ++a) {
+    const size_t k = (size_t)d * r + a;
+    const double g = e[2 + a];
+    const double mk = b1 * m[k] + (1.0 - b1) * g;
+    const double vk = b2 * v[k] + (1.0 - b2) * (g * g);
+    m[k] = mk;
+    v[k] = vk;
+    x0s[k] = x0s[k] + (eta * (mk / c1)) / (__builtin_sqrt(vk / c2) + eps);
+  }
 }
 
 // ---- multi-GPU exchange on the device: Chan merge of the all-gathered shard moments ---------
@@ -794,6 +825,21 @@ int mrbo_sga_step(mrbo_plan_t* P, const double* eto, double* x0s, int32_t* activ
   const int R = P->p.R;
   hipLaunchKernelGGL(sga_kernel, dim3((R + 63) / 64), dim3(64), 0, (hipStream_t)stream, eto, x0s, (int*)active, R, P->d,
                      sample_size, eta);
+  HIP_TRY(hipGetLastError());
+  return MRBO_OK;
+}
+
+int mrbo_adam_step(mrbo_plan_t* P, const double* eto, double* x0s, int32_t* active, double* m, double* v, int32_t t,
+                   double sample_size, double eta, double beta1, double beta2, double eps, uint32_t flags,
+                   void* stream) {
+  if (!P || !eto || !x0s || !active || !m || !v) return fail(MRBO_ERR_ARG, "null argument");
+  if (flags & MRBO_FLAG_HOST_POINTERS) return fail(MRBO_ERR_ARG, "mrbo_adam_step takes device pointers");
+  if (t < 1) return fail(MRBO_ERR_ARG, "t=%d: the update count starts at 1", t);
+  if (hipSetDevice(P->device) != hipSuccess) return fail(MRBO_ERR_HIP, "hipSetDevice");
+  const int R = P->p.R;
+  const double c1 = 1.0 - std::pow(beta1, (double)t), c2 = 1.0 - std::pow(beta2, (double)t);
+  hipLaunchKernelGGL(adam_kernel, dim3((R + 63) / 64), dim3(64), 0, (hipStream_t)stream, eto, x0s, (int*)active, m, v,
+                     R, P->d, sample_size, eta, beta1, beta2, eps, c1, c2);
   HIP_TRY(hipGetLastError());
   return MRBO_OK;
 }

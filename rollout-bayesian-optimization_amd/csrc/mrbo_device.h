@@ -160,6 +160,17 @@ __device__ __forceinline__ void row_blocks(double v, double& blk_p, double& blk_
   blk_p2 = djoin(c[1], d[1]);
 }
 
+// The value of lane (l & 31) + 32·H in every lane l: one v_permlane32_swap per dword of the
+// register with itself leaves the lower half's values in both halves of the first result and the
+// upper half's in both halves of the second (H a compile-time constant after unrolling).
+__device__ __forceinline__ double half_value(double v, int H) {
+  int lo, hi;
+  dsplit(v, lo, hi);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return H ? djoin(a[1], b[1]) : djoin(a[0], b[0]);
+}
+
 // M = 8, 4, 2, 1: v from a partner lane that differs in bit M and agrees on all higher bits
 // (DPP row_mirror, row_half_mirror, quad_perm xor2 / xor1 -- one VALU move per dword).
 template <int M>

@@ -786,22 +786,21 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       for (int c = 0; c < TT; ++c) {
         const int qc = c >> 1, hc = c & 1;
         const double piv = readlane_d(a[qc], c + 32 * hc);
-        if (!(piv > 0.0)) {   // the same value in every lane: a uniform exit
-          bad = true;
-          break;
-        }
+        // no early exit (a non-positive pivot sets `bad`; the remaining columns run on values that
+        // are discarded), so the column loop unrolls completely: every register index and the
+        // readlane lane are compile-time constants, and the update is selects, not branches
+        bad = bad || !(piv > 0.0);
         double lcc, rl;
         sqrt_rsqrt(piv, lcc, rl);
-        const double other = __shfl_xor(a[qc], 32, 64);
-        const double lic = ((h == hc) ? a[qc] : other) * rl;   // l_ic of this lane's row
+        const double lic = half_value(a[qc], hc) * rl;   // l_ic of this lane's row
         if (h == 0) colc[i] = lic;
         lds_order();   // one wave: its LDS operations execute in issue order, so no wait is needed
 #pragma unroll
         for (int q2 = 0; q2 < TT / 2; ++q2) {
           if (2 * q2 + 1 > c) {   // some column j = 2·q2 + h of this slot lies right of c
             const int j = 2 * q2 + h;
-            const double ljc = colc[j];
-            if ((j > c) & (j <= i)) a[q2] = fma(-lic, ljc, a[q2]);
+            const double upd = fma(-lic, colc[j], a[q2]);
+            a[q2] = ((j > c) & (j <= i)) ? upd : a[q2];
           }
         }
         if (h == hc) a[qc] = (i == c) ? lcc : ((i > c) ? lic : a[qc]);

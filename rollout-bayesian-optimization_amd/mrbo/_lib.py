@@ -35,7 +35,7 @@ EXPORTS = [
     "mrbo_simulate_mc", "mrbo_simulate_ghq", "mrbo_eto_reduce", "mrbo_partial_moments", "mrbo_eval_base", "mrbo_rnstream",
     "mrbo_initial_guesses", "mrbo_dual_uniform", "mrbo_last_kernel_ms", "mrbo_gp_fit", "mrbo_gp_fit_theta",
     "mrbo_plan_info", "mrbo_last_gp_fit_ms", "mrbo_plan_set_order", "mrbo_base_solve", "mrbo_sga_step",
-    "mrbo_kernel_times", "mrbo_merge_moments",
+    "mrbo_kernel_times", "mrbo_merge_moments", "mrbo_adam_step",
 ]
 
 
@@ -89,6 +89,8 @@ def load():
     L.mrbo_partial_moments.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_int32, _vp, ctypes.c_uint32, _vp]
     L.mrbo_eval_base.argtypes = [_vp, ctypes.c_int32, _vp, _vp, ctypes.c_uint32, _vp]
     L.mrbo_sga_step.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_uint32, _vp]
+    L.mrbo_adam_step.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int32] + [ctypes.c_double] * 5 + [
+        ctypes.c_uint32, _vp]
     L.mrbo_base_solve.argtypes = [_vp, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]
     L.mrbo_rnstream.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _dp]
     L.mrbo_initial_guesses.argtypes = [ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp]

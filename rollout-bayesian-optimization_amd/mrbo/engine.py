@@ -169,6 +169,18 @@ class RolloutPlan:
         _lib.check(self.lib.mrbo_sga_step(self.handle, p(eto), p(x0s), p(active), float(sample_size), float(eta), 0,
                                           ctypes.c_void_p(st.cuda_stream)))
 
+    def adam_step(self, eto, x0s, active, m, v, t, sample_size, eta=0.001, beta1=0.9, beta2=0.999, eps=1e-8,
+                  stream=None):
+        """mrbo_adam_step: eswavs + Adam update! (optimizers.jl:49-74) for every active restart, in
+        place on the device tensors x0s, m, v (d·R, column-major, m = v = 0 before update 1) and
+        active (R, int32); t is this update's count (1, 2, ...)."""
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        p = lambda t_: ctypes.c_void_p(t_.data_ptr())
+        _lib.check(self.lib.mrbo_adam_step(self.handle, p(eto), p(x0s), p(active), p(m), p(v), int(t),
+                                           float(sample_size), float(eta), float(beta1), float(beta2), float(eps), 0,
+                                           ctypes.c_void_p(st.cuda_stream)))
+
     def eval_base(self, xs):
         """eval(s, x, θ) at the columns of xs (d×P); returns (3+4d+d²)×P numpy."""
         torch = _torch()

@@ -89,6 +89,25 @@ def sga_step_batch(x0, active, grad, std_grad, sample_size, eta, lbs=None, ubs=N
     return x0, active
 
 
+def adam_step_batch(x0, active, m, v, t, grad, std_grad, sample_size, eta=0.001, beta1=0.9, beta2=0.999, eps=1e-8):
+    """sga_step_batch with Adam update! (optimizers.jl:49-74) in place of StandardSGA, in place on
+    x0, m, v (d×R) and active: t is the update count of the active restarts (1 on the first
+    update; a stopped restart never updates again, so they share it).  Per column exactly the
+    arithmetic of mrbo.optimizers.Adam.update."""
+    d = x0.shape[0]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ratio = np.sum(grad ** 2 / std_grad ** 2, axis=0)
+    active &= ~((1.0 - (sample_size / d) * ratio) > 0.0)
+    if active.any():
+        g = grad[:, active]
+        m[:, active] = beta1 * m[:, active] + (1 - beta1) * g
+        v[:, active] = beta2 * v[:, active] + (1 - beta2) * g ** 2
+        m_hat = m[:, active] / (1 - beta1 ** t)
+        v_hat = v[:, active] / (1 - beta2 ** t)
+        x0[:, active] = x0[:, active] + eta * m_hat / (np.sqrt(v_hat) + eps)
+    return x0, active
+
+
 class ExperimentSetup:
     """utils.jl:174-208"""
 

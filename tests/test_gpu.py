@@ -280,3 +280,33 @@ def test_device_sga_step_matches_host(gpu):
         sga_step_batch(x0, active, eto[2:2 + d], eto[2 + d:2 + 2 * d], sample_size, 0.01)
         np.testing.assert_array_equal(from_device(dx, (d, R)), x0)
         np.testing.assert_array_equal(da.cpu().numpy().astype(bool), active)
+
+
+def test_device_adam_step_matches_host(gpu):
+    """mrbo_adam_step (eswavs + Adam update!, optimizers.jl:49-74, moments kept on the device)
+    against the host mirror adam_step_batch over consecutive updates, bit for bit: x, m, v and the
+    active flags after every step, including steps where the stop rule retires restarts."""
+    import torch
+    from mrbo.engine import from_device, to_device
+    from mrbo.utils import adam_step_batch
+    g = _problem_arrays("C3", 32, 8)
+    p = _plan(g)
+    r = _run(p, g, want_policy=False)
+    d, R = p.d, p.R
+    eto0 = np.asfortranarray(r["eto"])
+    x0 = np.array(g["x0s"], dtype=np.float64, order="F")
+    m, v = np.zeros((d, R), order="F"), np.zeros((d, R), order="F")
+    active = np.ones(R, dtype=bool)
+    active[3] = False
+    dx, dm, dv = (to_device(a, "cuda:0") for a in (x0, m, v))
+    da = torch.tensor(active.astype(np.int32), device="cuda:0")
+    for t, sample_size in enumerate((32.0, 1e6, 32.0, 1e-3, 32.0), start=1):
+        eto = eto0.copy(order="F")
+        eto[2:2 + d] *= (1.0 + 0.25 * t) * (-1.0) ** t
+        p.adam_step(to_device(eto, "cuda:0"), dx, da, dm, dv, t, sample_size, eta=0.02)
+        torch.cuda.synchronize()
+        adam_step_batch(x0, active, m, v, t, eto[2:2 + d], eto[2 + d:2 + 2 * d], sample_size, eta=0.02)
+        np.testing.assert_array_equal(da.cpu().numpy().astype(bool), active)
+        np.testing.assert_array_equal(from_device(dm, (d, R)), m)
+        np.testing.assert_array_equal(from_device(dv, (d, R)), v)
+        np.testing.assert_array_equal(from_device(dx, (d, R)), x0)

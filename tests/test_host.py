@@ -282,3 +282,34 @@ def test_sga_step_batch_equals_per_restart_rules():
         x2, a2 = sga_step_batch(x.copy(), act.copy(), g, sd, M, 0.01, lbs, ubs, clip=clip)
         assert (a1 == a2).all()
         np.testing.assert_array_equal(x1, x2)
+
+
+def test_adam_step_batch_equals_per_restart_rules():
+    """The vectorised Adam outer step == eswavs + Adam.update! per restart (optimizers.jl:49-74)
+    over consecutive steps: one optimizer per restart, a stopped restart never updates again."""
+    from mrbo.optimizers import Adam
+    from mrbo.utils import adam_step_batch, eswavs
+    rng = np.random.default_rng(1)
+    d, R, M = 5, 48, 1024
+    x = rng.random((d, R))
+    act = rng.random(R) > 0.1
+    x1, a1, opts = x.copy(), act.copy(), [Adam(η=0.05) for _ in range(R)]
+    x2, a2, m, v = x.copy(), act.copy(), np.zeros((d, R)), np.zeros((d, R))
+    for t in range(1, 8):
+        g = rng.standard_normal((d, R)) * rng.choice([1e-3, 1.0, 1e3])
+        sd = np.abs(rng.standard_normal((d, R))) * rng.choice([1e-2, 1.0, 30.0])
+        g[0, rng.integers(0, R, 1)] = np.nan
+        for r in range(R):
+            if not a1[r]:
+                continue
+            if eswavs(g[:, r], sd[:, r] ** 2, M):
+                a1[r] = False
+                continue
+            opts[r].update(x1[:, r], g[:, r])
+        adam_step_batch(x2, a2, m, v, t, g, sd, M, eta=0.05)
+        assert (a1 == a2).all()
+        np.testing.assert_array_equal(x1, x2)
+        for r in np.flatnonzero(a1):
+            assert opts[r].t == t
+            np.testing.assert_array_equal(opts[r].m[-1], m[:, r])
+            np.testing.assert_array_equal(opts[r].v[-1], v[:, r])
