@@ -743,25 +743,39 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   // (tile by tile: the tile's (I, J) once per tile instead of a square root per entry; the
   // diagonal tiles' strict upper triangles are never read -- the factor, the copy-out and the
   // traces take the lower part -- so they are zero-filled without a radial evaluation)
+  // Each thread takes TT²/TT_THREADS = 4 entries of a tile -- one row gi, columns gj + 8m --
+  // as four independent chains (one wave per SIMD: the chains' interleaving is the latency
+  // hiding), with the row's coordinates loaded once per dimension.
+  static_assert(TT * TT == 4 * TT_THREADS, "K pass: four entries per thread and tile");
   for (int qt = 0; qt < (int)ntile; ++qt) {
-   int I, J;
-   tile_ij(qt, I, J);
-   for (int el = tid; el < TT * TT; el += TT_THREADS) {
-    const size_t e = (size_t)qt * (TT * TT) + el;
-    const int gi = TT * I + (el & 31), gj = TT * J + (el >> 5);
-    double v = (gi == gj) ? 1.0 : 0.0;
-    double dps[2] = {0.0, 0.0};
-    if (gi < N && gj < N && gj <= gi) {
-      double r2 = 0.0;
-      for (int u = 0; u < d; ++u) { const double r = XS[u * NP + gi] - XS[u * NP + gj]; r2 = fma(r, r, r2); }
-      double psi;
-      psi_dtheta(q.kernel, ell, per, (gi == gj) ? 0.0 : sqrt(r2), psi, dps);
-      v = (gi == gj) ? psi + q.sn2 : psi;
-    }
-    Lt[e] = v;
+    int I, J;
+    tile_ij(qt, I, J);
+    const int gi = TT * I + (tid & 31), gj0 = TT * J + (tid >> 5);
+    double r2[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int u = 0; u < d; ++u) {
+      const double* xu = XS + (size_t)u * NP;
+      const double xi = xu[gi];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) Dt[(size_t)t * ntile * (TT * TT) + e] = dps[t];   // the same bits the traces used to recompute
-   }
+      for (int m = 0; m < 4; ++m) {
+        const double r = xi - xu[gj0 + 8 * m];
+        r2[m] = fma(r, r, r2[m]);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int gj = gj0 + 8 * m;
+      const size_t e = (size_t)qt * (TT * TT) + tid + TT_THREADS * m;
+      double v = (gi == gj) ? 1.0 : 0.0;
+      double dps[2] = {0.0, 0.0};
+      if (gi < N && gj < N && gj <= gi) {
+        double psi;
+        psi_dtheta(q.kernel, ell, per, (gi == gj) ? 0.0 : sqrt(r2[m]), psi, dps);
+        v = (gi == gj) ? psi + q.sn2 : psi;
+      }
+      Lt[e] = v;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) Dt[(size_t)t * ntile * (TT * TT) + e] = dps[t];   // the same bits the traces used to recompute
+    }
   }
   __syncthreads();
   TT_STAMP(1);
