@@ -834,21 +834,19 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
         if (lane == 0) fail = 1;
       } else {
         if (lane < TT && TT * k + lane < N) lgl += log(Dk[lane * TT_LD + lane]);
-        // W column j = lane (< 32): W_ij = (δ_ij − Σ_{m<i} L_im W_mj)/L_ii, rows ascending, the
-        // column in registers (W_mj = 0 for m < j comes out of the same recursion); two partial
-        // sums halve the dependent chain
+        // W column j = lane (< 32): W_ij = (δ_ij − Σ_{m<i} L_im W_mj)/L_ii, the column in
+        // registers, column-oriented: once W_mj is final it is eliminated from every later row
+        // (W_mj = 0 for m < j comes out of the same recursion).  The dependent chain is two
+        // operations per row; the 31 − m updates of a step are independent.
         if (lane < TT) {
           double wc[TT];
 #pragma unroll
-          for (int r = 0; r < TT; ++r) {
-            double s0 = (r == lane) ? 1.0 : 0.0, s1 = 0.0;
+          for (int r = 0; r < TT; ++r) wc[r] = (r == lane) ? 1.0 : 0.0;
 #pragma unroll
-            for (int m = 0; m + 1 < r; m += 2) {
-              s0 = fma(-Dk[m * TT_LD + r], wc[m], s0);
-              s1 = fma(-Dk[(m + 1) * TT_LD + r], wc[m + 1], s1);
-            }
-            if (r & 1) s0 = fma(-Dk[(r - 1) * TT_LD + r], wc[r - 1], s0);
-            wc[r] = (s0 + s1) * rd[r];
+          for (int m = 0; m < TT; ++m) {
+            wc[m] *= rd[m];
+#pragma unroll
+            for (int r = m + 1; r < TT; ++r) wc[r] = fma(-Dk[m * TT_LD + r], wc[m], wc[r]);
           }
 #pragma unroll
           for (int r = 0; r < TT; ++r) Wk[lane * TT_LD + r] = wc[r];
@@ -872,22 +870,21 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     if (fail) break;
     // panel: L_Ik = A_Ik·L_kk⁻ᵀ by forward substitution, one row per lane (lanes < 32), the row in
     // registers: L_Ik[r][c] = (A_Ik[r][c] − Σ_{m<c} L_Ik[r][m]·L_kk[c][m]) / L_kk[c][c], the
-    // factor's own recurrence (a product with the explicit inverse W_k is ≈ κ(L_kk) less accurate)
+    // factor's own recurrence (a product with the explicit inverse W_k is ≈ κ(L_kk) less accurate),
+    // column-oriented: entry m, once final, is eliminated from every later column (independent
+    // updates; the dependent chain is two operations per column)
     for (int I = k + 1 + w; I < T; I += 4) {
       double* A = Lt + tile_at(I, k);
       if (lane < TT) {
         const int r = lane;
         double lrow[TT];
 #pragma unroll
-        for (int c = 0; c < TT; ++c) {
-          double v0 = A[c * TT + r], v1 = 0.0;
+        for (int c = 0; c < TT; ++c) lrow[c] = A[c * TT + r];
 #pragma unroll
-          for (int m = 0; m + 1 < c; m += 2) {
-            v0 = fma(-lrow[m], Dk[m * TT_LD + c], v0);
-            v1 = fma(-lrow[m + 1], Dk[(m + 1) * TT_LD + c], v1);
-          }
-          if (c & 1) v0 = fma(-lrow[c - 1], Dk[(c - 1) * TT_LD + c], v0);
-          lrow[c] = (v0 + v1) * rd[c];
+        for (int m = 0; m < TT; ++m) {
+          lrow[m] *= rd[m];
+#pragma unroll
+          for (int c = m + 1; c < TT; ++c) lrow[c] = fma(-lrow[m], Dk[m * TT_LD + c], lrow[c]);
         }
 #pragma unroll
         for (int c = 0; c < TT; ++c) A[c * TT + r] = lrow[c];
