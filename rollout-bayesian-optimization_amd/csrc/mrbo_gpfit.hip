@@ -945,20 +945,31 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     double yc = 0.0;
     // every tile's L entries are loaded into registers ahead of the dependent FMA chains (fully
     // unrolled: the workspace loads of a tile issue together instead of one per step)
+    // (the off-diagonal tiles of a block row are software-pipelined: tile J + 1's loads are in
+    // flight during tile J's products, which run as four partial sums)
     for (int I = 0; I < T; ++I) {
       double r = yv[TT * I + i];
-      double lm[TT];
+      double lm[TT], lj[TT];
       const double* LD_ = Lt + tile_at(I, I);
 #pragma unroll
       for (int m = 0; m < TT; ++m) lm[m] = LD_[m * TT + i];
-      for (int J = 0; J < I; ++J) {
-        const double* L = Lt + tile_at(I, J);
-        double lj[TT];
+      if (I > 0) {
 #pragma unroll
-        for (int j = 0; j < TT; ++j) lj[j] = L[j * TT + i];
-#pragma unroll
-        for (int j = 0; j < TT; ++j) r = fma(-lj[j], uv[TT * J + j], r);
+        for (int j = 0; j < TT; ++j) lj[j] = Lt[tile_at(I, 0) + j * TT + i];
       }
+      double r4[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int J = 0; J < I; ++J) {
+        double cur[TT];
+#pragma unroll
+        for (int j = 0; j < TT; ++j) cur[j] = lj[j];
+        if (J + 1 < I) {
+#pragma unroll
+          for (int j = 0; j < TT; ++j) lj[j] = Lt[tile_at(I, J + 1) + j * TT + i];
+        }
+#pragma unroll
+        for (int j = 0; j < TT; ++j) r4[j & 3] = fma(-cur[j], uv[TT * J + j], r4[j & 3]);
+      }
+      r += (r4[0] + r4[1]) + (r4[2] + r4[3]);
 #pragma unroll
       for (int m = 0; m < TT; ++m) {
         const double zm = readlane_d(r, m) * rdall[TT * I + m];
@@ -970,18 +981,27 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     }
     for (int I = T - 1; I >= 0; --I) {
       double r = uv[TT * I + i];
-      double lm[TT];
+      double lm[TT], lj[TT];
       const double* LD_ = Lt + tile_at(I, I);
 #pragma unroll
       for (int m = 0; m < TT; ++m) lm[m] = LD_[i * TT + m];
-      for (int J = I + 1; J < T; ++J) {
-        const double* L = Lt + tile_at(J, I);
-        double lj[TT];
+      if (I + 1 < T) {
 #pragma unroll
-        for (int j = 0; j < TT; ++j) lj[j] = L[i * TT + j];
-#pragma unroll
-        for (int j = 0; j < TT; ++j) r = fma(-lj[j], yv[TT * J + j], r);
+        for (int j = 0; j < TT; ++j) lj[j] = Lt[tile_at(I + 1, I) + i * TT + j];
       }
+      double r4[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int J = I + 1; J < T; ++J) {
+        double cur[TT];
+#pragma unroll
+        for (int j = 0; j < TT; ++j) cur[j] = lj[j];
+        if (J + 1 < T) {
+#pragma unroll
+          for (int j = 0; j < TT; ++j) lj[j] = Lt[tile_at(J + 1, I) + i * TT + j];
+        }
+#pragma unroll
+        for (int j = 0; j < TT; ++j) r4[j & 3] = fma(-cur[j], yv[TT * J + j], r4[j & 3]);
+      }
+      r += (r4[0] + r4[1]) + (r4[2] + r4[3]);
 #pragma unroll
       for (int m = TT - 1; m >= 0; --m) {
         const double cm = readlane_d(r, m) * rdall[TT * I + m];
