@@ -1027,27 +1027,34 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   for (int pi = w; pi < (int)ntile; pi += 4) {
     int I, J;
     tile_ij(pi, I, J);
+    // this lane's δK_t entries of the tile (from the K pass) and c_i·c_j, loaded before the
+    // products so that their latency hides behind the MFMA chain
+    double dk[NT][16], cc[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int bi = e >> 3, bj = (e >> 2) & 1, j = e & 3;
+      const int li = 16 * bi + (lane >> 4) + 4 * j, lj = 16 * bj + (lane & 15);
+      cc[e] = yv[TT * I + li] * yv[TT * J + lj];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) dk[t][e] = Dt[(size_t)t * ntile * (TT * TT) + tile_at(I, J) + lj * TT + li];
+    }
     f64x4 c[2][2];
     tile_zero(c);
     for (int M = I; M < T; ++M) tile_xyt<false>(c, Vt + tile_at(M, I), Vt + tile_at(M, J), lane);   // V_MIᵀ·V_MJ
 #pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
+    for (int e = 0; e < 16; ++e) {
+      const int bi = e >> 3, bj = (e >> 2) & 1, j = e & 3;
+      const int li = 16 * bi + (lane >> 4) + 4 * j, lj = 16 * bj + (lane & 15);
+      const int gi = TT * I + li, gj = TT * J + lj;
+      if (gi > gj && gi < N) {
+        const double kij = c[bi][bj][j];
 #pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int li = 16 * bi + (lane >> 4) + 4 * j, lj = 16 * bj + (lane & 15);
-          const int gi = TT * I + li, gj = TT * J + lj;
-          if (gi > gj && gi < N) {
-            const double cc = yv[gi] * yv[gj], kij = c[bi][bj][j];
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-              const double dk = Dt[(size_t)t * ntile * (TT * TT) + tile_at(I, J) + lj * TT + li];   // δK_t,ij from the K pass
-              tr[t] = fma(kij, dk, tr[t]);
-              cgc[t] = fma(cc, dk, cgc[t]);
-            }
-          }
+        for (int t = 0; t < NT; ++t) {
+          tr[t] = fma(kij, dk[t][e], tr[t]);
+          cgc[t] = fma(cc[e], dk[t][e], cgc[t]);
         }
+      }
+    }
   }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
