@@ -148,6 +148,45 @@ __device__ __forceinline__ bool gr_chol(double (&a)[4][16], double& dg, int lane
   return ok;
 }
 
+// The same register Cholesky for one 32 × 32 diagonal tile of gpfit_tile_kernel: lane i holds row
+// i & 31 in a[2][16] (lanes 32-63 duplicate lanes 0-31: they consume broadcasts, produce none),
+// the pivot column broadcast by DPP inside the fused FMAs, the next pivot formed ahead by its own
+// lane.  Every operation is the one the LDS-broadcast formulation applied (a_ij + l_jc·(−l_ic) by
+// one fused multiply-add), so the factor is bit-identical to it.  rl = 1/L_ii of this lane's row.
+template <int K>
+__device__ __forceinline__ void tt_rank1(double (&a)[2][16], double col, double m) {
+  constexpr int J0 = K + 1, B0 = J0 / 16, N0 = J0 % 16;
+  if constexpr (J0 < 32) {
+    double b0, b2, b1, b3;
+    if constexpr (B0 == 0) {
+      row_blocks<0>(col, b0, b2);
+      RankAsm<N0>::run(a[0], b0, m);
+    }
+    row_blocks<1>(col, b1, b3);
+    RankAsm<(B0 == 1) ? N0 : 0>::run(a[1], b1, m);
+  }
+}
+template <int K>
+__device__ __forceinline__ bool tt_chol_step(double (&a)[2][16], double& rl, double& piv, int i) {
+  double& akk = a[K / 16][K % 16];
+  const bool ok = piv > 0.0;   // PosDefException; NaNs propagate harmlessly until the end
+  double lkk, ilkk;
+  sqrt_rsqrt(piv, lkk, ilkk);
+  const double col = (i > K) ? akk * ilkk : akk;
+  akk = (i == K) ? lkk : col;
+  rl = (i == K) ? ilkk : rl;
+  if constexpr (K + 1 < 32) piv = readlane_d(fma(col, -col, a[(K + 1) / 16][(K + 1) % 16]), K + 1);
+  tt_rank1<K>(a, col, (i > K) ? -col : 0.0);
+  return ok;
+}
+template <int... K>
+__device__ __forceinline__ bool tt_chol(double (&a)[2][16], double& rl, int i, std::integer_sequence<int, K...>) {
+  bool ok = true;
+  double piv = readlane_d(a[0][0], 0);
+  ((ok = tt_chol_step<K>(a, rl, piv, i) && ok), ...);
+  return ok;
+}
+
 // c = L'\(L\y), column-oriented substitutions with ck broadcast by readlane: forward step K uses
 // this lane's L[i][K] (register), backward step K its L[K][i] (LDS, row K of L)
 template <int K>
@@ -785,48 +824,20 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       // A_kk → L_kk in LDS (right-looking; PosDefException → status 1), then W_k = L_kk⁻¹
       const int i = lane & 31, h = lane >> 5;
       const double* A = Lt + tile_at(k, k);
-      // A_kk → L_kk with the rows in registers: lane (i, h) holds a_ij for the columns j = 2q + h
-      // (i = lane & 31, h = lane >> 5).  Per column c the pivot comes by readlane, a_ic from the
-      // partner half by one swap, and column c of L reaches every lane through one LDS broadcast;
-      // the rank-1 update is then 16 predicated FMAs per lane on registers.  (Broadcasting every
-      // l_jc by readlane into scalar FMA operands instead measured 2.6x slower: ≈ 500 readlane
-      // pairs per tile, each a VALU-to-SGPR round trip.)
-      bool bad = false;
-      double a[TT / 2];
+      // A_kk → L_kk with the rows in registers (tt_chol: lane i holds row i, the pivot column
+      // broadcast by DPP inside the fused FMAs, no LDS round trip per column).  The round-4
+      // formulations before it -- each column of L through one LDS broadcast, or every l_jc by
+      // readlane into scalar FMA operands -- ran 71 k and 186 k cycles per tile at N = 128.
+      double a[2][16];
 #pragma unroll
-      for (int q2 = 0; q2 < TT / 2; ++q2) a[q2] = A[(2 * q2 + h) * TT + i];
-      double* colc = Wk;   // column c of L (32 doubles); W_k is formed after the factorization
+      for (int j = 0; j < TT; ++j) a[j / 16][j % 16] = A[j * TT + i];
+      double rl = 0.0;
+      const bool bad = !tt_chol(a, rl, i, std::make_integer_sequence<int, TT>{});
+      if (!bad && h == 0) {
 #pragma unroll
-      for (int c = 0; c < TT; ++c) {
-        const int qc = c >> 1, hc = c & 1;
-        const double piv = readlane_d(a[qc], c + 32 * hc);
-        // no early exit (a non-positive pivot sets `bad`; the remaining columns run on values that
-        // are discarded), so the column loop unrolls completely: every register index and the
-        // readlane lane are compile-time constants, and the update is selects, not branches
-        bad = bad || !(piv > 0.0);
-        double lcc, rl;
-        sqrt_rsqrt(piv, lcc, rl);
-        const double lic = half_value(a[qc], hc) * rl;   // l_ic of this lane's row
-        if (h == 0) colc[i] = lic;
-        lds_order();   // one wave: its LDS operations execute in issue order, so no wait is needed
-#pragma unroll
-        for (int q2 = 0; q2 < TT / 2; ++q2) {
-          if (2 * q2 + 1 > c) {   // some column j = 2·q2 + h of this slot lies right of c
-            const int j = 2 * q2 + h;
-            const double upd = fma(-lic, colc[j], a[q2]);
-            a[q2] = ((j > c) & (j <= i)) ? upd : a[q2];
-          }
-        }
-        if (h == hc) a[qc] = (i == c) ? lcc : ((i > c) ? lic : a[qc]);
-        if (lane == 0) {
-          rd[c] = rl;
-          rdall[TT * k + c] = rl;
-        }
-        lds_order();   // colc is rewritten by the next column after these reads were issued
-      }
-      if (!bad) {
-#pragma unroll
-        for (int q2 = 0; q2 < TT / 2; ++q2) Dk[(2 * q2 + h) * TT_LD + i] = a[q2];
+        for (int j = 0; j < TT; ++j) Dk[j * TT_LD + i] = a[j / 16][j % 16];
+        rd[i] = rl;
+        rdall[TT * k + i] = rl;
       }
       gr_sync();
       TT_STAMP(8);
