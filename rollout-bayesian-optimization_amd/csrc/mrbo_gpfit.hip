@@ -731,6 +731,38 @@ __device__ __forceinline__ void tile_ij(int q, int& I, int& J) {
   J = q - I * (I + 1) / 2;
 }
 
+// Triangular substitution step of the tile kernel with the L row broadcast by DPP (the
+// gpfit_reg_kernel idiom): v[R] = (init − Σ_{m<R} L[R][m]·v[m]) · rdR, where lane m holds
+// lr = L[R][m] (read from the column-major diagonal tile) and v is this lane's vector in
+// registers -- W_k by columns (lane j: v = column j of L_kk⁻¹, init = δ_Rj) and the panel by rows
+// (lane r: v = row r of L_Ik, init = A_Ik[r][R]).  Two FMA chains per step, no LDS access inside
+// the sums; lanes 32-63 receive the same broadcasts as lanes 0-31.
+template <int R>
+__device__ __forceinline__ void tt_subst_step(double (&v)[TT], double init, double lr, double rdR) {
+  double t0 = 0.0, t1 = 0.0;
+  if constexpr (R > 0) {
+    double b0, b2;
+    row_blocks<0>(lr, b0, b2);
+    DotAsm<(R < 16 ? R : 16)>::run(t0, t1, b0, &v[0]);
+    if constexpr (R > 16) {
+      double b1, b3;
+      row_blocks<1>(lr, b1, b3);
+      DotAsm<R - 16>::run(t0, t1, b1, &v[16]);
+    }
+  }
+  v[R] = (init - (t0 + t1)) * rdR;
+}
+template <int... R>
+__device__ __forceinline__ void tt_inverse(double (&v)[TT], const double* Dk, double rl, int i,
+                                           std::integer_sequence<int, R...>) {
+  ((tt_subst_step<R>(v, (i == R) ? 1.0 : 0.0, Dk[i * TT_LD + R], readlane_d(rl, R))), ...);
+}
+template <int... R>
+__device__ __forceinline__ void tt_panel(double (&v)[TT], const double* Dk, const double* rd, int i,
+                                         std::integer_sequence<int, R...>) {
+  ((tt_subst_step<R>(v, v[R], Dk[i * TT_LD + R], rd[R])), ...);
+}
+
 // -DMRBO_GPFIT_STAMPS: cycles per phase of candidate 0 (thread 0, after each workgroup barrier):
 // K, then per tile column the diagonal factor + inverse, the panel, the trailing update (summed
 // over k), V by tile rows, c, K⁻¹ + traces
@@ -845,20 +877,11 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
         if (lane == 0) fail = 1;
       } else {
         if (lane < TT && TT * k + lane < N) lgl += log(Dk[lane * TT_LD + lane]);
-        // W column j = lane (< 32): W_ij = (δ_ij − Σ_{m<i} L_im W_mj)/L_ii, the column in
-        // registers, column-oriented: once W_mj is final it is eliminated from every later row
-        // (W_mj = 0 for m < j comes out of the same recursion).  The dependent chain is two
-        // operations per row; the 31 − m updates of a step are independent.
+        // W column j = lane & 31: W_ij = (δ_ij − Σ_{m<i} L_im W_mj)/L_ii, the column in registers
+        // (W_mj = 0 for m < j comes out of the same recursion), row i of L broadcast by DPP
+        double wc[TT];
+        tt_inverse(wc, Dk, rl, i, std::make_integer_sequence<int, TT>{});
         if (lane < TT) {
-          double wc[TT];
-#pragma unroll
-          for (int r = 0; r < TT; ++r) wc[r] = (r == lane) ? 1.0 : 0.0;
-#pragma unroll
-          for (int m = 0; m < TT; ++m) {
-            wc[m] *= rd[m];
-#pragma unroll
-            for (int r = m + 1; r < TT; ++r) wc[r] = fma(-Dk[m * TT_LD + r], wc[m], wc[r]);
-          }
 #pragma unroll
           for (int r = 0; r < TT; ++r) Wk[lane * TT_LD + r] = wc[r];
         }
@@ -879,26 +902,24 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     __syncthreads();
     TT_STAMP(2);
     if (fail) break;
-    // panel: L_Ik = A_Ik·L_kk⁻ᵀ by forward substitution, one row per lane (lanes < 32), the row in
-    // registers: L_Ik[r][c] = (A_Ik[r][c] − Σ_{m<c} L_Ik[r][m]·L_kk[c][m]) / L_kk[c][c], the
-    // factor's own recurrence (a product with the explicit inverse W_k is ≈ κ(L_kk) less accurate),
-    // column-oriented: entry m, once final, is eliminated from every later column (independent
-    // updates; the dependent chain is two operations per column)
-    for (int I = k + 1 + w; I < T; I += 4) {
-      double* A = Lt + tile_at(I, k);
-      if (lane < TT) {
-        const int r = lane;
+    // panel: L_Ik = A_Ik·L_kk⁻ᵀ by forward substitution, one row per lane, the row in registers:
+    // L_Ik[r][c] = (A_Ik[r][c] − Σ_{m<c} L_Ik[r][m]·L_kk[c][m]) / L_kk[c][c], the factor's own
+    // recurrence (a product with the explicit inverse W_k is ≈ κ(L_kk) less accurate), row c of
+    // L_kk broadcast by DPP; the two half-waves take two tiles (I and I + 4)
+    {
+      const int i = lane & 31, h = lane >> 5;
+      for (int I0 = k + 1 + w; I0 < T; I0 += 8) {
+        const int I = I0 + 4 * h;
+        const bool has = I < T;
+        double* A = Lt + tile_at(has ? I : I0, k);
         double lrow[TT];
 #pragma unroll
-        for (int c = 0; c < TT; ++c) lrow[c] = A[c * TT + r];
+        for (int c = 0; c < TT; ++c) lrow[c] = has ? A[c * TT + i] : 0.0;
+        tt_panel(lrow, Dk, rd, i, std::make_integer_sequence<int, TT>{});
+        if (has) {
 #pragma unroll
-        for (int m = 0; m < TT; ++m) {
-          lrow[m] *= rd[m];
-#pragma unroll
-          for (int c = m + 1; c < TT; ++c) lrow[c] = fma(-lrow[m], Dk[m * TT_LD + c], lrow[c]);
+          for (int c = 0; c < TT; ++c) A[c * TT + i] = lrow[c];
         }
-#pragma unroll
-        for (int c = 0; c < TT; ++c) A[c * TT + r] = lrow[c];
       }
     }
     __syncthreads();
