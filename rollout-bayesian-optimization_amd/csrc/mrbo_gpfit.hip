@@ -179,6 +179,18 @@ __device__ __forceinline__ bool tt_chol_step(double (&a)[2][16], double& rl, dou
   tt_rank1<K>(a, col, (i > K) ? -col : 0.0);
   return ok;
 }
+// Forward substitution in a factored diagonal tile, rows in registers (lane i: a = row i of L_kk,
+// rl = 1/L_ii): the solved entry z_M broadcast by readlane, eliminated from the rows below.
+template <int M>
+__device__ __forceinline__ void tt_fwd_step(double& r, const double (&a)[2][16], double rl, int i) {
+  const double zm = readlane_d(r, M) * readlane_d(rl, M);
+  r = (i == M) ? zm : ((i > M) ? fma(-a[M / 16][M % 16], zm, r) : r);
+}
+template <int... M>
+__device__ __forceinline__ void tt_fwd(double& r, const double (&a)[2][16], double rl, int i,
+                                       std::integer_sequence<int, M...>) {
+  (tt_fwd_step<M>(r, a, rl, i), ...);
+}
 template <int... K>
 __device__ __forceinline__ bool tt_chol(double (&a)[2][16], double& rl, int i, std::integer_sequence<int, K...>) {
   bool ok = true;
@@ -871,6 +883,13 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
         rd[i] = rl;
         rdall[TT * k + i] = rl;
       }
+      if (!bad) {
+        // the forward half of c = L'\(L\y), fused into the factorisation: z_k = L_kk⁻¹ r_k, where
+        // r_k = y_k − Σ_{J<k} L_kJ z_J was accumulated by the panels of the earlier tile columns
+        double r = yv[TT * k + i];
+        tt_fwd(r, a, rl, i, std::make_integer_sequence<int, TT>{});
+        if (lane < TT) uv[TT * k + i] = r;
+      }
       gr_sync();
       TT_STAMP(8);
       if (bad) {
@@ -916,9 +935,17 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
 #pragma unroll
         for (int c = 0; c < TT; ++c) lrow[c] = has ? A[c * TT + i] : 0.0;
         tt_panel(lrow, Dk, rd, i, std::make_integer_sequence<int, TT>{});
+        // r_I −= L_Ik z_k (the forward substitution's update of the rows below; z_k by DPP)
+        double t0 = 0.0, t1 = 0.0, b0, b1, b2, b3;
+        const double zl = uv[TT * k + i];
+        row_blocks<0>(zl, b0, b2);
+        DotAsm<16>::run(t0, t1, b0, &lrow[0]);
+        row_blocks<1>(zl, b1, b3);
+        DotAsm<16>::run(t0, t1, b1, &lrow[16]);
         if (has) {
 #pragma unroll
           for (int c = 0; c < TT; ++c) A[c * TT + i] = lrow[c];
+          yv[TT * I + i] -= t0 + t1;
         }
       }
     }
@@ -969,48 +996,16 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     TT_STAMP(5);
   }
   // c = L'\(L\y) by blocked substitution (wave 0; lane i < 32 = row i of the current tile):
-  // forward z_I = L_II⁻¹(y_I − Σ_{J<I} L_IJ z_J), backward c_I = L_II⁻ᵀ(z_I − Σ_{J>I} L_JIᵀ c_J);
+  // forward z_I = L_II⁻¹(y_I − Σ_{J<I} L_IJ z_J) (done during the factorisation), backward
+  // c_I = L_II⁻ᵀ(z_I − Σ_{J>I} L_JIᵀ c_J);
   // inside a tile the column-oriented substitution with the solved entry broadcast by readlane.
   // yᵀc as the reference's log_likelihood forms it.
   if (w == 0) {
     const int i = lane & 31;
     double yc = 0.0;
-    // every tile's L entries are loaded into registers ahead of the dependent FMA chains (fully
-    // unrolled: the workspace loads of a tile issue together instead of one per step)
-    // (the off-diagonal tiles of a block row are software-pipelined: tile J + 1's loads are in
-    // flight during tile J's products, which run as four partial sums)
-    for (int I = 0; I < T; ++I) {
-      double r = yv[TT * I + i];
-      double lm[TT], lj[TT];
-      const double* LD_ = Lt + tile_at(I, I);
-#pragma unroll
-      for (int m = 0; m < TT; ++m) lm[m] = LD_[m * TT + i];
-      if (I > 0) {
-#pragma unroll
-        for (int j = 0; j < TT; ++j) lj[j] = Lt[tile_at(I, 0) + j * TT + i];
-      }
-      double r4[4] = {0.0, 0.0, 0.0, 0.0};
-      for (int J = 0; J < I; ++J) {
-        double cur[TT];
-#pragma unroll
-        for (int j = 0; j < TT; ++j) cur[j] = lj[j];
-        if (J + 1 < I) {
-#pragma unroll
-          for (int j = 0; j < TT; ++j) lj[j] = Lt[tile_at(I, J + 1) + j * TT + i];
-        }
-#pragma unroll
-        for (int j = 0; j < TT; ++j) r4[j & 3] = fma(-cur[j], uv[TT * J + j], r4[j & 3]);
-      }
-      r += (r4[0] + r4[1]) + (r4[2] + r4[3]);
-#pragma unroll
-      for (int m = 0; m < TT; ++m) {
-        const double zm = readlane_d(r, m) * rdall[TT * I + m];
-        if (i == m) r = zm;
-        else if (i > m) r = fma(-lm[m], zm, r);
-      }
-      if (lane < TT) uv[TT * I + i] = r;   // z
-      gr_sync();
-    }
+    // (z = L⁻¹y is in uv: the factorisation's diagonal steps and panels formed it; the
+    // backward tiles' loads are software-pipelined: tile J + 1's loads are in flight during tile
+    // J's products, which run as four partial sums)
     for (int I = T - 1; I >= 0; --I) {
       double r = uv[TT * I + i];
       double lm[TT], lj[TT];
