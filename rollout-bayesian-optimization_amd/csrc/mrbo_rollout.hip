@@ -1937,6 +1937,12 @@ template <int D>
 __device__ __forceinline__ bool lu_det_solve(double (&A)[D][D], double* b, double& det, bool do_solve) {
   int piv[D];
   bool sing = false;
+  // the right-hand side is permuted beside A's rows, step by step (the same swaps, in the same
+  // order, as applying the pivots after the factorisation): applied afterwards from piv[], the
+  // select chains were turned into an indexed load of a scratch copy of b
+  double bw[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) bw[i] = b[i];
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     int p = k;
@@ -1954,6 +1960,14 @@ __device__ __forceinline__ bool lu_det_solve(double (&A)[D][D], double* b, doubl
       for (int i = k + 1; i < D; ++i) A[i][j] = (i == p) ? A[k][j] : A[i][j];
       A[k][j] = rowp;
     }
+    if (do_solve) {
+      double bp = bw[k];
+#pragma unroll
+      for (int i = k + 1; i < D; ++i) bp = (i == p) ? bw[i] : bp;
+#pragma unroll
+      for (int i = k + 1; i < D; ++i) bw[i] = (i == p) ? bw[k] : bw[i];
+      bw[k] = bp;
+    }
     if (A[k][k] == 0.0) { sing = true; continue; }
 #pragma unroll
     for (int i = k + 1; i < D; ++i) A[i][k] /= A[k][k];
@@ -1968,14 +1982,7 @@ __device__ __forceinline__ bool lu_det_solve(double (&A)[D][D], double* b, doubl
   if (sing) det = 0.0;
   if (!do_solve || sing) return !sing;
 #pragma unroll
-  for (int k = 0; k < D; ++k) {
-    double bp = b[k];
-#pragma unroll
-    for (int i = k + 1; i < D; ++i) bp = (i == piv[k]) ? b[i] : bp;
-#pragma unroll
-    for (int i = k + 1; i < D; ++i) b[i] = (i == piv[k]) ? b[k] : b[i];
-    b[k] = bp;
-  }
+  for (int i = 0; i < D; ++i) b[i] = bw[i];
 #pragma unroll
   for (int i = 0; i < D; ++i) {
     double s = b[i];
