@@ -402,6 +402,49 @@ static void pool_give(void* p, size_t bytes) {
 // staging helper for MRBO_FLAG_HOST_POINTERS: the plan's persistent device buffers (slot k =
 // the k-th staged argument of the call), so a host-pointer call allocates nothing once warm;
 // without a plan (mrbo_gp_fit) the buffers come from the device pool and return to it
+// Pinned host bounce buffers for the plan-less calls' packed transfers (mrbo_gp_fit: its inputs
+// go to the device in one copy and its small outputs come back in one): pooled like DevPool, a
+// hipHostMalloc costs far more than the copies it serves.
+struct HostPool {
+  std::mutex m;
+  std::vector<std::pair<void*, size_t>> free;
+};
+static HostPool g_hpool;
+
+struct Pinned {
+  void* p = nullptr;
+  size_t n = 0;
+  explicit Pinned(size_t bytes) {
+    if (!bytes) return;
+    {
+      std::lock_guard<std::mutex> lk(g_hpool.m);
+      size_t best = g_hpool.free.size();
+      for (size_t i = 0; i < g_hpool.free.size(); ++i)
+        if (g_hpool.free[i].second >= bytes &&
+            (best == g_hpool.free.size() || g_hpool.free[i].second < g_hpool.free[best].second))
+          best = i;
+      if (best < g_hpool.free.size()) {
+        p = g_hpool.free[best].first;
+        n = g_hpool.free[best].second;
+        g_hpool.free.erase(g_hpool.free.begin() + best);
+        return;
+      }
+      for (size_t i = g_hpool.free.size(); i-- > 0;) {   // too small for what calls now ask for
+        (void)hipHostFree(g_hpool.free[i].first);
+        g_hpool.free.erase(g_hpool.free.begin() + i);
+      }
+    }
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) p = nullptr;
+    else n = bytes;
+  }
+  ~Pinned() {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(g_hpool.m);
+    g_hpool.free.push_back({p, n});
+  }
+  void abandon() { p = nullptr; }   // a copy may still read it: keep it out of the pool
+};
+
 struct Stage {
   mrbo_plan_t* P;
   std::vector<std::pair<void*, size_t>> own;
@@ -954,17 +997,27 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
   if (s->kernel == 4 && nt == 1 && !(s->period > 0.0)) return fail(MRBO_ERR_ARG, "gp_fit: period %g", s->period);
   hipStream_t st = (hipStream_t)stream;
   const size_t P = (size_t)np, NN = (size_t)N * N, NTP = (size_t)nt * P;
+  const bool host = flags & MRBO_FLAG_HOST_POINTERS;
   Stage sg;
-  const double* dth = thetas;
+  // inputs [θ (host calls) | X | y] packed into one pinned buffer and one host→device copy; the
+  // small outputs of host calls [ll | grad | status] in one device block and one copy back
+  const size_t n_th = host ? NTP : 0, n_in = n_th + (size_t)d * N + N;
+  const size_t out_bytes = sizeof(double) * (P + NTP) + sizeof(int32_t) * P;
+  double* din = (double*)sg.slot(sizeof(double) * n_in);
+  if (!din) return fail(MRBO_ERR_NOMEM, "staging the inputs");
+  const double* dth = host ? din : thetas;
+  const double* dX = din + n_th;
+  const double* dy = dX + (size_t)d * N;
   double *dll_ = ll, *dgr = grad, *dL = L_out, *dc = c_out;
   int32_t* dst = status;
-  if (flags & MRBO_FLAG_HOST_POINTERS) {
-    if (sg.in(thetas, NTP, &dth) || sg.out(P, ll, &dll_) || sg.out(NTP, grad, &dgr) || sg.out(P, status, &dst) ||
-        sg.out(NN * P, L_out, &dL) || sg.out((size_t)N * P, c_out, &dc))
+  if (host) {
+    char* dout = (char*)sg.slot(out_bytes);
+    if (!dout || sg.out(NN * P, L_out, &dL) || sg.out((size_t)N * P, c_out, &dc))
       return fail(MRBO_ERR_NOMEM, "staging allocation failed");
+    dll_ = (double*)dout;
+    dgr = dll_ + P;
+    dst = (int32_t*)(dgr + NTP);
   }
-  const double *dX = nullptr, *dy = nullptr;
-  if (sg.in(s->X, (size_t)d * N, &dX) || sg.in(s->y, (size_t)N, &dy)) return fail(MRBO_ERR_NOMEM, "staging X, y");
   GpFitParams q{d, N, s->kernel, s->sigma_n2, dX, dy, nt, dth, s->period, dll_, dgr, (int*)dst, dL, dc, nullptr};
   {
     int dev = 0, lds_max = 0;
@@ -978,6 +1031,14 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
   if (!gpfit_in_regs(q) && !gpfit_in_lds(q)) {   // the register (N ≤ 64) and LDS (N ≤ 80) kernels need none
     q.work = (double*)sg.slot(sizeof(double) * gpfit_tile_work_doubles(N, nt) * P);
     if (!q.work) return fail(MRBO_ERR_NOMEM, "gp_fit workspace");
+  }
+  Pinned pin_in(sizeof(double) * n_in), pin_out(host ? out_bytes : 0);
+  if (!pin_in.p || (host && !pin_out.p)) return fail(MRBO_ERR_NOMEM, "pinned staging");
+  {
+    double* h = (double*)pin_in.p;
+    if (host) std::memcpy(h, thetas, sizeof(double) * NTP);
+    std::memcpy(h + n_th, s->X, sizeof(double) * d * N);
+    std::memcpy(h + n_th + (size_t)d * N, s->y, sizeof(double) * N);
   }
   // timing events per device (an event records only on streams of the device it was created on)
   static std::mutex gev_m;
@@ -999,7 +1060,18 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
     gev[0] = gevs[dev].first;
     gev[1] = gevs[dev].second;
   }
-  HIP_TRY(hipEventRecord(gev[0], st));
+  // from here on every return path synchronises the stream first (the copy reads pin_in)
+  {
+    const hipError_t e = hipMemcpyAsync(din, pin_in.p, sizeof(double) * n_in, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) {
+      if (hipStreamSynchronize(st) != hipSuccess) { sg.abandon(); pin_in.abandon(); }
+      return fail(MRBO_ERR_HIP, "gp_fit: staging copy: %s", hipGetErrorString(e));
+    }
+  }
+  if (const hipError_t e = hipEventRecord(gev[0], st); e != hipSuccess) {
+    if (hipStreamSynchronize(st) != hipSuccess) { sg.abandon(); pin_in.abandon(); }
+    return fail(MRBO_ERR_HIP, "gp_fit: hipEventRecord: %s", hipGetErrorString(e));
+  }
   launch_gpfit(np, st, q);
   // the staging buffers and the workspace go back to the pool on return: once the launch is
   // issued, every path synchronises the stream first (an error after the launch must not hand
@@ -1011,6 +1083,7 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
     const hipError_t es = hipStreamSynchronize(st);
     if (es != hipSuccess) {
       sg.abandon();
+      pin_in.abandon();
       return fail(MRBO_ERR_HIP, "gp_fit: hipStreamSynchronize: %s", hipGetErrorString(es));
     }
     if (e != hipSuccess) return fail(MRBO_ERR_HIP, "gp_fit launch: %s", hipGetErrorString(e));
@@ -1019,10 +1092,12 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
     float ms = -1.f;
     if (hipEventElapsedTime(&ms, gev[0], gev[1]) == hipSuccess) g_gpfit_ms = ms;
   }
-  if (flags & MRBO_FLAG_HOST_POINTERS) {
-    HIP_TRY(hipMemcpy(ll, dll_, sizeof(double) * P, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(grad, dgr, sizeof(double) * NTP, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(status, dst, sizeof(int32_t) * P, hipMemcpyDeviceToHost));
+  if (host) {
+    HIP_TRY(hipMemcpy(pin_out.p, dll_, out_bytes, hipMemcpyDeviceToHost));
+    const double* h = (const double*)pin_out.p;
+    std::memcpy(ll, h, sizeof(double) * P);
+    std::memcpy(grad, h + P, sizeof(double) * NTP);
+    std::memcpy(status, h + P + NTP, sizeof(int32_t) * P);
     if (L_out) HIP_TRY(hipMemcpy(L_out, dL, sizeof(double) * NN * P, hipMemcpyDeviceToHost));
     if (c_out) HIP_TRY(hipMemcpy(c_out, dc, sizeof(double) * N * P, hipMemcpyDeviceToHost));
   }
