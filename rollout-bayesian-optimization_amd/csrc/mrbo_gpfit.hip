@@ -835,6 +835,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     tile_ij(qt, I, J);
     const int gi = TT * I + (tid & 31), gj0 = TT * J + (tid >> 5);
     double r2[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 3
     for (int u = 0; u < d; ++u) {
       const double* xu = XS + (size_t)u * NP;
       const double xi = xu[gi];
@@ -906,21 +907,26 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
         }
         gr_sync();
         TT_STAMP(9);
-        double* Lkk = Lt + tile_at(k, k);
-        double* Vkk = Vt + tile_at(k, k);
-        double* Wkk = Wt + (size_t)k * (TT * TT);
-        for (int e = lane; e < TT * TT; e += 64) {
-          const int r = e & 31, cc = e >> 5;                 // column-major (r, cc)
-          Lkk[e] = (r >= cc) ? Dk[cc * TT_LD + r] : 0.0;
-          Wkk[e] = Wk[cc * TT_LD + r];
-          Vkk[r * TT + cc] = Wk[cc * TT_LD + r];              // row-major copy: V_kk = W_k
-        }
-        TT_STAMP(10);
       }
     }
     __syncthreads();
     TT_STAMP(2);
     if (fail) break;
+    {
+      // L_kk, W_k and V_kk = W_k (row-major) to the workspace by the whole workgroup, beside the
+      // panel (Dk and Wk stay in LDS until the next diagonal step; the readers come after later
+      // barriers); every store coalesced
+      double* Lkk = Lt + tile_at(k, k);
+      double* Vkk = Vt + tile_at(k, k);
+      double* Wkk = Wt + (size_t)k * (TT * TT);
+      for (int e = tid; e < TT * TT; e += TT_THREADS) {
+        const int r = e & 31, cc = e >> 5;                 // column-major (r, cc)
+        Lkk[e] = (r >= cc) ? Dk[cc * TT_LD + r] : 0.0;
+        Wkk[e] = Wk[cc * TT_LD + r];
+        Vkk[e] = Wk[r * TT_LD + cc];                       // row-major: V_kk[cc][r] = W_k[cc][r]
+      }
+    }
+    TT_STAMP(10);
     // panel: L_Ik = A_Ik·L_kk⁻ᵀ by forward substitution, one row per lane, the row in registers:
     // L_Ik[r][c] = (A_Ik[r][c] − Σ_{m<c} L_Ik[r][m]·L_kk[c][m]) / L_kk[c][c], the factor's own
     // recurrence (a product with the explicit inverse W_k is ≈ κ(L_kk) less accurate), row c of
