@@ -765,9 +765,9 @@ __device__ __forceinline__ void tt_subst_step(double (&v)[TT], double init, doub
   v[R] = (init - (t0 + t1)) * rdR;
 }
 template <int... R>
-__device__ __forceinline__ void tt_inverse(double (&v)[TT], const double* Dk, double rl, int i,
+__device__ __forceinline__ void tt_inverse(double (&v)[TT], const double* Dk, const double* rd, int i,
                                            std::integer_sequence<int, R...>) {
-  ((tt_subst_step<R>(v, (i == R) ? 1.0 : 0.0, Dk[i * TT_LD + R], readlane_d(rl, R))), ...);
+  ((tt_subst_step<R>(v, (i == R) ? 1.0 : 0.0, Dk[i * TT_LD + R], rd[R])), ...);
 }
 template <int... R>
 __device__ __forceinline__ void tt_panel(double (&v)[TT], const double* Dk, const double* rd, int i,
@@ -866,7 +866,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   double lgl = 0.0;   // Σ log L_ii: lane i < 32 of wave 0 sums row i of every diagonal tile
   for (int k = 0; k < T; ++k) {
     if (w == 0) {
-      // A_kk → L_kk in LDS (right-looking; PosDefException → status 1), then W_k = L_kk⁻¹
+      // A_kk → L_kk (PosDefException → status 1) and the forward substitution's z_k
       const int i = lane & 31, h = lane >> 5;
       const double* A = Lt + tile_at(k, k);
       // A_kk → L_kk with the rows in registers (tt_chol: lane i holds row i, the pivot column
@@ -895,63 +895,71 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       TT_STAMP(8);
       if (bad) {
         if (lane == 0) fail = 1;
-      } else {
-        if (lane < TT && TT * k + lane < N) lgl += log(Dk[lane * TT_LD + lane]);
-        // W column j = lane & 31: W_ij = (δ_ij − Σ_{m<i} L_im W_mj)/L_ii, the column in registers
-        // (W_mj = 0 for m < j comes out of the same recursion), row i of L broadcast by DPP
-        double wc[TT];
-        tt_inverse(wc, Dk, rl, i, std::make_integer_sequence<int, TT>{});
-        if (lane < TT) {
-#pragma unroll
-          for (int r = 0; r < TT; ++r) Wk[lane * TT_LD + r] = wc[r];
-        }
-        gr_sync();
-        TT_STAMP(9);
+      } else if (lane < TT && TT * k + lane < N) {
+        lgl += log(Dk[lane * TT_LD + lane]);
       }
     }
     __syncthreads();
     TT_STAMP(2);
     if (fail) break;
     {
-      // L_kk, W_k and V_kk = W_k (row-major) to the workspace by the whole workgroup, beside the
-      // panel (Dk and Wk stay in LDS until the next diagonal step; the readers come after later
-      // barriers); every store coalesced
+      // L_kk to the workspace by the whole workgroup, beside the panel (Dk stays in LDS until the
+      // next diagonal step; the readers come after later barriers), coalesced
       double* Lkk = Lt + tile_at(k, k);
-      double* Vkk = Vt + tile_at(k, k);
-      double* Wkk = Wt + (size_t)k * (TT * TT);
       for (int e = tid; e < TT * TT; e += TT_THREADS) {
         const int r = e & 31, cc = e >> 5;                 // column-major (r, cc)
         Lkk[e] = (r >= cc) ? Dk[cc * TT_LD + r] : 0.0;
-        Wkk[e] = Wk[cc * TT_LD + r];
-        Vkk[e] = Wk[r * TT_LD + cc];                       // row-major: V_kk[cc][r] = W_k[cc][r]
       }
     }
     TT_STAMP(10);
     // panel: L_Ik = A_Ik·L_kk⁻ᵀ by forward substitution, one row per lane, the row in registers:
     // L_Ik[r][c] = (A_Ik[r][c] − Σ_{m<c} L_Ik[r][m]·L_kk[c][m]) / L_kk[c][c], the factor's own
     // recurrence (a product with the explicit inverse W_k is ≈ κ(L_kk) less accurate), row c of
-    // L_kk broadcast by DPP; the two half-waves take two tiles (I and I + 4)
+    // L_kk broadcast by DPP.  Meanwhile wave 0 forms W_k = L_kk⁻¹ (needed only by the V pass):
+    // the panel tiles go to the half-waves of waves 1-3 first (slots 0-5), wave 0's two halves
+    // take slots 6 and 7 after W_k.
     {
-      const int i = lane & 31, h = lane >> 5;
-      for (int I0 = k + 1 + w; I0 < T; I0 += 8) {
-        const int I = I0 + 4 * h;
-        const bool has = I < T;
-        double* A = Lt + tile_at(has ? I : I0, k);
+      const int i = lane & 31, h = lane >> 5, npanel = T - k - 1;
+      if (w == 0) {
+        // W column j = lane & 31: W_ij = (δ_ij − Σ_{m<i} L_im W_mj)/L_ii, the column in registers
+        // (W_mj = 0 for m < j comes out of the same recursion), row i of L broadcast by DPP
+        double wc[TT];
+        tt_inverse(wc, Dk, rd, i, std::make_integer_sequence<int, TT>{});
+        if (lane < TT) {
+#pragma unroll
+          for (int r = 0; r < TT; ++r) Wk[lane * TT_LD + r] = wc[r];
+        }
+        gr_sync();
+        double* Vkk = Vt + tile_at(k, k);
+        double* Wkk = Wt + (size_t)k * (TT * TT);
+        for (int e = lane; e < TT * TT; e += 64) {
+          const int r = e & 31, cc = e >> 5;
+          Wkk[e] = Wk[cc * TT_LD + r];                     // column-major
+          Vkk[e] = Wk[r * TT_LD + cc];                     // row-major: V_kk = W_k
+        }
+        TT_STAMP(9);
+      }
+      const int slot0 = (w == 0) ? 6 : 2 * (w - 1), slot = slot0 + h;
+      for (int t0 = 0; t0 + slot0 < npanel; t0 += 8) {     // wave-uniform: some half has a tile
+        const int t = t0 + slot;
+        const bool has = t < npanel;
+        const int I = k + 1 + (has ? t : 0);
+        double* A = Lt + tile_at(I, k);
         double lrow[TT];
 #pragma unroll
         for (int c = 0; c < TT; ++c) lrow[c] = has ? A[c * TT + i] : 0.0;
         tt_panel(lrow, Dk, rd, i, std::make_integer_sequence<int, TT>{});
         // r_I −= L_Ik z_k (the forward substitution's update of the rows below; z_k by DPP)
-        double t0 = 0.0, t1 = 0.0, b0, b1, b2, b3;
+        double t0s = 0.0, t1s = 0.0, b0, b1, b2, b3;
         const double zl = uv[TT * k + i];
         row_blocks<0>(zl, b0, b2);
-        DotAsm<16>::run(t0, t1, b0, &lrow[0]);
+        DotAsm<16>::run(t0s, t1s, b0, &lrow[0]);
         row_blocks<1>(zl, b1, b3);
-        DotAsm<16>::run(t0, t1, b1, &lrow[16]);
+        DotAsm<16>::run(t0s, t1s, b1, &lrow[16]);
         if (has) {
 #pragma unroll
           for (int c = 0; c < TT; ++c) A[c * TT + i] = lrow[c];
-          yv[TT * I + i] -= t0 + t1;
+          yv[TT * I + i] -= t0s + t1s;
         }
       }
     }
