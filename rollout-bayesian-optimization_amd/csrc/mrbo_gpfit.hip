@@ -916,11 +916,11 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     // L_Ik[r][c] = (A_Ik[r][c] − Σ_{m<c} L_Ik[r][m]·L_kk[c][m]) / L_kk[c][c], the factor's own
     // recurrence (a product with the explicit inverse W_k is ≈ κ(L_kk) less accurate), row c of
     // L_kk broadcast by DPP.  Meanwhile wave 0 forms W_k = L_kk⁻¹ (needed only by the V pass):
-    // the panel tiles go to the half-waves of waves 1-3 first (slots 0-5), wave 0's two halves
-    // take slots 6 and 7 after W_k.
+    // the panel tiles go to the half-waves of waves 1-3 first (slots 0-5 of every round of 8),
+    // wave 0's two halves take slots 6 and 7.
     {
       const int i = lane & 31, h = lane >> 5, npanel = T - k - 1;
-      if (w == 0) {
+      auto form_w = [&]() {
         // W column j = lane & 31: W_ij = (δ_ij − Σ_{m<i} L_im W_mj)/L_ii, the column in registers
         // (W_mj = 0 for m < j comes out of the same recursion), row i of L broadcast by DPP
         double wc[TT];
@@ -938,7 +938,10 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
           Vkk[e] = Wk[r * TT_LD + cc];                     // row-major: V_kk = W_k
         }
         TT_STAMP(9);
-      }
+      };
+      // with at most six panel tiles wave 0 has none and W_k runs entirely beside the panel;
+      // with more, wave 0 takes its tiles first and W_k after them
+      if (w == 0 && npanel <= 6) form_w();
       const int slot0 = (w == 0) ? 6 : 2 * (w - 1), slot = slot0 + h;
       for (int t0 = 0; t0 + slot0 < npanel; t0 += 8) {     // wave-uniform: some half has a tile
         const int t = t0 + slot;
@@ -962,6 +965,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
           yv[TT * I + i] -= t0s + t1s;
         }
       }
+      if (w == 0 && npanel > 6) form_w();
     }
     __syncthreads();
     TT_STAMP(3);
