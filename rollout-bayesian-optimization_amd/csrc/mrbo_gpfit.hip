@@ -895,8 +895,20 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       TT_STAMP(8);
       if (bad) {
         if (lane == 0) fail = 1;
-      } else if (lane < TT && TT * k + lane < N) {
-        lgl += log(Dk[lane * TT_LD + lane]);
+      } else {
+        if (lane < TT && TT * k + lane < N) lgl += log(Dk[lane * TT_LD + lane]);
+        if (T - k - 1 > 6) {
+          // more panel tiles than waves 1-3 take in one round: W_k here, serially (below, it
+          // would delay wave 0's own panel tiles), copied out by the whole workgroup
+          double wc[TT];
+          tt_inverse(wc, Dk, rd, i, std::make_integer_sequence<int, TT>{});
+          if (lane < TT) {
+#pragma unroll
+            for (int r = 0; r < TT; ++r) Wk[lane * TT_LD + r] = wc[r];
+          }
+          gr_sync();
+        }
+        TT_STAMP(9);
       }
     }
     __syncthreads();
@@ -906,9 +918,16 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       // L_kk to the workspace by the whole workgroup, beside the panel (Dk stays in LDS until the
       // next diagonal step; the readers come after later barriers), coalesced
       double* Lkk = Lt + tile_at(k, k);
+      double* Vkk = Vt + tile_at(k, k);
+      double* Wkk = Wt + (size_t)k * (TT * TT);
+      const bool w_done = T - k - 1 > 6;
       for (int e = tid; e < TT * TT; e += TT_THREADS) {
         const int r = e & 31, cc = e >> 5;                 // column-major (r, cc)
         Lkk[e] = (r >= cc) ? Dk[cc * TT_LD + r] : 0.0;
+        if (w_done) {
+          Wkk[e] = Wk[cc * TT_LD + r];
+          Vkk[e] = Wk[r * TT_LD + cc];                     // row-major: V_kk = W_k
+        }
       }
     }
     TT_STAMP(10);
@@ -937,10 +956,9 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
           Wkk[e] = Wk[cc * TT_LD + r];                     // column-major
           Vkk[e] = Wk[r * TT_LD + cc];                     // row-major: V_kk = W_k
         }
-        TT_STAMP(9);
       };
-      // with at most six panel tiles wave 0 has none and W_k runs entirely beside the panel;
-      // with more, wave 0 takes its tiles first and W_k after them
+      // with at most six panel tiles wave 0 has none and W_k runs entirely beside the panel
+      // (with more, the diagonal step formed it)
       if (w == 0 && npanel <= 6) form_w();
       const int slot0 = (w == 0) ? 6 : 2 * (w - 1), slot = slot0 + h;
       for (int t0 = 0; t0 + slot0 < npanel; t0 += 8) {     // wave-uniform: some half has a tile
@@ -965,7 +983,6 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
           yv[TT * I + i] -= t0s + t1s;
         }
       }
-      if (w == 0 && npanel > 6) form_w();
     }
     __syncthreads();
     TT_STAMP(3);
