@@ -735,6 +735,33 @@ __device__ __forceinline__ void tile_xyt(f64x4 (&c)[2][2], const double* X, cons
   }
 }
 __device__ __forceinline__ size_t tile_at(int I, int J) { return (size_t)(I * (I + 1) / 2 + J) * (TT * TT); }
+// The operands of one tile_xyt in registers (the A- and B-fragments of its eight k-steps), so
+// that a loop over tiles can load tile n + 1's operands while tile n's products run
+struct TileFrag {
+  double a[TT / 4][2], b[TT / 4][2];
+};
+__device__ __forceinline__ void frag_load(TileFrag& f, const double* X, const double* Y, int lane) {
+  const int r = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < TT / 4; ++s) {
+    f.a[s][0] = X[(4 * s + kk) * TT + r];
+    f.a[s][1] = X[(4 * s + kk) * TT + 16 + r];
+    f.b[s][0] = Y[(4 * s + kk) * TT + r];
+    f.b[s][1] = Y[(4 * s + kk) * TT + 16 + r];
+  }
+}
+// c −= X·Yᵀ from the fragments (tile_xyt<true>'s products, in its order)
+__device__ __forceinline__ void frag_sub(f64x4 (&c)[2][2], const TileFrag& f) {
+#pragma unroll
+  for (int s = 0; s < TT / 4; ++s) {
+    const double a0 = -f.a[s][0], a1 = -f.a[s][1];
+    c[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, f.b[s][0], c[0][0], 0, 0, 0);
+    c[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, f.b[s][1], c[0][1], 0, 0, 0);
+    c[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, f.b[s][0], c[1][0], 0, 0, 0);
+    c[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, f.b[s][1], c[1][1], 0, 0, 0);
+  }
+}
+
 // lower-triangle index q = I(I+1)/2 + J → (I, J)
 __device__ __forceinline__ void tile_ij(int q, int& I, int& J) {
   I = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
@@ -987,16 +1014,42 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     __syncthreads();
     TT_STAMP(3);
     // trailing update A_IJ −= L_Ik·L_Jkᵀ, k < J ≤ I
+    // (software-pipelined: a wave loads its next pair's C tile and operands before the current
+    // pair's products, so one global round trip per pair overlaps the matrix-core work)
     const int m = T - k - 1, npair = m * (m + 1) / 2;
-    for (int pi = w; pi < npair; pi += 4) {
+    if (w < npair) {
       int I, J;
-      tile_ij(pi, I, J);
+      tile_ij(w, I, J);
       I += k + 1;
       J += k + 1;
       f64x4 c[2][2];
+      TileFrag f;
       tile_load<false>(c, Lt + tile_at(I, J), lane);
-      tile_xyt<true>(c, Lt + tile_at(I, k), Lt + tile_at(J, k), lane);
-      tile_store<false>(c, Lt + tile_at(I, J), lane);
+      frag_load(f, Lt + tile_at(I, k), Lt + tile_at(J, k), lane);
+      for (int pi = w; pi < npair; pi += 4) {
+        const bool more = pi + 4 < npair;
+        int In = I, Jn = J;
+        f64x4 cn[2][2];
+        TileFrag fn;
+        if (more) {
+          tile_ij(pi + 4, In, Jn);
+          In += k + 1;
+          Jn += k + 1;
+          tile_load<false>(cn, Lt + tile_at(In, Jn), lane);
+          frag_load(fn, Lt + tile_at(In, k), Lt + tile_at(Jn, k), lane);
+        }
+        frag_sub(c, f);
+        tile_store<false>(c, Lt + tile_at(I, J), lane);
+        if (more) {
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) c[bi][bj] = cn[bi][bj];
+          f = fn;
+          I = In;
+          J = Jn;
+        }
+      }
     }
     __syncthreads();
     TT_STAMP(4);
