@@ -750,12 +750,11 @@ __device__ __forceinline__ void frag_load(TileFrag& f, const double* X, const do
     f.b[s][1] = Y[(4 * s + kk) * TT + 16 + r];
   }
 }
-// c ±= X·Yᵀ from the fragments (tile_xyt's products, in its order)
-template <bool NEG>
-__device__ __forceinline__ void frag_mma(f64x4 (&c)[2][2], const TileFrag& f) {
+// c −= X·Yᵀ from the fragments (tile_xyt<true>'s products, in its order)
+__device__ __forceinline__ void frag_sub(f64x4 (&c)[2][2], const TileFrag& f) {
 #pragma unroll
   for (int s = 0; s < TT / 4; ++s) {
-    const double a0 = NEG ? -f.a[s][0] : f.a[s][0], a1 = NEG ? -f.a[s][1] : f.a[s][1];
+    const double a0 = -f.a[s][0], a1 = -f.a[s][1];
     c[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, f.b[s][0], c[0][0], 0, 0, 0);
     c[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, f.b[s][1], c[0][1], 0, 0, 0);
     c[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, f.b[s][0], c[1][0], 0, 0, 0);
@@ -801,21 +800,6 @@ template <int... R>
 __device__ __forceinline__ void tt_panel(double (&v)[TT], const double* Dk, const double* rd, int i,
                                          std::integer_sequence<int, R...>) {
   ((tt_subst_step<R>(v, v[R], Dk[i * TT_LD + R], rd[R])), ...);
-}
-
-// c ±= Σ_{m0 ≤ M < m1} X_M·Y_Mᵀ (tile_xyt over a chain of tiles) with tile M + 1's operands
-// loaded while tile M's products run
-template <bool NEG, class XF, class YF>
-__device__ __forceinline__ void tile_chain(f64x4 (&c)[2][2], int m0, int m1, XF xat, YF yat, int lane) {
-  if (m0 >= m1) return;
-  TileFrag f;
-  frag_load(f, xat(m0), yat(m0), lane);
-  for (int M = m0; M < m1; ++M) {
-    TileFrag fn = f;
-    if (M + 1 < m1) frag_load(fn, xat(M + 1), yat(M + 1), lane);
-    frag_mma<NEG>(c, f);
-    f = fn;
-  }
 }
 
 // -DMRBO_GPFIT_STAMPS: cycles per phase of candidate 0 (thread 0, after each workgroup barrier):
@@ -1054,7 +1038,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
           tile_load<false>(cn, Lt + tile_at(In, Jn), lane);
           frag_load(fn, Lt + tile_at(In, k), Lt + tile_at(Jn, k), lane);
         }
-        frag_mma<true>(c, f);
+        frag_sub(c, f);
         tile_store<false>(c, Lt + tile_at(I, J), lane);
         if (more) {
 #pragma unroll
@@ -1087,8 +1071,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     for (int J = w; J < I; J += 4) {
       f64x4 c[2][2];
       tile_zero(c);
-      tile_chain<false>(c, J, I, [&](int M) { return Lt + tile_at(I, M); }, [&](int M) { return Vt + tile_at(M, J); },
-                        lane);   // Σ_M L_IM·V_MJ
+      for (int M = J; M < I; ++M) tile_xyt<false>(c, Lt + tile_at(I, M), Vt + tile_at(M, J), lane);   // L_IM·V_MJ
       double* S = Sw + w * (TT * TT);
       tile_store<true>(c, S, lane);
       gr_sync();
@@ -1172,8 +1155,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     }
     f64x4 c[2][2];
     tile_zero(c);
-    tile_chain<false>(c, I, T, [&](int M) { return Vt + tile_at(M, I); }, [&](int M) { return Vt + tile_at(M, J); },
-                      lane);   // Σ_M V_MIᵀ·V_MJ
+    for (int M = I; M < T; ++M) tile_xyt<false>(c, Vt + tile_at(M, I), Vt + tile_at(M, J), lane);   // V_MIᵀ·V_MJ
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int bi = e >> 3, bj = (e >> 2) & 1, j = e & 3;
