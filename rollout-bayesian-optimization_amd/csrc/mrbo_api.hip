@@ -1080,10 +1080,14 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
   {
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipEventRecord(gev[1], st);
+    // the small outputs of a host call come back on the same stream (into pinned memory), so
+    // one synchronisation covers the kernel and the copy
+    if (e == hipSuccess && host) e = hipMemcpyAsync(pin_out.p, dll_, out_bytes, hipMemcpyDeviceToHost, st);
     const hipError_t es = hipStreamSynchronize(st);
     if (es != hipSuccess) {
       sg.abandon();
       pin_in.abandon();
+      pin_out.abandon();
       return fail(MRBO_ERR_HIP, "gp_fit: hipStreamSynchronize: %s", hipGetErrorString(es));
     }
     if (e != hipSuccess) return fail(MRBO_ERR_HIP, "gp_fit launch: %s", hipGetErrorString(e));
@@ -1093,7 +1097,6 @@ int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t np, int32_t nt, const d
     if (hipEventElapsedTime(&ms, gev[0], gev[1]) == hipSuccess) g_gpfit_ms = ms;
   }
   if (host) {
-    HIP_TRY(hipMemcpy(pin_out.p, dll_, out_bytes, hipMemcpyDeviceToHost));
     const double* h = (const double*)pin_out.p;
     std::memcpy(ll, h, sizeof(double) * P);
     std::memcpy(grad, h + P, sizeof(double) * NTP);
