@@ -1014,9 +1014,8 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     __syncthreads();
     TT_STAMP(3);
     // trailing update A_IJ −= L_Ik·L_Jkᵀ, k < J ≤ I
-    // (software-pipelined: a wave loads its next pair's operands before the current pair's
-    // products and its C tile right after their stores, so the global round trips overlap the
-    // matrix-core work)
+    // (software-pipelined: a wave loads its next pair's C tile and operands before the current
+    // pair's products, so one global round trip per pair overlaps the matrix-core work)
     const int m = T - k - 1, npair = m * (m + 1) / 2;
     if (w < npair) {
       int I, J;
@@ -1030,17 +1029,22 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
       for (int pi = w; pi < npair; pi += 4) {
         const bool more = pi + 4 < npair;
         int In = I, Jn = J;
+        f64x4 cn[2][2];
         TileFrag fn;
         if (more) {
           tile_ij(pi + 4, In, Jn);
           In += k + 1;
           Jn += k + 1;
+          tile_load<false>(cn, Lt + tile_at(In, Jn), lane);
           frag_load(fn, Lt + tile_at(In, k), Lt + tile_at(Jn, k), lane);
         }
         frag_sub(c, f);
         tile_store<false>(c, Lt + tile_at(I, J), lane);
         if (more) {
-          tile_load<false>(c, Lt + tile_at(In, Jn), lane);   // in flight during the stores above
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) c[bi][bj] = cn[bi][bj];
           f = fn;
           I = In;
           J = Jn;
