@@ -282,6 +282,7 @@ __global__ void __launch_bounds__(64 * GR_WAVES) gpfit_reg_kernel(GpFitParams q,
   double* DK = LV + 64 * GR_LD;         // δK_t (symmetric) at t·64·LD + i·LD + j
   double* cs = DK + NT * 64 * GR_LD;    // c
   double* XS = cs + 64;                 // X[u][j] at u·64 + j (u < d)
+  double* VS = XS + 16 * 64;            // V = L⁻¹, row-major (m·LD + j)
   const int N = q.N, d = q.d;
   const bool act = lane < N;
   double ell, per;
@@ -292,47 +293,74 @@ __global__ void __launch_bounds__(64 * GR_WAVES) gpfit_reg_kernel(GpFitParams q,
   GR_STAMP(0);
   // K (eval_KXX :161-178, ψ(0) + σn2 on the diagonal; padding = identity) and δK_t (eval_Dθ_KXX
   // :264-284) over the 2080 pairs j ≤ i of the lower triangle, lanes over pairs, both halves written
-  for (int q0 = 0; q0 < 64 * 65 / 2; q0 += 64 * GR_WAVES) {
-    const int qq = q0 + tid;
-    if (qq >= 64 * 65 / 2) break;
-    int i = (int)((sqrt(8.0 * qq + 1.0) - 1.0) * 0.5);
-    i += ((i + 1) * (i + 2) / 2 <= qq) ? 1 : 0;   // exact row of the triangle index
-    i -= (i * (i + 1) / 2 > qq) ? 1 : 0;
-    const int j = qq - i * (i + 1) / 2;
-    double r2 = 0.0;
+  // (two pairs per thread and pass as independent chains: one wave per SIMD, nothing else hides
+  // the LDS and transcendental latencies)
+  constexpr int NPAIR = 64 * 65 / 2;
+  for (int q0 = 0; q0 < NPAIR; q0 += 2 * 64 * GR_WAVES) {
+    int ii[2], jj[2];
+    double r2[2] = {0.0, 0.0};
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int qq = min(q0 + 64 * GR_WAVES * e + tid, NPAIR - 1);
+      int i = (int)((sqrt(8.0 * qq + 1.0) - 1.0) * 0.5);
+      i += ((i + 1) * (i + 2) / 2 <= qq) ? 1 : 0;   // exact row of the triangle index
+      i -= (i * (i + 1) / 2 > qq) ? 1 : 0;
+      ii[e] = i;
+      jj[e] = qq - i * (i + 1) / 2;
+    }
 #pragma unroll
     for (int u = 0; u < 16; ++u)
-      if (u < d) { const double r = XS[u * 64 + i] - XS[u * 64 + j]; r2 = fma(r, r, r2); }
-    double psi, dps[2];
-    psi_dtheta(q.kernel, ell, per, (i == j) ? 0.0 : sqrt(r2), psi, dps);
-    const bool v = i < N;   // j ≤ i
-    const double kij = v ? ((i == j) ? psi + q.sn2 : psi) : ((i == j) ? 1.0 : 0.0);
-    LV[i * GR_LD + j] = kij;
-    LV[j * GR_LD + i] = kij;
+      if (u < d) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const double dk = (v && i != j) ? dps[t] : 0.0;
-      DK[t * 64 * GR_LD + i * GR_LD + j] = dk;
-      DK[t * 64 * GR_LD + j * GR_LD + i] = dk;
+        for (int e = 0; e < 2; ++e) {
+          const double r = XS[u * 64 + ii[e]] - XS[u * 64 + jj[e]];
+          r2[e] = fma(r, r, r2[e]);
+        }
+      }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int i = ii[e], j = jj[e];
+      double psi, dps[2];
+      psi_dtheta(q.kernel, ell, per, (i == j) ? 0.0 : sqrt(r2[e]), psi, dps);
+      if (q0 + 64 * GR_WAVES * e + tid < NPAIR) {
+        const bool v = i < N;   // j ≤ i
+        const double kij = v ? ((i == j) ? psi + q.sn2 : psi) : ((i == j) ? 1.0 : 0.0);
+        LV[i * GR_LD + j] = kij;
+        LV[j * GR_LD + i] = kij;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const double dk = (v && i != j) ? dps[t] : 0.0;
+          DK[t * 64 * GR_LD + i * GR_LD + j] = dk;
+          DK[t * 64 * GR_LD + j * GR_LD + i] = dk;
+        }
+      }
     }
   }
   __syncthreads();
   GR_STAMP(1);
-  // wave 0: the register phases; the other waves wait at the next barrier
+  // wave 0: the Cholesky in registers; then wave 0 solves for c while wave 1 forms V = L⁻¹
   __shared__ double part[GR_WAVES][2 * NT + 2];   // per-wave partial sums; [0][2NT..] = yc, log det
   __shared__ int failed;
-  if (tid < 64) {
-    double a[4][16];
+  const int w = tid >> 6;
+  double a[4][16];
+  double dg = 1.0;
+  if (w == 0) {
 #pragma unroll
     for (int j = 0; j < 64; ++j) a[j / 16][j % 16] = LV[lane * GR_LD + j];
     // right-looking Cholesky in registers (PosDefException → status 1); dg = L_ii of this row
-    double dg = 1.0;
     const bool chol_ok = gr_chol(a, dg, lane, std::make_integer_sequence<int, 64>{});
     GR_STAMP(2);
     gr_sync();
 #pragma unroll
     for (int j = 0; j < 64; ++j) LV[lane * GR_LD + j] = a[j / 16][j % 16];
-    gr_sync();
+    const double ld = gr_sum(act ? log(dg) : 0.0);
+    if (lane == 0) {
+      failed = !chol_ok;
+      part[0][2 * NT + 1] = ld;
+    }
+  }
+  __syncthreads();
+  if (w == 0) {
     // c = L'\(L\y), column-oriented substitutions (ck broadcast by readlane)
     const double rdg = 1.0 / dg;
     double c = act ? q.y[lane] : 0.0;
@@ -340,23 +368,20 @@ __global__ void __launch_bounds__(64 * GR_WAVES) gpfit_reg_kernel(GpFitParams q,
     GR_STAMP(3);
     cs[lane] = c;
     const double yc = gr_sum(act ? q.y[lane] * c : 0.0);
-    const double ld = gr_sum(act ? log(dg) : 0.0);
-    // V = L⁻¹ by columns (lane j = column j), rows ascending (rows ≥ N: identity, no effect on rows < N)
+    if (lane == 0) part[0][2 * NT] = yc;
+  } else if (w == 1) {
+    // V = L⁻¹ by columns (lane j = column j), rows ascending (rows ≥ N: identity, no effect on
+    // rows < N); 1/L_jj from the stored factor (the same division wave 0 makes)
+    const double rdg = 1.0 / LV[lane * GR_LD + lane];
     double v[64];
 #pragma unroll
     for (int r = 0; r < 64; ++r) v[r] = 0.0;
     gr_inv(v, LV, rdg, lane, N, std::make_integer_sequence<int, 64>{});
-    gr_sync();
 #pragma unroll
-    for (int m = 0; m < 64; ++m) LV[m * GR_LD + lane] = v[m];   // V row-major for every wave
-    if (lane == 0) {
-      failed = !chol_ok;
-      part[0][2 * NT] = yc;
-      part[0][2 * NT + 1] = ld;
-    }
-    GR_STAMP(4);
+    for (int m = 0; m < 64; ++m) VS[m * GR_LD + lane] = v[m];   // V row-major for every wave
   }
   __syncthreads();
+  GR_STAMP(4);
   if (failed) {
     if (tid == 0) {
       q.ll[p] = NAN;
@@ -367,10 +392,9 @@ __global__ void __launch_bounds__(64 * GR_WAVES) gpfit_reg_kernel(GpFitParams q,
   }
   // tr(K⁻¹δK_t) = Σ_ib K⁻¹_ib δK_t[i][b] and cᵀδK_t c = Σ_ib c_i δK_t[i][b] c_b (full sums; δK_ii = 0).
   // Wave w: K⁻¹ columns b of block w (K⁻¹ = VᵀV by DPP broadcasts of V[m][b]), lane i = row.
-  const int w = tid >> 6;
   double v[64];
 #pragma unroll
-  for (int m = 0; m < 64; ++m) v[m] = LV[m * GR_LD + lane];
+  for (int m = 0; m < 64; ++m) v[m] = VS[m * GR_LD + lane];
   const double c = cs[lane];
   double kb[16];
 #pragma unroll
@@ -415,7 +439,7 @@ __global__ void __launch_bounds__(64 * GR_WAVES) gpfit_reg_kernel(GpFitParams q,
   }
 #ifdef MRBO_GPFIT_STAMPS
   if (p == 0 && tid == 0)
-    printf("gpfit_reg cycles: X %llu  K rows %llu  chol %llu  c %llu  inv %llu  traces %llu\n", gr_ts[0] - gr_t0,
+    printf("gpfit_reg cycles: X %llu  K rows %llu  chol %llu  c %llu  inv beyond c %llu  traces %llu\n", gr_ts[0] - gr_t0,
            gr_ts[1] - gr_ts[0], gr_ts[2] - gr_ts[1], gr_ts[3] - gr_ts[2], gr_ts[4] - gr_ts[3], gr_ts[5] - gr_ts[4]);
 #endif
 }
@@ -1217,7 +1241,7 @@ size_t gpfit_tile_work_doubles(int N, int nt) {
 
 size_t gpfit_lds_bytes() { return sizeof(double) * ((size_t)GL_N * GL_LD + 16 * GL_N + 3 * GL_N); }
 
-size_t gpfit_reg_lds(int nt) { return sizeof(double) * ((size_t)(1 + nt) * 64 * GR_LD + 64 + 16 * 64); }
+size_t gpfit_reg_lds(int nt) { return sizeof(double) * ((size_t)(2 + nt) * 64 * GR_LD + 64 + 16 * 64); }
 
 size_t gpfit_launch_lds(const GpFitParams& q) {
   if (gpfit_in_regs(q)) return gpfit_reg_lds(q.nt);
