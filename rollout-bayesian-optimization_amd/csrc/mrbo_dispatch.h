@@ -77,10 +77,12 @@ size_t gpfit_tile_work_doubles(int N, int nt);
 // d·⌈N/32⌉·32 doubles, so large d can exceed the CU's 160 KB)
 size_t gpfit_launch_lds(const GpFitParams& q);
 void launch_gpfit(int P, hipStream_t st, const GpFitParams& q);
-// N ≤ 64, d ≤ 16 and no factor / coefficient outputs: the one-wave-per-candidate register kernel
-// (no workspace)
+// 32 < N ≤ 64, d ≤ 16 and no factor / coefficient outputs: the one-wave-per-candidate register
+// kernel (no workspace).  N ≤ 32 is one tile of the tile kernel: its register factor and inverse
+// of a 32 × 32 tile do a quarter of the 64-row kernel's work (N = 32: 0.045 ms per 256 candidates
+// in the register kernel)
 inline bool gpfit_in_regs(const GpFitParams& q) {
-  return q.N <= 64 && q.d <= 16 && !q.L_out && !q.c_out;
+  return q.N > 32 && q.N <= 64 && q.d <= 16 && !q.L_out && !q.c_out;
 }
 // 64 < N ≤ 80 (and N ≤ 64 with factor outputs): gpfit_lds_kernel, no global workspace.  The
 // ceiling is measured: the tile kernel pads N to a multiple of 32 and overtakes
@@ -90,7 +92,7 @@ inline bool gpfit_in_regs(const GpFitParams& q) {
 #define MRBO_GPFIT_LDS_MAX 80
 #endif
 inline bool gpfit_in_lds(const GpFitParams& q) {
-  return q.N <= MRBO_GPFIT_LDS_MAX && q.d <= 16 && !gpfit_in_regs(q);
+  return q.N > 32 && q.N <= MRBO_GPFIT_LDS_MAX && q.d <= 16 && !gpfit_in_regs(q);
 }
 
 }  // namespace mrbo

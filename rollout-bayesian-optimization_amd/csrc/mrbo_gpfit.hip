@@ -10,16 +10,18 @@
 // which optimize! (radial_basis_surrogates.jl:805-829) evaluates once per L-BFGS iterate.
 // θ = (ℓ) for the Matérn / SE kernels, (ℓ, p) for Periodic (radial_basis_functions.jl:98-103).
 //
-// N ≤ 64, no factor output (gpfit_reg_kernel): one workgroup per candidate whose four waves
+// N ≤ 32: gpfit_tile_kernel (below) on its single 32 × 32 tile -- the register factor, inverse
+// and substitutions of the diagonal step without a panel (a quarter of the 64-row kernel's work).
+// 32 < N ≤ 64, no factor output (gpfit_reg_kernel): one workgroup per candidate whose four waves
 // evaluate K and δK (one per SIMD); then ONE WAVE, lane i owning row i of K in REGISTERS.  The right-looking Cholesky broadcasts column k with DPP row_newbcast fused into
 // v_fmac_f64 (the column's 16-row blocks replicated by permlane swaps, gpfit_asm.h), so the
 // N³/6 trailing updates run at the FMA rate with no LDS round trip; c by substitution with
 // readlane broadcasts; V = L⁻¹ by columns (lane j = column j) and K⁻¹ = VᵀV with the same DPP
 // broadcasts; tr(K⁻¹δK) and cᵀδKc from K⁻¹.  K and δK are evaluated once per pair j ≤ i.  The
 // reference's operations (chol, then triangular solves); summation orders differ (tolerance).
-// 64 < N ≤ MRBO_GPFIT_LDS_MAX (80), or N ≤ 64 with L / c requested: gpfit_lds_kernel (below;
+// 64 < N ≤ MRBO_GPFIT_LDS_MAX (80), or 32 < N ≤ 64 with L / c requested: gpfit_lds_kernel (below;
 // everything in LDS; it holds candidates up to N = 128, but the tile kernel is faster above 80).
-// 128 < N ≤ 512: gpfit_tile_kernel (below): one workgroup per candidate, the blocked algorithm on
+// 80 < N ≤ 512: gpfit_tile_kernel (below): one workgroup per candidate, the blocked algorithm on
 // 32 × 32 tiles in a global workspace with the tile products on the fp64 matrix cores.
 #include <hip/hip_runtime.h>
 

@@ -173,7 +173,7 @@ def test_gp_fit_vs_oracle(gpu, oracle, kernel, d, N):
     ells = np.array([0.2, 0.5, 1.0, 2.0, 4.0]) * np.sqrt(d) * (0.15 if kernel == "se" else 1.0)
     s = _surrogate(X, y, kernel, 1.0)
     r = gp_fit_batch(s, ells, want_fit=True)
-    rr = gp_fit_batch(s, ells)   # N ≤ 64: the register kernel; N ≤ 80: the LDS kernel (no factor outputs)
+    rr = gp_fit_batch(s, ells)   # no factor outputs: N ≤ 32 the tile kernel, ≤ 64 the register kernel, ≤ 80 the LDS kernel
     for p, ell in enumerate(ells):
         ll, dll, L, c = oracle.log_likelihood(X, y, kernel, ell, 1e-6, want_fit=True)
         if np.isnan(ll):
