@@ -58,7 +58,7 @@ for step in "$@"; do
       AB_TAG="" timeout -k 10 400 bash tools/ab_run.sh ${AB_VARIANTS:-old new oldst newst} > "$out/ab.log" 2>&1
       rc=$?; cp gpurun_out/ab_*.json gpurun_out/ab_*.err "$out/" 2>/dev/null; grep -v "^\[mrbo stamps\] .* 0.00%" "$out/ab.log" | tail -60 ;;
     gpfit)
-      timeout -k 10 400 python -u tools/bench_rows.py --rows gp_fit --cpu-seconds 2 > "$out/gpfit_rows.jsonl" 2> "$out/gpfit_rows.err"
+      timeout -k 10 400 python -u tools/bench_rows.py --rows gp_fit --gpfit-n ${GPFIT_N:-64,128,256,384,512} --cpu-seconds 2 > "$out/gpfit_rows.jsonl" 2> "$out/gpfit_rows.err"
       rc=$?; python -c "
 import sys, json
 for l in open(sys.argv[1]):
