@@ -55,11 +55,12 @@ def parse():
                     help="cost-weighted EI with NonUniformCost (cost_functions.jl:5-20; build-defined, "
                          "parity unpinned)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--schedule", choices=("auto", "index", "longest-first"), default="index",
-                    help="order in which the persistent waves take the trajectories: index order "
-                         "(default), or longest first by the first step's work counters; auto = longest "
-                         "first when the launch is at most two rounds of the resident waves deep (C2: "
-                         "kernel 0.56 -> 0.53 ms; at C3's 32 rounds it measured 1 %% slower; DESIGN.md §9)")
+    ap.add_argument("--schedule", choices=("auto", "index", "longest-first"), default="auto",
+                    help="order in which the persistent waves take the trajectories: index order, or "
+                         "longest first by the first step's work counters; auto (default) = longest first "
+                         "when the launch is at most two rounds of the resident waves deep, index order "
+                         "otherwise (C2: kernel 0.544 -> 0.518 ms, 7.34 -> 7.71 M traj/s; at C3's 32 rounds "
+                         "longest first measured 1 %% slower, so C3 stays in index order; DESIGN.md §9)")
     ap.add_argument("--longest-first", action="store_true", help="same as --schedule longest-first")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--solver", choices=("sga", "adam"), default="sga",
