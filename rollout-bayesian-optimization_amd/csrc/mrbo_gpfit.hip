@@ -706,17 +706,6 @@ __global__ void __launch_bounds__(GL_THREADS) gpfit_lds_kernel(GpFitParams q, in
 //   lower entries (δK stored by the K pass; δK_ii = 0), as the LDS kernel above does.
 // ≈ N³/2 multiply-adds (N³/6 each for L, V and K⁻¹), all but the diagonal tiles' on the MFMA pipe.
 constexpr int TT = 32, TT_THREADS = 256, TT_LD = 33;
-// LDS doubles of the tile kernel: X, Dk, Wk, rd, the per-wave scratch, y/c, z, 1/L_ii -- plus, when
-// the whole lower triangle of tiles fits beside them (T ≤ 4), a padded copy of L for the backward
-// substitution (conflict-free column walks; its global loads were that phase's cost)
-__host__ __device__ inline size_t tt_base_doubles(int d, int N) {
-  const size_t NP = (size_t)((N + TT - 1) / TT) * TT;
-  return (size_t)d * NP + 2 * TT * TT_LD + TT + 4 * TT * TT + 3 * NP;
-}
-__host__ __device__ inline size_t tt_stage_doubles(int d, int N) {
-  const size_t T = (N + TT - 1) / TT, st = T * (T + 1) / 2 * (TT * TT_LD);
-  return (T <= 4 && (tt_base_doubles(d, N) + st) * sizeof(double) <= 160 * 1024) ? st : 0;
-}
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 // c[bi][bj][j] holds tile entry (16·bi + (lane >> 4) + 4·j, 16·bj + (lane & 15)) (the f64 MFMA's
@@ -870,8 +859,6 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   double* yv = Sw + 4 * TT * TT;         // y, then c
   double* uv = yv + NP;                  // z = L⁻¹y
   double* rdall = uv + NP;               // 1/L_ii of every row (the substitutions multiply)
-  double* LS = rdall + NP;                // staged L tiles (tt_stage_doubles), TT_LD-padded columns
-  const bool stage_l = tt_stage_doubles(d, N) > 0;
   __shared__ double part[TT_THREADS / 64][2 * NT + 2];
   __shared__ int fail;
   double ell, per;
@@ -1127,31 +1114,21 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   // c_I = L_II⁻ᵀ(z_I − Σ_{J>I} L_JIᵀ c_J);
   // inside a tile the column-oriented substitution with the solved entry broadcast by readlane.
   // yᵀc as the reference's log_likelihood forms it.
-  if (stage_l) {
-    for (int e = tid; e < (int)ntile * (TT * TT); e += TT_THREADS) {
-      const int t = e >> 10, c = (e >> 5) & 31, r = e & 31;
-      LS[t * (TT * TT_LD) + c * TT_LD + r] = Lt[e];
-    }
-    __syncthreads();
-  }
   if (w == 0) {
     const int i = lane & 31;
     double yc = 0.0;
-    // tile (I, J)'s column i, entry j: staged in LDS or in the workspace
-    auto lcol = [&](int I, int J, int j) {
-      return stage_l ? LS[(tile_at(I, J) >> 10) * (TT * TT_LD) + i * TT_LD + j] : Lt[tile_at(I, J) + i * TT + j];
-    };
     // (z = L⁻¹y is in uv: the factorisation's diagonal steps and panels formed it; the
     // backward tiles' loads are software-pipelined: tile J + 1's loads are in flight during tile
     // J's products, which run as four partial sums)
     for (int I = T - 1; I >= 0; --I) {
       double r = uv[TT * I + i];
       double lm[TT], lj[TT];
+      const double* LD_ = Lt + tile_at(I, I);
 #pragma unroll
-      for (int m = 0; m < TT; ++m) lm[m] = lcol(I, I, m);
+      for (int m = 0; m < TT; ++m) lm[m] = LD_[i * TT + m];
       if (I + 1 < T) {
 #pragma unroll
-        for (int j = 0; j < TT; ++j) lj[j] = lcol(I + 1, I, j);
+        for (int j = 0; j < TT; ++j) lj[j] = Lt[tile_at(I + 1, I) + i * TT + j];
       }
       double r4[4] = {0.0, 0.0, 0.0, 0.0};
       for (int J = I + 1; J < T; ++J) {
@@ -1160,7 +1137,7 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
         for (int j = 0; j < TT; ++j) cur[j] = lj[j];
         if (J + 1 < T) {
 #pragma unroll
-          for (int j = 0; j < TT; ++j) lj[j] = lcol(J + 1, I, j);
+          for (int j = 0; j < TT; ++j) lj[j] = Lt[tile_at(J + 1, I) + i * TT + j];
         }
 #pragma unroll
         for (int j = 0; j < TT; ++j) r4[j & 3] = fma(-cur[j], yv[TT * J + j], r4[j & 3]);
@@ -1254,7 +1231,10 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
     for (int i = tid; i < N; i += TT_THREADS) q.c_out[(size_t)N * p + i] = yv[i];
 }
 
-size_t gpfit_tile_lds(int d, int N) { return sizeof(double) * (tt_base_doubles(d, N) + tt_stage_doubles(d, N)); }
+size_t gpfit_tile_lds(int d, int N) {
+  const int NP = ((N + TT - 1) / TT) * TT;
+  return sizeof(double) * ((size_t)d * NP + 2 * TT * TT_LD + TT + 4 * TT * TT + 3 * (size_t)NP);
+}
 
 size_t gpfit_tile_work_doubles(int N, int nt) {
   const size_t T = (N + TT - 1) / TT, ntile = T * (T + 1) / 2;
