@@ -34,33 +34,39 @@ namespace mrbo {
 
 // ψ(ρ) and ∂ψ/∂θ_t(ρ) for the radial kernels (radial_basis_functions.jl:60-103; ∇θ_ψ by
 // ForwardDiff there, closed forms here).  dps[0] = ∂/∂ℓ; Periodic also dps[1] = ∂/∂p.
+// Divisions by the candidate's constants are multiplications by reciprocals formed once per
+// candidate (1/ℓ, 1/3, 1/p: loop invariants the compiler hoists out of the pair loops): an IEEE
+// f64 division is a ten-instruction dependent chain, three per entry in the Matérn 5/2 case.
 __device__ __forceinline__ void psi_dtheta(int kind, double ell, double per, double rho, double& psi,
                                            double (&dps)[2]) {
+  constexpr double third = 1.0 / 3.0;
+  const double il = 1.0 / ell;
   dps[1] = 0.0;
   if (kind == 4) {  // Periodic: exp(−2 sin²(πρ/p)/ℓ²)
-    const double u = 3.141592653589793 * rho / per, su = sin(u), il2 = 1.0 / (ell * ell);
+    const double ip = 1.0 / per;
+    const double u = 3.141592653589793 * rho * ip, su = sin(u), il2 = il * il;
     psi = exp(-2.0 * su * su * il2);
-    dps[0] = psi * 4.0 * su * su * il2 / ell;                                   // ∂/∂ℓ
-    dps[1] = psi * 2.0 * u * il2 * sin(2.0 * u) / per;                          // ∂/∂p = ψ·2πρ sin(2u)/(ℓ²p²)
+    dps[0] = psi * 4.0 * su * su * il2 * il;                                    // ∂/∂ℓ
+    dps[1] = psi * 2.0 * u * il2 * sin(2.0 * u) * ip;                           // ∂/∂p = ψ·2πρ sin(2u)/(ℓ²p²)
     return;
   }
   if (kind == 3) {  // SE: exp(−ρ²/(2ℓ²))
-    const double t = rho * rho / (ell * ell);
+    const double t = rho * rho * (il * il);
     psi = exp(-0.5 * t);
-    dps[0] = psi * t / ell;
+    dps[0] = psi * t * il;
     return;
   }
-  const double c = (kind == 0) ? sqrt(5.0) / ell : (kind == 1) ? sqrt(3.0) / ell : 1.0 / ell;
+  const double c = (kind == 0) ? sqrt(5.0) * il : (kind == 1) ? sqrt(3.0) * il : il;
   const double s = c * rho, e = exp(-s);
   if (kind == 0) {          // (1+s+s²/3)e⁻ˢ ; ∂/∂ℓ = (s²/3)(1+s)e⁻ˢ/ℓ
-    psi = (1.0 + s * (1.0 + s / 3.0)) * e;
-    dps[0] = (s * s / 3.0) * (1.0 + s) * e / ell;
+    psi = (1.0 + s * (1.0 + s * third)) * e;
+    dps[0] = (s * s * third) * (1.0 + s) * e * il;
   } else if (kind == 1) {   // (1+s)e⁻ˢ ; ∂/∂ℓ = s²e⁻ˢ/ℓ
     psi = (1.0 + s) * e;
-    dps[0] = s * s * e / ell;
+    dps[0] = s * s * e * il;
   } else {                  // e⁻ˢ ; ∂/∂ℓ = s e⁻ˢ/ℓ
     psi = e;
-    dps[0] = s * e / ell;
+    dps[0] = s * e * il;
   }
 }
 
