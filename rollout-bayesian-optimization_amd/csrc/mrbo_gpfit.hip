@@ -25,6 +25,7 @@
 // 32 × 32 tiles in a global workspace with the tile products on the fp64 matrix cores.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
 #include <utility>
 
 #include "mrbo_dispatch.h"
@@ -37,36 +38,44 @@ namespace mrbo {
 // Divisions by the candidate's constants are multiplications by reciprocals formed once per
 // candidate (1/ℓ, 1/3, 1/p: loop invariants the compiler hoists out of the pair loops): an IEEE
 // f64 division is a ten-instruction dependent chain, three per entry in the Matérn 5/2 case.
-__device__ __forceinline__ void psi_dtheta(int kind, double ell, double per, double rho, double& psi,
-                                           double (&dps)[2]) {
+template <int KIND>
+__device__ __forceinline__ void psi_dtheta_k(double ell, double per, double rho, double& psi, double (&dps)[2]) {
   constexpr double third = 1.0 / 3.0;
   const double il = 1.0 / ell;
   dps[1] = 0.0;
-  if (kind == 4) {  // Periodic: exp(−2 sin²(πρ/p)/ℓ²)
+  if constexpr (KIND == 4) {  // Periodic: exp(−2 sin²(πρ/p)/ℓ²)
     const double ip = 1.0 / per;
     const double u = 3.141592653589793 * rho * ip, su = sin(u), il2 = il * il;
     psi = exp(-2.0 * su * su * il2);
     dps[0] = psi * 4.0 * su * su * il2 * il;                                    // ∂/∂ℓ
     dps[1] = psi * 2.0 * u * il2 * sin(2.0 * u) * ip;                           // ∂/∂p = ψ·2πρ sin(2u)/(ℓ²p²)
-    return;
-  }
-  if (kind == 3) {  // SE: exp(−ρ²/(2ℓ²))
+  } else if constexpr (KIND == 3) {  // SE: exp(−ρ²/(2ℓ²))
     const double t = rho * rho * (il * il);
     psi = exp(-0.5 * t);
     dps[0] = psi * t * il;
-    return;
+  } else {
+    const double c = (KIND == 0) ? sqrt(5.0) * il : (KIND == 1) ? sqrt(3.0) * il : il;
+    const double s = c * rho, e = exp(-s);
+    if constexpr (KIND == 0) {          // (1+s+s²/3)e⁻ˢ ; ∂/∂ℓ = (s²/3)(1+s)e⁻ˢ/ℓ
+      psi = (1.0 + s * (1.0 + s * third)) * e;
+      dps[0] = (s * s * third) * (1.0 + s) * e * il;
+    } else if constexpr (KIND == 1) {   // (1+s)e⁻ˢ ; ∂/∂ℓ = s²e⁻ˢ/ℓ
+      psi = (1.0 + s) * e;
+      dps[0] = s * s * e * il;
+    } else {                            // e⁻ˢ ; ∂/∂ℓ = s e⁻ˢ/ℓ
+      psi = e;
+      dps[0] = s * e * il;
+    }
   }
-  const double c = (kind == 0) ? sqrt(5.0) * il : (kind == 1) ? sqrt(3.0) * il : il;
-  const double s = c * rho, e = exp(-s);
-  if (kind == 0) {          // (1+s+s²/3)e⁻ˢ ; ∂/∂ℓ = (s²/3)(1+s)e⁻ˢ/ℓ
-    psi = (1.0 + s * (1.0 + s * third)) * e;
-    dps[0] = (s * s * third) * (1.0 + s) * e * il;
-  } else if (kind == 1) {   // (1+s)e⁻ˢ ; ∂/∂ℓ = s²e⁻ˢ/ℓ
-    psi = (1.0 + s) * e;
-    dps[0] = s * s * e * il;
-  } else {                  // e⁻ˢ ; ∂/∂ℓ = s e⁻ˢ/ℓ
-    psi = e;
-    dps[0] = s * e * il;
+}
+__device__ __forceinline__ void psi_dtheta(int kind, double ell, double per, double rho, double& psi,
+                                           double (&dps)[2]) {
+  switch (kind) {
+    case 0: psi_dtheta_k<0>(ell, per, rho, psi, dps); break;
+    case 1: psi_dtheta_k<1>(ell, per, rho, psi, dps); break;
+    case 2: psi_dtheta_k<2>(ell, per, rho, psi, dps); break;
+    case 3: psi_dtheta_k<3>(ell, per, rho, psi, dps); break;
+    default: psi_dtheta_k<4>(ell, per, rho, psi, dps); break;
   }
 }
 
@@ -889,36 +898,46 @@ __global__ void __launch_bounds__(TT_THREADS) gpfit_tile_kernel(GpFitParams q, i
   // as four independent chains (one wave per SIMD: the chains' interleaving is the latency
   // hiding), with the row's coordinates loaded once per dimension.
   static_assert(TT * TT == 4 * TT_THREADS, "K pass: four entries per thread and tile");
-  for (int qt = 0; qt < (int)ntile; ++qt) {
-    int I, J;
-    tile_ij(qt, I, J);
-    const int gi = TT * I + (tid & 31), gj0 = TT * J + (tid >> 5);
-    double r2[4] = {0.0, 0.0, 0.0, 0.0};
+  // (the kernel kind is dispatched once around the pass, and every entry is evaluated without a
+  // branch -- padding and upper entries on a dummy radius, selected away -- so that the four
+  // chains really interleave instead of running as four exec-masked regions)
+  auto kpass = [&](auto kind_c) {
+    constexpr int KIND = decltype(kind_c)::value;
+    for (int qt = 0; qt < (int)ntile; ++qt) {
+      int I, J;
+      tile_ij(qt, I, J);
+      const int gi = TT * I + (tid & 31), gj0 = TT * J + (tid >> 5);
+      double r2[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 3
-    for (int u = 0; u < d; ++u) {
-      const double* xu = XS + (size_t)u * NP;
-      const double xi = xu[gi];
+      for (int u = 0; u < d; ++u) {
+        const double* xu = XS + (size_t)u * NP;
+        const double xi = xu[gi];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const double r = xi - xu[gj0 + 8 * m];
+          r2[m] = fma(r, r, r2[m]);
+        }
+      }
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        const double r = xi - xu[gj0 + 8 * m];
-        r2[m] = fma(r, r, r2[m]);
+        const int gj = gj0 + 8 * m;
+        const size_t e = (size_t)qt * (TT * TT) + tid + TT_THREADS * m;
+        const bool ok = gi < N && gj < N && gj <= gi;
+        double psi, dps[2];
+        psi_dtheta_k<KIND>(ell, per, (gi == gj || !ok) ? 0.0 : sqrt(r2[m]), psi, dps);
+        Lt[e] = ok ? ((gi == gj) ? psi + q.sn2 : psi) : ((gi == gj) ? 1.0 : 0.0);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)   // the same bits the traces used to recompute
+          Dt[(size_t)t * ntile * (TT * TT) + e] = ok ? dps[t] : 0.0;
       }
     }
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int gj = gj0 + 8 * m;
-      const size_t e = (size_t)qt * (TT * TT) + tid + TT_THREADS * m;
-      double v = (gi == gj) ? 1.0 : 0.0;
-      double dps[2] = {0.0, 0.0};
-      if (gi < N && gj < N && gj <= gi) {
-        double psi;
-        psi_dtheta(q.kernel, ell, per, (gi == gj) ? 0.0 : sqrt(r2[m]), psi, dps);
-        v = (gi == gj) ? psi + q.sn2 : psi;
-      }
-      Lt[e] = v;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) Dt[(size_t)t * ntile * (TT * TT) + e] = dps[t];   // the same bits the traces used to recompute
-    }
+  };
+  switch (q.kernel) {
+    case 0: kpass(std::integral_constant<int, 0>{}); break;
+    case 1: kpass(std::integral_constant<int, 1>{}); break;
+    case 2: kpass(std::integral_constant<int, 2>{}); break;
+    case 3: kpass(std::integral_constant<int, 3>{}); break;
+    default: kpass(std::integral_constant<int, 4>{}); break;
   }
   __syncthreads();
   TT_STAMP(1);
