@@ -313,6 +313,9 @@ __global__ void __launch_bounds__(64 * GR_WAVES) gpfit_reg_kernel(GpFitParams q,
   // (two pairs per thread and pass as independent chains: one wave per SIMD, nothing else hides
   // the LDS and transcendental latencies)
   constexpr int NPAIR = 64 * 65 / 2;
+  // (the kernel kind dispatched once around the pass: the two chains interleave)
+  auto kpairs = [&](auto kind_c) {
+  constexpr int KIND = decltype(kind_c)::value;
   for (int q0 = 0; q0 < NPAIR; q0 += 2 * 64 * GR_WAVES) {
     int ii[2], jj[2];
     double r2[2] = {0.0, 0.0};
@@ -338,7 +341,7 @@ __global__ void __launch_bounds__(64 * GR_WAVES) gpfit_reg_kernel(GpFitParams q,
     for (int e = 0; e < 2; ++e) {
       const int i = ii[e], j = jj[e];
       double psi, dps[2];
-      psi_dtheta(q.kernel, ell, per, (i == j) ? 0.0 : sqrt(r2[e]), psi, dps);
+      psi_dtheta_k<KIND>(ell, per, (i == j) ? 0.0 : sqrt(r2[e]), psi, dps);
       if (q0 + 64 * GR_WAVES * e + tid < NPAIR) {
         const bool v = i < N;   // j ≤ i
         const double kij = v ? ((i == j) ? psi + q.sn2 : psi) : ((i == j) ? 1.0 : 0.0);
@@ -352,6 +355,14 @@ __global__ void __launch_bounds__(64 * GR_WAVES) gpfit_reg_kernel(GpFitParams q,
         }
       }
     }
+  }
+  };
+  switch (q.kernel) {
+    case 0: kpairs(std::integral_constant<int, 0>{}); break;
+    case 1: kpairs(std::integral_constant<int, 1>{}); break;
+    case 2: kpairs(std::integral_constant<int, 2>{}); break;
+    case 3: kpairs(std::integral_constant<int, 3>{}); break;
+    default: kpairs(std::integral_constant<int, 4>{}); break;
   }
   __syncthreads();
   GR_STAMP(1);
