@@ -299,6 +299,9 @@ def main():
     elapsed = float(el.item())
     # HIP events around each timed step's rollout kernel alone, on its launch stream (mrbo_kernel_times)
     kernel_ms = plan.kernel_times(args.steps) if args.steps > 0 else []
+    if args.steps > len(kernel_ms):
+        print(f"bench: kernel_ms averages the last {len(kernel_ms)} of {args.steps} timed launches (event ring)",
+              file=sys.stderr)
     last["eto"] = last["eto_dev"].cpu().numpy().reshape((W, R), order="F")
     x0 = from_device(dx0, (d, R))
     active = dactive.cpu().numpy().astype(bool)
@@ -346,6 +349,7 @@ def main():
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": f"rollout_kernel<{d},{info['rpl']},{info['spec']}>", "kernel_ms": kms, "flops_per_launch": fl,
+                     "kernel_ms_launches": len(kernel_ms),   # the plan keeps the last 64 launches' events
                      "launch": info,
                      "note": "compute-bound fp64: peak = the dense fp64 matrix peak, equal to the fp64 vector "
                              "peak on MI355X; the kernel issues VALU v_fma_f64 (matrix-vector work, not "

@@ -120,7 +120,9 @@ typedef struct {
   double sigma_tol;     /* EI / POI σtol (decision_rules.jl:84, :102) = 1e-8     */
   uint64_t seed;        /* δx for solve_dual_y (rollout.jl:133) when dual_y_dx == NULL */
   int32_t sample_offset;/* global index of this plan's first MC sample (multi-GPU shard), 0 */
-  int32_t samples_total;/* global MC samples per restart (0 → M); keys the δx counter RNG  */
+  int32_t samples_total;/* global MC samples per restart (0 → M); informational: the δx     */
+                        /* counter RNG is keyed by the global sample index alone (round 5),*/
+                        /* so restart r of a launch equals an R = 1 launch at its x0       */
   int32_t cost;         /* mrbo_cost_t: NonUniformCost weighting of the inner-solve rule      */
   double cost_c0;       /* cost family parameter c0                                          */
   const double* cost_w; /* d weights, HOST (NULL with MRBO_COST_NONE)                        */
@@ -242,10 +244,12 @@ int mrbo_base_solve(mrbo_plan_t* plan, int32_t n, const double* xstarts, double*
  * status[p] = 0, or 1 when cholesky throws PosDefException (ll, grad = NaN).  L_out (N×N×P,
  * lower, zeros above) and c_out (N×P) are optional (NULL).  thetas / ll / grad / status / L_out
  * / c_out are device pointers unless MRBO_FLAG_HOST_POINTERS; N ≤ 512 (every N the rollout
- * accepts).  N ≤ 80 runs without workspace (one wave per candidate at N ≤ 64 without L_out /
- * c_out, the candidate in LDS up to N = 80); N > 80 runs the 32 × 32-tile kernel on the fp64
- * matrix cores with ((2 + nt)·T(T+1)/2 + T)·1024·P doubles of workspace, T = ⌈N/32⌉, allocated for the
- * call.  Synchronises the stream before returning.                                          */
+ * accepts).  Kernel by size: N ≤ 32 (and any N > 80) runs the 32 × 32-tile kernel on the fp64
+ * matrix cores with ((2 + nt)·T(T+1)/2 + T)·1024·P doubles of workspace, T = ⌈N/32⌉, from the
+ * per-device pool; 32 < N ≤ 64 with d ≤ 16 and without L_out / c_out runs the register kernel
+ * (one candidate per workgroup, no workspace); otherwise 32 < N ≤ 80 with d ≤ 16 runs the LDS
+ * kernel (the candidate in LDS, no workspace); d > 16 runs the tile kernel.  A configuration whose LDS (dynamic + the kernel's static arrays) exceeds
+ * the device limit fails with MRBO_ERR_UNSUPPORTED.  Synchronises the stream before returning. */
 int mrbo_gp_fit_theta(const mrbo_surrogate_t* s, int32_t P, int32_t nt, const double* thetas, double* ll,
                       double* grad, int32_t* status, double* L_out, double* c_out, uint32_t flags, void* stream);
 /* mrbo_gp_fit_theta with nt = 1: ells[p] = ℓ_p, dll[p] = ∂ll/∂ℓ (Periodic: p = s->period). */

@@ -1140,7 +1140,7 @@ static int run_trajectory(const traj_in* in, int r, int m, const double* x0, fsu
       double dx[16];
       for (int k = 0; k < d; ++k)
         dx[k] = in->dual_y_dx ? in->dual_y_dx[(int64_t)k + (int64_t)d * ((j - 1) + (int64_t)h * (m + (int64_t)M * r))]
-                              : rbo_dual_uniform(p->seed, (int64_t)(p->sample_offset + m) + (int64_t)(p->samples_total > 0 ? p->samples_total : M) * r, j, k);
+                              : rbo_dual_uniform(p->seed, (int64_t)(p->sample_offset + m), j, k);
       double yd = 0;
       for (int i = j; i <= t; ++i) {
         perturb_grad(fs, &rec[i], i - 1, j - 1, dx, 1, p->theta, p->sigma_tol, sc, col);

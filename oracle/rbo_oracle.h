@@ -67,7 +67,8 @@ typedef struct {
   double sigma_tol;        /* EI σtol (decision_rules.jl:84)                     */
   uint64_t seed;           /* counter-based δx for solve_dual_y when dual_y_dx==NULL */
   int32_t sample_offset;   /* global index of the first sample (sharded runs), 0      */
-  int32_t samples_total;   /* global samples per restart keying the δx RNG (0 → M)    */
+  int32_t samples_total;   /* global samples per restart (informational; the δx RNG is */
+                           /* keyed by the global sample index sample_offset + m)      */
   int32_t with_gradient;
   int32_t nthreads;        /* OpenMP threads for the (restart, sample) loop      */
   int32_t rule;            /* RBO_RULE_* base decision rule of the trajectory    */

@@ -708,7 +708,8 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
        hipMemcpy(P->dlbs, P->lbs.data(), sizeof(double) * d, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(P->dubs, P->ubs.data(), sizeof(double) * d, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemset(P->dwork, 0, sizeof(double) * (size_t)slots * P->work_stride) == hipSuccess;
-  for (int k = 0; ok && k < 2 * mrbo_plan::NEV; ++k) ok = hipEventCreate(&P->ev[k]) == hipSuccess;
+  // the timing ring's events are created on first use by a launch (launch_events), not here: a plan
+  // used for a few launches (the Julia drop-in's R = 1 calls) creates only what it records
   if (!ok) {
     mrbo_plan_destroy(P);
     return fail(MRBO_ERR_NOMEM, "device allocation failed");
@@ -787,6 +788,10 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
     HIP_TRY(hipGetLastError());
   }
   const int slot = (int)(P->nlaunch % mrbo_plan::NEV);
+  if (!P->ev[2 * slot]) {   // lazily created ring slot (destroyed with the plan)
+    HIP_TRY(hipEventCreate(&P->ev[2 * slot]));
+    HIP_TRY(hipEventCreate(&P->ev[2 * slot + 1]));
+  }
   HIP_TRY(hipEventRecord(P->ev[2 * slot], st));
   launch_rollout(d, P->RPL, P->fx, P->spec, dim3(P->blocks), dim3(P->wpg * WAVE), P->smem, st, kp);
   HIP_TRY(hipGetLastError());
@@ -1131,6 +1136,7 @@ int mrbo_plan_info(const mrbo_plan_t* P, int32_t* info, int32_t n) {
 static double launch_ms(mrbo_plan_t* P, long long launch) {
   const int slot = (int)(launch % mrbo_plan::NEV);
   float ms = -1.f;
+  if (!P->ev[2 * slot] || !P->ev[2 * slot + 1]) return -1.0;
   if (hipEventSynchronize(P->ev[2 * slot + 1]) != hipSuccess) return -1.0;
   if (hipEventElapsedTime(&ms, P->ev[2 * slot], P->ev[2 * slot + 1]) != hipSuccess) return -1.0;
   return ms;

@@ -1281,10 +1281,25 @@ size_t gpfit_lds_bytes() { return sizeof(double) * ((size_t)GL_N * GL_LD + 16 * 
 
 size_t gpfit_reg_lds(int nt) { return sizeof(double) * ((size_t)(2 + nt) * 64 * GR_LD + 64 + 16 * 64); }
 
+// dynamic LDS of the launch plus the selected kernel's static __shared__ arrays (part[][], the
+// failure flags), so that mrbo_gp_fit_theta's limit check sees what the launch will request
 size_t gpfit_launch_lds(const GpFitParams& q) {
-  if (gpfit_in_regs(q)) return gpfit_reg_lds(q.nt);
-  if (gpfit_in_lds(q)) return gpfit_lds_bytes();
-  return gpfit_tile_lds(q.d, q.N);
+  size_t dyn;
+  const void* fn;
+  if (gpfit_in_regs(q)) {
+    dyn = gpfit_reg_lds(q.nt);
+    fn = q.nt == 2 ? (const void*)gpfit_reg_kernel<2> : (const void*)gpfit_reg_kernel<1>;
+  } else if (gpfit_in_lds(q)) {
+    dyn = gpfit_lds_bytes();
+    fn = q.nt == 2 ? (const void*)gpfit_lds_kernel<2> : (const void*)gpfit_lds_kernel<1>;
+  } else {
+    dyn = gpfit_tile_lds(q.d, q.N);
+    fn = q.nt == 2 ? (const void*)gpfit_tile_kernel<2> : (const void*)gpfit_tile_kernel<1>;
+  }
+  hipFuncAttributes fa{};
+  if (hipFuncGetAttributes(&fa, fn) == hipSuccess) dyn += fa.sharedSizeBytes;
+  else dyn += 4096;   // attributes unavailable: keep a margin for the static arrays
+  return dyn;
 }
 
 void launch_gpfit(int P, hipStream_t st, const GpFitParams& q) {

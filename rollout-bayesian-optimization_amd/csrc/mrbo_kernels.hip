@@ -22,7 +22,14 @@
 
 namespace mrbo {
 
+// MRBO_AB_MIN (A/B variant builds of one configuration only, tools/build_variants.sh): the unit holds
+// RPL = 1 and the specialised kernel alone (it also stands in for the generic one), so a variant of
+// the N ≤ 64 kernel compiles in seconds instead of minutes; plans of other shapes fail to create.
+#ifdef MRBO_AB_MIN
+constexpr bool has_rpl(int d, int rpl) { return rpl == 1; }
+#else
 constexpr bool has_rpl(int d, int rpl) { return rpl == 1 || rpl == 2 || (d <= 8 && (rpl == 4 || rpl == 8)); }
+#endif
 constexpr bool has_spec(int d, int rpl) { return d <= 8 && rpl <= 4; }
 
 template <int D, int RPL>
@@ -30,12 +37,21 @@ static KernelSet kset() {
   using Ly = Lay<D, RPL>;
   const void* spec = nullptr;
   if constexpr (has_spec(D, RPL)) spec = (const void*)&rollout_kernel<D, RPL, 1>;
+#ifdef MRBO_AB_MIN
+  return KernelSet{spec, spec, (const void*)&eval_base_kernel<D, RPL>,
+#else
   return KernelSet{(const void*)&rollout_kernel<D, RPL, 0>, spec, (const void*)&eval_base_kernel<D, RPL>,
+#endif
                    sizeof(double) * Ly::WAVE_LDS, Ly::SQ, Ly::BC && !Ly::SQ, Ly::LD, Ly::LINV_DOUBLES, Ly::GL,
                    Ly::LINV_GLOBAL, KBounds<D, RPL>::threads};
 }
 
 bool MRBO_SFX(kset_d)(int rpl, KernelSet& ks) {
+#ifdef MRBO_AB_MIN
+  if (rpl != 1) return false;
+  ks = kset<MRBO_D, 1>();
+  return true;
+#else
   if (rpl == 1) ks = kset<MRBO_D, 1>();
   else if (rpl == 2) ks = kset<MRBO_D, 2>();
 #if MRBO_D <= 8
@@ -44,12 +60,18 @@ bool MRBO_SFX(kset_d)(int rpl, KernelSet& ks) {
 #endif
   else return false;
   return true;
+#endif
 }
 
 template <int RPL, int SPEC>
 static void launch_one(dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
+#ifdef MRBO_AB_MIN
+  if constexpr (has_rpl(MRBO_D, RPL) && has_spec(MRBO_D, RPL))
+    hipLaunchKernelGGL((rollout_kernel<MRBO_D, RPL, 1>), g, b, sm, st, kp);
+#else
   if constexpr (has_rpl(MRBO_D, RPL) && (SPEC == 0 || has_spec(MRBO_D, RPL)))
     hipLaunchKernelGGL((rollout_kernel<MRBO_D, RPL, SPEC>), g, b, sm, st, kp);
+#endif
 }
 
 template <int SPEC>

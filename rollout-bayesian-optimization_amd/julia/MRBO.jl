@@ -33,7 +33,7 @@ using Main: Surrogate, Trajectory, TrajectoryParameters, ExpectedTrajectoryOutpu
             get_spatial_bounds, get_starting_point, get_base_surrogate, set_start!
 import Distributions
 
-export MrboBackend, MrboPlan, mrbo_multistart_base_solve!, mrbo_log_likelihood
+export MrboBackend, MrboPlan, mrbo_multistart_base_solve!, mrbo_log_likelihood, mrbo_release_plans!
 
 const libmrbo = joinpath(@__DIR__, "..", "mrbo", "libmrbo.so")
 const MRBO_FLAG_HOST_POINTERS = UInt32(1)
@@ -108,9 +108,11 @@ mrbo_rule_id(g) = get_name(g) == "EI" ? Int32(0) : get_name(g) == "POI" ? Int32(
                   get_name(g) == "LCB" ? Int32(2) : error("decision rule not compiled into libmrbo")
 
 # The device state of simulate_trajectory_mc's setup: FantasySurrogate(s, h) over the base
-# surrogate (radial_basis_surrogates.jl:345-381) + TrajectoryParameters (trajectory.jl:43-94).
+# surrogate (radial_basis_surrogates.jl:345-381) + TrajectoryParameters (trajectory.jl:43-94),
+# for R restart points per launch.  The caller owns the returned plan and must release it with
+# mrbo_plan_destroy!; the rollout methods below take theirs from the plan cache instead.
 function MrboPlan(s::Surrogate, tp::TrajectoryParameters, θ::Vector{Float64}, nstarts::Int;
-                  device::Int = 0, max_iters = 50, max_ls = 20, seed = 1906, M::Int = tp.mc_iters)
+                  device::Int = 0, max_iters = 50, max_ls = 20, seed = 1906, M::Int = tp.mc_iters, R::Int = 1)
     N = get_observed(s)
     X = Matrix{Float64}(get_active_covariates(s))
     L = Matrix{Float64}(get_active_cholesky(s))
@@ -123,15 +125,66 @@ function MrboPlan(s::Surrogate, tp::TrajectoryParameters, θ::Vector{Float64}, n
         sd = MrboSurrogateC(Int32(size(X, 1)), Int32(N), mrbo_kernel_id(get_kernel(s)), get_kernel(s).θ[1], s.σn2,
                             fmini, pointer(X), pointer(L), Int32(N), pointer(c), pointer(y),
                             mrbo_kernel_period(get_kernel(s)))
-        pd = MrboParamsC(Int32(tp.horizon), Int32(M), Int32(1), Int32(nstarts), mrbo_rule_id(get_decision_rule(s)),
+        pd = MrboParamsC(Int32(tp.horizon), Int32(M), Int32(R), Int32(nstarts), mrbo_rule_id(get_decision_rule(s)),
                          θ[1], pointer(lbs), pointer(ubs), Int32(max_iters), Int32(max_ls), 1e-3, 1e-3, 1e-8,
                          1e-4, 1e-8, UInt64(seed), Int32(0), Int32(0), Int32(0), 1.0, Ptr{Float64}(C_NULL))
         mrbo_check(ccall((:mrbo_plan_create, libmrbo), Cint,
                          (Ref{MrboSurrogateC}, Ref{MrboParamsC}, Cint, Ref{Ptr{Cvoid}}), sd, pd, device, h))
     end
-    plan = MrboPlan(h[], size(X, 1), M, 1, tp.horizon)
-    finalizer(p -> ccall((:mrbo_plan_destroy, libmrbo), Cint, (Ptr{Cvoid},), p.handle), plan)
-    return plan
+    return MrboPlan(h[], size(X, 1), M, R, tp.horizon)
+end
+
+# Deterministic release of a plan's device memory (Julia's GC does not see device memory, so no
+# finalizer is used: a plan lives until it is destroyed here).  Idempotent.
+function mrbo_plan_destroy!(p::MrboPlan)
+    if p.handle != C_NULL
+        mrbo_check(ccall((:mrbo_plan_destroy, libmrbo), Cint, (Ptr{Cvoid},), p.handle))
+        p.handle = C_NULL
+    end
+    return nothing
+end
+
+# ---- plan cache ------------------------------------------------------------------------------
+# The reference's outer ascent (stochastic_solve, utils.jl:235-265) calls simulate_trajectory_mc
+# up to 50 times per restart on the same surrogate and TrajectoryParameters, moving only x0; a
+# plan per call would pack L0⁻¹ on the host, copy the surrogate to HBM and allocate the launch
+# workspace every time.  One plan per (surrogate state, tp, θ, start count, M, R, device) is built
+# once and reused -- the key holds the surrogate's identity AND a hash of its active data, so a
+# conditioned or refitted surrogate gets a new plan.  At most MRBO_PLAN_CACHE_MAX plans live:
+# beyond that every cached plan is destroyed (mrbo_plan_destroy!) before the new one is built, and
+# mrbo_release_plans!() empties the cache explicitly (also run at exit).
+const MRBO_PLAN_CACHE_MAX = 8
+const PLAN_CACHE = Dict{Any, MrboPlan}()
+
+function mrbo_release_plans!()
+    for p in values(PLAN_CACHE)
+        mrbo_plan_destroy!(p)
+    end
+    empty!(PLAN_CACHE)
+    return nothing
+end
+
+function mrbo_plan_key(s::Surrogate, tp::TrajectoryParameters, θ::Vector{Float64}, nstarts::Int, device::Int,
+                       M::Int, R::Int)
+    lbs, ubs = get_spatial_bounds(tp)
+    return (objectid(s), get_observed(s), hash(get_active_covariates(s)), hash(get_active_observations(s)),
+            hash(get_active_cholesky(s)), hash(get_observations(s)), hash(get_kernel(s).θ), s.σn2,
+            get_name(get_decision_rule(s)), tp.horizon, hash(lbs), hash(ubs), θ[1], nstarts, M, R, device)
+end
+
+function mrbo_cached_plan(s::Surrogate, tp::TrajectoryParameters, θ::Vector{Float64}, nstarts::Int;
+                          device::Int = 0, M::Int = tp.mc_iters, R::Int = 1)
+    key = mrbo_plan_key(s, tp, θ, nstarts, device, M, R)
+    p = get(PLAN_CACHE, key, nothing)
+    p === nothing || return p
+    length(PLAN_CACHE) >= MRBO_PLAN_CACHE_MAX && mrbo_release_plans!()
+    p = MrboPlan(s, tp, θ, nstarts; device = device, M = M, R = R)
+    PLAN_CACHE[key] = p
+    return p
+end
+
+function __init__()
+    atexit(mrbo_release_plans!)
 end
 
 # ExpectedTrajectoryOutput tail of rollout.jl:328-339 (the reference's own reductions)
@@ -152,7 +205,7 @@ function simulate_trajectory_mc(T::Trajectory, tp::TrajectoryParameters, backend
                                 spatial_gradients_container::Union{Nothing, Matrix{Float64}} = nothing,
                                 hyperparameter_gradients_container::Union{Nothing, Matrix{Float64}} = nothing)
     set_start!(T, get_starting_point(tp))
-    plan = MrboPlan(get_base_surrogate(T), tp, T.θ, size(inner_solve_xstarts, 2); device = backend.device)
+    plan = mrbo_cached_plan(get_base_surrogate(T), tp, T.θ, size(inner_solve_xstarts, 2); device = backend.device)
     with_grad = !isnothing(spatial_gradients_container) && !isnothing(hyperparameter_gradients_container)
     x0 = copy(T.x0)
     rns = tp.rnstream_sequence
@@ -173,6 +226,48 @@ function simulate_trajectory_mc(T::Trajectory, tp::TrajectoryParameters, backend
     return mrbo_eto(resolutions, with_grad ? gx : nothing, with_grad ? gθ : nothing)
 end
 
+# Batched restarts: the x0 batch of the outer ascent (generate_batch, utils.jl:97-106) as the
+# columns of X0, all of them in ONE launch (R = size(X0, 2) restarts × tp.mc_iters samples on the
+# GPU at once; the R = 1 method above puts one x0's 1 024 trajectories on a chip with ≈ 2 048
+# resident waves).  Returns one ExpectedTrajectoryOutput per column, each equal to the R = 1
+# method's result at that x0 (every trajectory is computed independently of the others in its
+# launch; tests/test_gpu.py holds the two call sequences bit for bit).  The optional containers are
+# the reference's per restart, stacked: resolutions M×R, spatial gradients d×M×R, hyperparameter
+# gradients 1×M×R (overwritten in place).  T is not modified (T.θ is used, Q12).
+function simulate_trajectory_mc(T::Trajectory, tp::TrajectoryParameters, X0::Matrix{Float64}, backend::MrboBackend;
+                                inner_solve_xstarts::Matrix{Float64}, with_gradient::Bool = true,
+                                resolutions::Matrix{Float64} = Matrix{Float64}(undef, tp.mc_iters, size(X0, 2)),
+                                spatial_gradients::Union{Nothing, Array{Float64, 3}} = nothing,
+                                hyperparameter_gradients::Union{Nothing, Array{Float64, 3}} = nothing)
+    d, R = size(X0)
+    M = tp.mc_iters
+    size(resolutions) == (M, R) || throw(DimensionMismatch("resolutions must be $M×$R"))
+    gx = with_grad_container(spatial_gradients, with_gradient, d, M, R)
+    gθ = with_grad_container(hyperparameter_gradients, with_gradient, 1, M, R)
+    plan = mrbo_cached_plan(get_base_surrogate(T), tp, T.θ, size(inner_solve_xstarts, 2); device = backend.device,
+                            R = R)
+    rns = tp.rnstream_sequence
+    status = zeros(Int32, M, R)
+    flags = MRBO_FLAG_HOST_POINTERS | (with_gradient ? UInt32(0) : MRBO_FLAG_NO_GRADIENT)
+    GC.@preserve X0 rns inner_solve_xstarts resolutions gx gθ status begin
+        mrbo_check(ccall((:mrbo_simulate_mc, libmrbo), Cint,
+                         (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                          Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Ptr{Float64},
+                          Ptr{Int64}, UInt32, Ptr{Cvoid}),
+                         plan.handle, X0, rns, inner_solve_xstarts, C_NULL, C_NULL, resolutions,
+                         with_gradient ? pointer(gx) : C_NULL, with_gradient ? pointer(gθ) : C_NULL, status,
+                         C_NULL, C_NULL, C_NULL, flags, C_NULL))
+    end
+    any(!=(0), status) && throw(ErrorException("rollout failed on $(count(!=(0), status)) trajectories (status bits $(reduce(|, status)))"))
+    return [mrbo_eto(resolutions[:, r], with_gradient ? gx[:, :, r] : nothing, with_gradient ? gθ[:, :, r] : nothing)
+            for r in 1:R]
+end
+
+with_grad_container(c, with_gradient, a, M, R) =
+    !with_gradient ? Array{Float64, 3}(undef, 0, 0, 0) :
+    isnothing(c) ? Array{Float64, 3}(undef, a, M, R) :
+    size(c) == (a, M, R) ? c : throw(DimensionMismatch("gradient container must be $a×$M×$R"))
+
 # The GPU method of simulate_trajectory_ghq (rollout.jl:409-467): node vectors nodes[indices[m]]
 # and weights[indices[m]] as M×(h+1) matrices for mrbo_simulate_ghq.
 function simulate_trajectory_ghq(T::Trajectory, tp::TrajectoryParameters, backend::MrboBackend;
@@ -189,7 +284,8 @@ function simulate_trajectory_ghq(T::Trajectory, tp::TrajectoryParameters, backen
         tn[m, :] .= nodes[collect(idx)]
         tw[m, :] .= weights[collect(idx)]
     end
-    plan = MrboPlan(get_base_surrogate(T), tp, T.θ, size(inner_solve_xstarts, 2); device = backend.device, M = M)
+    plan = mrbo_cached_plan(get_base_surrogate(T), tp, T.θ, size(inner_solve_xstarts, 2); device = backend.device,
+                            M = M)
     with_grad = !isnothing(spatial_gradients_container) && !isnothing(hyperparameter_gradients_container)
     x0 = copy(T.x0)
     status = zeros(Int32, M)

@@ -310,3 +310,59 @@ def test_device_adam_step_matches_host(gpu):
         np.testing.assert_array_equal(from_device(dm, (d, R)), m)
         np.testing.assert_array_equal(from_device(dv, (d, R)), v)
         np.testing.assert_array_equal(from_device(dx, (d, R)), x0)
+
+
+def test_shim_call_sequence_matches_batched_launch(gpu):
+    """The Julia drop-in's call sequence (mrbo.shim, the Python mirror of julia/MRBO.jl: R = 1,
+    host pointers, plans from the bounded cache) against its batched method, bit for bit: every
+    restart's R = 1 launch equals that restart's column of one batched launch (values, ∇x, ∇θ and
+    the ETO), and the reference's outer loop (stochastic_solve, utils.jl:235-265: 50 iterations,
+    eswavs, StandardSGA) driven through the R = 1 method reaches the same x0 as the batched loop,
+    with every call's per-trajectory outputs equal -- on ONE plan reused for all of its calls."""
+    from mrbo import configs, shim
+    M, R = 256, 8
+    pb = configs.problem("C3", M=M, R=R)
+    T, tp, xs = pb.T, pb.tp, pb.es.get_starts()
+    d = pb.x0s.shape[0]
+    shim.release_plans()
+    etos, vals, gx, gt = shim.simulate_trajectory_mc_batch(T, tp, pb.x0s, xs)
+    assert (vals > 0).mean() > 0.25 and (np.abs(gx).max(axis=0) > 0).mean() > 0.1   # not vacuous
+    n0 = shim.stats["plans_created"]
+    for r in range(R):
+        tp.set_starting_point(pb.x0s[:, r].copy())
+        res, g, t = np.zeros(M), np.zeros((d, M), order="F"), np.zeros((1, M), order="F")
+        e = shim.simulate_trajectory_mc(T, tp, xs, res, g, t)
+        np.testing.assert_array_equal(res, vals[:, r])
+        np.testing.assert_array_equal(g, gx[:, :, r])
+        np.testing.assert_array_equal(t, gt[:, :, r])
+        assert e.μxθ == etos[r].μxθ and e.σ_μxθ == etos[r].σ_μxθ
+        np.testing.assert_array_equal(e.gradient(), etos[r].gradient())
+    assert shim.stats["plans_created"] == n0 + 1          # one R = 1 plan served every restart
+    # the outer loop: batched (all restarts per launch) vs the R = 1 sequence per restart
+    x = np.array(pb.x0s, dtype=np.float64, order="F")
+    active = np.ones(R, dtype=bool)
+    steps = np.zeros(R, dtype=int)
+    hist = []
+    for _ in range(50):
+        if not active.any():
+            break
+        es_, v_, g_, _ = shim.simulate_trajectory_mc_batch(T, tp, x, xs)
+        hist.append((v_, g_))
+        for r in np.flatnonzero(active):
+            steps[r] += 1
+            if shim.eswavs(es_[r].gradient(), es_[r].std_gradient() ** 2, M):
+                active[r] = False
+            else:
+                x[:, r] = x[:, r] + 0.01 * es_[r].gradient()
+    n1 = shim.stats["plans_created"]
+    for r in range(R):
+        trace = []
+        xr = shim.stochastic_solve(T, tp, xs, pb.x0s[:, r], eta=0.01, trace=trace)
+        np.testing.assert_array_equal(xr, x[:, r])
+        assert len(trace) == steps[r]
+        for k, (rv, rg) in enumerate(trace):
+            np.testing.assert_array_equal(rv, hist[k][0][:, r])
+            np.testing.assert_array_equal(rg, hist[k][1][:, :, r])
+    assert shim.stats["plans_created"] == n1               # the cached R = 1 plan, reused
+    assert steps.max() > 1                                  # the loop moved x0
+    shim.release_plans()

@@ -313,3 +313,19 @@ def test_adam_step_batch_equals_per_restart_rules():
             assert opts[r].t == t
             np.testing.assert_array_equal(opts[r].m[-1], m[:, r])
             np.testing.assert_array_equal(opts[r].v[-1], v[:, r])
+
+
+def test_tight_value_check_has_teeth():
+    """tests/parity.py's tight value check (rel 1e-9, absolute floor 1e-12·max|v|)
+    flags a per-trajectory error 1000× the measured C3 one, which the first-order bound vb alone
+    (~1e5× above the measured errors) would let through."""
+    import numpy as np
+    from parity import tight_value_stats, value_bound_stats
+    rng = np.random.default_rng(0)
+    v = rng.uniform(1e-4, 1.0, 4096)
+    err = 5e-14 * np.ones_like(v)                  # the C3 launch's largest replay error (abs)
+    vb = 3e-9 * np.ones_like(v)                    # the order of the C3 bounds
+    assert tight_value_stats(err, v, v.max())["over_tight"] == 0
+    worse = 1000 * err
+    assert value_bound_stats(worse, vb)["over_bound"] == 0      # the bound alone misses it
+    assert tight_value_stats(worse, v, v.max())["over_tight"] > 0

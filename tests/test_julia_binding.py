@@ -324,3 +324,55 @@ def test_integration_doc_matches_the_shim():
     for name in re.findall(r"\b(mrbo_\w+!?)\(", doc):
         if name.endswith("!") or name in ("mrbo_log_likelihood",):
             assert re.search(rf"(?m)^function {re.escape(name)}\(", src), name
+
+
+def _functions(shim):
+    """(name, body) of every top-level `function … end` block (the shim indents bodies, so a
+    function ends at the first `end` in column 0)."""
+    return re.findall(rf"(?ms)^function\s+({IDENT})\s*\((.*?)^end\b", shim)
+
+
+def test_plan_lifecycle_is_deterministic(shim):
+    """Every device plan the shim creates is released deterministically: no
+    GC finalizer (Julia's GC does not see device memory); a function that calls mrbo_plan_create
+    directly destroys the handle in a `finally` block unless it is the MrboPlan constructor; every
+    MrboPlan(…) construction outside the constructor goes into the bounded plan cache; the cache's
+    eviction and release path calls mrbo_plan_destroy!, which calls mrbo_plan_destroy; and the
+    rollout methods (R = 1, batched, Gauss–Hermite) take their plans from that cache."""
+    assert "finalizer(" not in shim
+    funcs = _functions(shim)
+    names = [n for n, _ in funcs]
+    body = dict(zip(names, (b for _, b in funcs)))
+    creators = [n for n, b in funcs if "mrbo_plan_create" in b]
+    assert creators, "no mrbo_plan_create call found"
+    for n, b in funcs:
+        if "mrbo_plan_create" not in b or n == "MrboPlan":
+            continue
+        fin = b.split("finally", 1)
+        assert len(fin) == 2 and "mrbo_plan_destroy" in fin[1], f"{n}: plan created without try … finally destroy"
+    # constructions of MrboPlan(…) with surrogate arguments outside the constructor itself
+    for n, b in funcs:
+        if n == "MrboPlan":
+            continue
+        for m in re.finditer(r"\bMrboPlan\s*\(", b):
+            assert n == "mrbo_cached_plan", f"{n} builds an MrboPlan outside the cache"
+    cp = body["mrbo_cached_plan"]
+    assert "PLAN_CACHE[key] = p" in cp and "MRBO_PLAN_CACHE_MAX" in cp and "mrbo_release_plans!()" in cp
+    assert "mrbo_plan_destroy!(p)" in body["mrbo_release_plans!"] and "empty!(PLAN_CACHE)" in body["mrbo_release_plans!"]
+    assert "mrbo_plan_destroy" in body["mrbo_plan_destroy!"] and "C_NULL" in body["mrbo_plan_destroy!"]
+    assert "atexit(mrbo_release_plans!)" in body["__init__"]
+    uses = [b for n, b in funcs if n in ("simulate_trajectory_mc", "simulate_trajectory_ghq")]
+    # two simulate_trajectory_mc methods (R = 1 and batched) + the ghq method
+    assert len(uses) == 3 and all("mrbo_cached_plan(" in b for b in uses)
+
+
+def test_batched_method_shapes(shim):
+    """The batched simulate_trajectory_mc method (one launch for the x0 batch of generate_batch,
+    utils.jl:97-106) passes R = size(X0, 2) to its plan and M×R / d×M×R containers to the C ABI,
+    and returns one ExpectedTrajectoryOutput per restart."""
+    funcs = [b for n, b in _functions(shim) if n == "simulate_trajectory_mc"]
+    bat = [b for b in funcs if "X0::Matrix{Float64}" in b]
+    assert len(bat) == 1
+    b = bat[0]
+    assert "R = R" in b and "d, R = size(X0)" in b and "zeros(Int32, M, R)" in b
+    assert "for r in 1:R]" in b and "mrbo_eto(" in b

@@ -428,6 +428,10 @@ def test_value_bound_covers_two_oracle_builds(oracle):
         assert np.isfinite(vb).all() and (vb > 0).all()
         dv = np.abs(a["values"] - b["values"])
         assert (dv <= vb).all(), (name, float((dv / vb).max()))
+        # the tight check (rel 1e-9, floor 1e-12·max|v|) holds between the two builds as well
+        from parity import tight_value_stats
+        ts = tight_value_stats(dv.ravel(), b["values"].ravel(), np.abs(b["values"]).max())
+        assert ts["over_tight"] == 0, (name, ts)
         nz += int((dv > 0).sum())
         assert (a["ylip"] >= 0).all()
     assert nz > 0

@@ -1,0 +1,76 @@
+#!/bin/bash
+# Round-5 GPU session: a chain of steps, each under its own time limit, stopping at the first
+# failure.  usage (on the box, from the repo root): bash tools/gpu_r04.sh <tag> step [step ...]
+#   tests     pytest -m gpu (all GPU tests; parity statistics -> parity.json)
+#   smoke     __graft_entry__.smoke()
+#   bench     python bench.py (the driver's default line, C3)
+#   rows      bench rows: C3 at the MLE ℓ, C4 at ℓ = 0.5 and MLE, C2 (no CPU baseline)
+#   ab        A/B of the library variants in mrbo/variants (AB_VARIANTS, default "old new oldst newst")
+#   gpfit     tools/bench_rows.py gp_fit rows (N = 64 .. 512, 256 lengthscales per launch)
+#   bo        tools/bo_compare.py, BO_TRIALS (40) trials per case, BO_CASES (default: the asserted
+#             set; a comma list of tools/bo_compare.py SETTINGS keys) -> bo_compare.jsonl
+#   sharded   C3 bench over the multi-rank path at one rank (--sharded: RCCL all-gather, device merge)
+#             beside the plain line, 10 steps each, no CPU baseline
+#   prof      rocprofv3 --kernel-trace --stats of the default bench (1 step) + FETCH_SIZE / WRITE_SIZE
+#             passes (tools/profile.sh), C3 and C3-MLE
+# Outputs under gpurun_out/<tag>/.
+root=${GRAFT_REPO_ROOT:-$PWD}
+tag=$1; shift
+out=$root/gpurun_out/$tag
+mkdir -p "$out"
+cd "$root"
+export MRBO_PARITY_REPORT=$out/parity.json
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+        > "$out/pytest.log" 2>&1
+      rc=$?; tail -5 "$out/pytest.log" ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
+      rc=$?; tail -3 "$out/smoke.log" ;;
+    bench)
+      timeout -k 10 300 python -u bench.py > "$out/bench_c3.json" 2> "$out/bench_c3.err"
+      rc=$?; tail -c 600 "$out/bench_c3.json" ;;
+    rows)
+      timeout -k 10 200 python -u bench.py --mle --no-cpu-baseline > "$out/bench_c3_mle.json" 2> "$out/bench_c3_mle.err" && \
+      timeout -k 10 200 python -u bench.py --config C4 --mc-per-gpu 1024 --steps 3 --warmup 1 --ell 0.5 --no-cpu-baseline \
+        > "$out/bench_c4_l05.json" 2> "$out/bench_c4_l05.err" && \
+      timeout -k 10 200 python -u bench.py --config C4 --mc-per-gpu 1024 --steps 3 --warmup 1 --mle --no-cpu-baseline \
+        > "$out/bench_c4_mle.json" 2> "$out/bench_c4_mle.err" && \
+      timeout -k 10 200 python -u bench.py --config C2 --no-cpu-baseline > "$out/bench_c2.json" 2> "$out/bench_c2.err"
+      rc=$?
+      for f in "$out"/bench_*.json; do
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1].split('/')[-1], d['value'], d['roofline']['frac'], d['roofline']['kernel_ms'], d['work_per_traj'])" "$f"
+      done ;;
+    sharded)
+      timeout -k 10 200 python -u bench.py --sharded --steps 10 --no-cpu-baseline > "$out/bench_c3_sharded.json" 2> "$out/bench_c3_sharded.err" && \
+      timeout -k 10 200 python -u bench.py --steps 10 --no-cpu-baseline > "$out/bench_c3_plain.json" 2> "$out/bench_c3_plain.err"
+      rc=$?
+      for f in "$out"/bench_c3_sharded.json "$out"/bench_c3_plain.json; do
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1].split('/')[-1], d['value'], d['ms_per_step'], d['roofline']['kernel_ms'])" "$f"
+      done ;;
+    prof)
+      bash tools/profile.sh "${tag}_c3" && bash tools/profile.sh "${tag}_c3mle" --steps 1 --warmup 1 --no-cpu-baseline --mle
+      rc=$? ;;
+    ab)
+      AB_TAG="" timeout -k 10 400 bash tools/ab_run.sh ${AB_VARIANTS:-old new oldst newst} > "$out/ab.log" 2>&1
+      rc=$?; cp gpurun_out/ab_*.json gpurun_out/ab_*.err "$out/" 2>/dev/null; grep -v "^\[mrbo stamps\] .* 0.00%" "$out/ab.log" | tail -60 ;;
+    gpfit)
+      timeout -k 10 400 python -u tools/bench_rows.py --rows gp_fit --gpfit-n ${GPFIT_N:-64,128,256,384,512} --cpu-seconds 2 > "$out/gpfit_rows.jsonl" 2> "$out/gpfit_rows.err"
+      rc=$?; python -c "
+import sys, json
+for l in open(sys.argv[1]):
+    if l.startswith('{'):
+        d = json.loads(l); print(d['config']['workload'], round(d['value']), 'fits/s;', round(d['kernel_ms'], 3), 'ms kernel; frac', round(d['roofline']['frac'], 4))" "$out/gpfit_rows.jsonl" ;;
+    bo)
+      timeout -k 10 ${BO_TIMEOUT:-1000} python -u tools/bo_compare.py --trials ${BO_TRIALS:-40} --cases ${BO_CASES:-asserted} ${BO_ARGS:-} \
+        --out "$out/bo_compare.jsonl" > /dev/null 2> "$out/bo_compare.err"
+      rc=$?; grep "final gap" "$out/bo_compare.err" ;;
+    *) echo "unknown step $step"; rc=2 ;;
+  esac
+  echo "== $step rc=$rc $(date +%T)"
+  [ $rc -ne 0 ] && exit $rc
+done
+exit 0
