@@ -63,7 +63,7 @@ struct mrbo_plan {
   double* dkxb = nullptr;   // batched starts, packed layouts: global start tables (start_tables_kernel)
   double* dgtab = nullptr;
   long long work_stride = 0;
-  int* dqueue = nullptr;
+  int* dqueue = nullptr;    // work-queue heads: one per XCD, 64 B apart (rollout_kernel)
   const int32_t* order = nullptr;   // mrbo_plan_set_order: caller-owned device permutation of M×R
   int wpg = 4, blocks = 0;
   size_t smem = 0;
@@ -691,7 +691,7 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
             (!P->batch || ks.square ||
              (hipMalloc(&P->dkxb, sizeof(double) * (size_t)P->NR * ns) == hipSuccess &&
               hipMalloc(&P->dgtab, sizeof(double) * (size_t)ns * ng) == hipSuccess)) &&
-            hipMalloc(&P->dqueue, sizeof(int) * 4) == hipSuccess &&
+            hipMalloc(&P->dqueue, sizeof(int) * MRBO_QUEUE_INTS) == hipSuccess &&
             (P->p.cost == MRBO_COST_NONE || hipMalloc(&P->dcost, sizeof(double) * 3 * d) == hipSuccess);
   if (ok && P->p.cost != MRBO_COST_NONE) {
     std::vector<double> tab(3 * (size_t)d);
@@ -772,7 +772,7 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
   kp.values = dvalues; kp.grad_x = with_grad ? dgx : nullptr; kp.grad_theta = with_grad ? dgt : nullptr;
   kp.status = (int*)dstatus; kp.policy = dpol; kp.obs = dobs; kp.evals = (long long*)devals;
   kp.order = P->order;
-  HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * 4, st));
+  HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * MRBO_QUEUE_INTS, st));
 #ifdef MRBO_STAMPS
   static unsigned long long* dstamps = nullptr;
   if (!dstamps) HIP_TRY(hipMalloc(&dstamps, sizeof(unsigned long long) * NSTAMP_SLOTS));
@@ -932,7 +932,7 @@ int mrbo_eval_base(mrbo_plan_t* P, int32_t npts, const double* xs, double* out, 
   }
   kp.pts = dxs;
   kp.pts_out = dout;
-  HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * 4, st));
+  HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * MRBO_QUEUE_INTS, st));
   launch_evalb(d, P->RPL, P->fx, dim3(P->eblocks), dim3(P->ewpg * WAVE), P->esmem, st, kp);
   HIP_TRY(hipGetLastError());
   if (flags & MRBO_FLAG_HOST_POINTERS) {
@@ -976,7 +976,7 @@ int mrbo_base_solve(mrbo_plan_t* P, int32_t n, const double* xstarts, double* xm
   kp.values = df;
   kp.status = (int*)dst;
   kp.evals = (long long*)dev;
-  HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * 4, st));
+  HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * MRBO_QUEUE_INTS, st));
   const int blocks = std::min(P->blocks, (n + P->wpg - 1) / P->wpg);
   launch_rollout(d, P->RPL, P->fx, P->spec, dim3(blocks), dim3(P->wpg * WAVE), P->smem, st, kp);
   HIP_TRY(hipGetLastError());

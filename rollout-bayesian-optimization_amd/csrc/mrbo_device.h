@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#define MRBO_QUEUE_INTS (8 * 16)   // eight work-queue heads, one 64-B line each
+
 namespace mrbo {
 
 // work counters per trajectory (for the algorithmic-FLOP roofline):
@@ -82,7 +84,7 @@ struct KParams {
   double* gtab_g;       //   [nstarts][NG] written by start_tables_kernel before the rollout launch
   const double* ghq_nodes;  // Gauss–Hermite estimator: M×(h+1) nodes and weights per sample (else null)
   const double* ghq_w;
-  int* queue;           // work-queue head (zeroed before every launch)
+  int* queue;           // work-queue heads, one per XCD at queue[16·x] (zeroed before every launch)
   const int* order;     // optional: queue position -> trajectory (mrbo_plan_set_order), else identity
   long long T;          // trajectories (or points for eval_base)
   const double* pts;    // eval_base: d×P
@@ -160,6 +162,23 @@ __device__ __forceinline__ void row_blocks(double v, double& blk_p, double& blk_
   blk_p2 = djoin(c[1], d[1]);
 }
 
+// All four blocks at once: one v_permlane16_swap and two v_permlane32_swap per dword (blocks 0, 2
+// from the first pl16 half, 1, 3 from the second) instead of a pl16 + pl32 pair per block pair.
+__device__ __forceinline__ void row_blocks4(double v, double& b0, double& b1, double& b2, double& b3) {
+  int lo, hi;
+  dsplit(v, lo, hi);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // [r0 r0 r2 r2], [r1 r1 r3 r3]
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const auto c0 = __builtin_amdgcn_permlane32_swap(a[0], a[0], false, false);   // [r0 ×4], [r2 ×4]
+  const auto d0 = __builtin_amdgcn_permlane32_swap(b[0], b[0], false, false);
+  const auto c1 = __builtin_amdgcn_permlane32_swap(a[1], a[1], false, false);   // [r1 ×4], [r3 ×4]
+  const auto d1 = __builtin_amdgcn_permlane32_swap(b[1], b[1], false, false);
+  b0 = djoin(c0[0], d0[0]);
+  b2 = djoin(c0[1], d0[1]);
+  b1 = djoin(c1[0], d1[0]);
+  b3 = djoin(c1[1], d1[1]);
+}
+
 // The value of lane (l & 31) + 32·H in every lane l: one v_permlane32_swap per dword of the
 // register with itself leaves the lower half's values in both halves of the first result and the
 // upper half's in both halves of the second (H a compile-time constant after unrolling).
@@ -229,7 +248,13 @@ __device__ __forceinline__ void wave_reduce(double (&v)[K], double* red, int lan
   if constexpr (S < 4) v[0] = fold_all<4>(v[0]);
   if constexpr (S < 5) v[0] = fold_all<2>(v[0]);
   v[0] = fold_all<1>(v[0]);
+#ifndef MRBO_REDUCE_LEADER_STORE
+  // every lane of a group holds the same bits and the same idx: an unconditional store keeps the
+  // reductions of one phase in one scheduling region (no exec-mask branch between them; C3 −0.3 %)
+  red[idx] = v[0];
+#else
   if ((lane & ((64 >> S) - 1)) == 0) red[idx] = v[0];
+#endif
 }
 
 // Sum over the 64 lanes in EVERY lane, no LDS round trip: the butterfly of wave_reduce<1>
@@ -286,12 +311,15 @@ __device__ __forceinline__ double fexp(double x) {
   return e;
 }
 
-// Default: leaf calls.  MRBO_FEXP inlines fexp instead (A/B on C3: no gain -- the calls' latency
-// is hidden by the second wave, and inlining raised VGPR spills 66 → 93).
+// Default (round 5): fexp inlined at every use, the paired xexp2 too.  Round 1 measured no gain from
+// inlining (the calls' latency hidden by the second wave, VGPR spills 66 → 93); on the round-5
+// kernel a leaf call costs ≈ 15 v_readlane reloads of spilled SGPRs before every s_swappc, and
+// inlining runs C3 1.2 % faster with the spill count unchanged (6 VGPRs).  MRBO_LEAF_EXP: the
+// round-4 leaf calls (A/B).
 #ifdef MRBO_INLINE_TRANSCENDENTALS
 __device__ __forceinline__ double xexp(double x) { return exp(x); }
 __device__ __forceinline__ double xerfc(double x) { return erfc(x); }
-#elif defined(MRBO_FEXP)
+#elif !defined(MRBO_LEAF_EXP)
 __device__ __forceinline__ double xexp(double x) { return fexp(x); }
 __device__ __attribute__((noinline)) double xerfc(double x) { return erfc(x); }
 #else
@@ -403,7 +431,11 @@ __device__ __forceinline__ void rad_eval(const Radial& k, double rho2, double& p
 struct Exp2 {
   double a, b;
 };
+#ifndef MRBO_LEAF_EXP
+__device__ __forceinline__ Exp2 xexp2(double a, double b) {
+#else
 __device__ __attribute__((noinline)) Exp2 xexp2(double a, double b) {
+#endif
   Exp2 r;
   r.a = fexp(a);
   r.b = fexp(b);
@@ -448,33 +480,80 @@ __device__ __forceinline__ PhiPair ei_phi_Phi(double z) {
   r = fma(r, fma(-ab, r, 1.0), r);
   r = fma(r, fma(-ab, r, 1.0), r);
   const double t = (u - 3.5) * b * r, t2 = t * t;
-  // even / odd halves of P(t) = Pe(t²) + t·Po(t²): two independent Horner chains
-  double pe = sconst<0xf1ab7ccbu, 0x3dd09a8bu>();
-  asm volatile("" : "+v"(pe));
-  pe = fma(t2, pe, sconst<0x73fda30du, 0x3e06db11u>());
-  pe = fma(t2, pe, sconst<0xf4266242u, 0xbe427e42u>());
-  pe = fma(t2, pe, sconst<0x1ed381c5u, 0xbe672292u>());
-  pe = fma(t2, pe, sconst<0xb901a919u, 0x3ec385e7u>());
-  pe = fma(t2, pe, sconst<0x645605dcu, 0xbf066e11u>());
-  pe = fma(t2, pe, sconst<0xfbfa9e67u, 0x3f427e65u>());
-  pe = fma(t2, pe, sconst<0xc891e642u, 0xbf7143c4u>());
-  pe = fma(t2, pe, sconst<0xf77381b3u, 0xbfa8ff5eu>());
-  pe = fma(t2, pe, sconst<0x0c35056au, 0xbfbd7683u>());
-  pe = fma(t2, pe, sconst<0x284b1971u, 0xbf859e2cu>());
-  pe = fma(t2, pe, sconst<0x9a0ee914u, 0x3ff3e0a9u>());
-  double po = sconst<0x617fb329u, 0xbe1406aau>();
-  asm volatile("" : "+v"(po));
-  po = fma(t2, po, sconst<0xdb5ecc9au, 0x3e4d421du>());
-  po = fma(t2, po, sconst<0x3786431fu, 0xbe79e096u>());
-  po = fma(t2, po, sconst<0xc09ddffau, 0x3ea42eb1u>());
-  po = fma(t2, po, sconst<0x97b263b0u, 0xbecffe87u>());
-  po = fma(t2, po, sconst<0x306b92a0u, 0x3ef97053u>());
-  po = fma(t2, po, sconst<0x5777da87u, 0xbf1fda8au>());
-  po = fma(t2, po, sconst<0xf98105c2u, 0xbf33cf36u>());
-  po = fma(t2, po, sconst<0x67477473u, 0x3f938ec6u>());
-  po = fma(t2, po, sconst<0x6045eed1u, 0x3fb68610u>());
-  po = fma(t2, po, sconst<0xec6b3bb9u, 0x3fb8f702u>());
-  po = fma(t2, po, sconst<0x20ea5946u, 0xbfc1ebd2u>());
+  // even / odd halves of P(t) = Pe(t²) + t·Po(t²), each split once more (Estrin):
+  // Pe = Pe_lo(t²) + t¹²·Pe_hi(t²), six-term Horner chains that run side by side (dependent depth
+  // 6 instead of 11; MRBO_NO_ESTRIN: the two plain Horner chains)
+#ifndef MRBO_NO_ESTRIN
+  const double u2 = t2 * t2, u3 = u2 * t2, u6 = u3 * u3;   // u = t²: u⁶ = t¹²
+  double pe, po;
+  {
+    double pe_h = sconst<0xf1ab7ccbu, 0x3dd09a8bu>();
+    asm volatile("" : "+v"(pe_h));
+    pe_h = fma(t2, pe_h, sconst<0x73fda30du, 0x3e06db11u>());
+    pe_h = fma(t2, pe_h, sconst<0xf4266242u, 0xbe427e42u>());
+    pe_h = fma(t2, pe_h, sconst<0x1ed381c5u, 0xbe672292u>());
+    pe_h = fma(t2, pe_h, sconst<0xb901a919u, 0x3ec385e7u>());
+    pe_h = fma(t2, pe_h, sconst<0x645605dcu, 0xbf066e11u>());
+    double pe_l = sconst<0xfbfa9e67u, 0x3f427e65u>();
+    asm volatile("" : "+v"(pe_l));
+    pe_l = fma(t2, pe_l, sconst<0xc891e642u, 0xbf7143c4u>());
+    pe_l = fma(t2, pe_l, sconst<0xf77381b3u, 0xbfa8ff5eu>());
+    pe_l = fma(t2, pe_l, sconst<0x0c35056au, 0xbfbd7683u>());
+    pe_l = fma(t2, pe_l, sconst<0x284b1971u, 0xbf859e2cu>());
+    pe_l = fma(t2, pe_l, sconst<0x9a0ee914u, 0x3ff3e0a9u>());
+    const double pe_ = fma(u6, pe_h, pe_l);
+    pe = pe_;
+    double po_h = sconst<0x617fb329u, 0xbe1406aau>();
+    asm volatile("" : "+v"(po_h));
+    po_h = fma(t2, po_h, sconst<0xdb5ecc9au, 0x3e4d421du>());
+    po_h = fma(t2, po_h, sconst<0x3786431fu, 0xbe79e096u>());
+    po_h = fma(t2, po_h, sconst<0xc09ddffau, 0x3ea42eb1u>());
+    po_h = fma(t2, po_h, sconst<0x97b263b0u, 0xbecffe87u>());
+    po_h = fma(t2, po_h, sconst<0x306b92a0u, 0x3ef97053u>());
+    double po_l = sconst<0x5777da87u, 0xbf1fda8au>();
+    asm volatile("" : "+v"(po_l));
+    po_l = fma(t2, po_l, sconst<0xf98105c2u, 0xbf33cf36u>());
+    po_l = fma(t2, po_l, sconst<0x67477473u, 0x3f938ec6u>());
+    po_l = fma(t2, po_l, sconst<0x6045eed1u, 0x3fb68610u>());
+    po_l = fma(t2, po_l, sconst<0xec6b3bb9u, 0x3fb8f702u>());
+    po_l = fma(t2, po_l, sconst<0x20ea5946u, 0xbfc1ebd2u>());
+    const double po_ = fma(u6, po_h, po_l);
+    po = po_;
+  }
+#else
+  double pe, po;
+  {
+    double pe_ = sconst<0xf1ab7ccbu, 0x3dd09a8bu>();
+    asm volatile("" : "+v"(pe_));
+    pe_ = fma(t2, pe_, sconst<0x73fda30du, 0x3e06db11u>());
+    pe_ = fma(t2, pe_, sconst<0xf4266242u, 0xbe427e42u>());
+    pe_ = fma(t2, pe_, sconst<0x1ed381c5u, 0xbe672292u>());
+    pe_ = fma(t2, pe_, sconst<0xb901a919u, 0x3ec385e7u>());
+    pe_ = fma(t2, pe_, sconst<0x645605dcu, 0xbf066e11u>());
+    pe_ = fma(t2, pe_, sconst<0xfbfa9e67u, 0x3f427e65u>());
+    pe_ = fma(t2, pe_, sconst<0xc891e642u, 0xbf7143c4u>());
+    pe_ = fma(t2, pe_, sconst<0xf77381b3u, 0xbfa8ff5eu>());
+    pe_ = fma(t2, pe_, sconst<0x0c35056au, 0xbfbd7683u>());
+    pe_ = fma(t2, pe_, sconst<0x284b1971u, 0xbf859e2cu>());
+    pe_ = fma(t2, pe_, sconst<0x9a0ee914u, 0x3ff3e0a9u>());
+    pe = pe_;
+    double po_ = sconst<0x617fb329u, 0xbe1406aau>();
+    asm volatile("" : "+v"(po_));
+    po_ = fma(t2, po_, sconst<0xdb5ecc9au, 0x3e4d421du>());
+    po_ = fma(t2, po_, sconst<0x3786431fu, 0xbe79e096u>());
+    po_ = fma(t2, po_, sconst<0xc09ddffau, 0x3ea42eb1u>());
+    po_ = fma(t2, po_, sconst<0x97b263b0u, 0xbecffe87u>());
+    po_ = fma(t2, po_, sconst<0x306b92a0u, 0x3ef97053u>());
+    po_ = fma(t2, po_, sconst<0x5777da87u, 0xbf1fda8au>());
+    po_ = fma(t2, po_, sconst<0xf98105c2u, 0xbf33cf36u>());
+    po_ = fma(t2, po_, sconst<0x67477473u, 0x3f938ec6u>());
+    po_ = fma(t2, po_, sconst<0x6045eed1u, 0x3fb68610u>());
+    po_ = fma(t2, po_, sconst<0xec6b3bb9u, 0x3fb8f702u>());
+    po_ = fma(t2, po_, sconst<0x20ea5946u, 0xbfc1ebd2u>());
+    po = po_;
+  }
+#endif
+
   const double P = fma(t, po, pe);
   const double q = 0.5 * E * (P * (a * r));   // ½·E·erfcx(u)
   PhiPair o;

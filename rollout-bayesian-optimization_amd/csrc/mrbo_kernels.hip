@@ -22,11 +22,14 @@
 
 namespace mrbo {
 
-// MRBO_AB_MIN (A/B variant builds of one configuration only, tools/build_variants.sh): the unit holds
-// RPL = 1 and the specialised kernel alone (it also stands in for the generic one), so a variant of
+// MRBO_AB_MIN (A/B variant builds of one configuration only, tools/ab_variant.py): the unit holds
+// RPL = MRBO_AB_RPL (default 1) and the specialised kernel alone (it also stands in for the generic one), so a variant of
 // the N ≤ 64 kernel compiles in seconds instead of minutes; plans of other shapes fail to create.
 #ifdef MRBO_AB_MIN
-constexpr bool has_rpl(int d, int rpl) { return rpl == 1; }
+#ifndef MRBO_AB_RPL
+#define MRBO_AB_RPL 1
+#endif
+constexpr bool has_rpl(int d, int rpl) { return rpl == MRBO_AB_RPL; }
 #else
 constexpr bool has_rpl(int d, int rpl) { return rpl == 1 || rpl == 2 || (d <= 8 && (rpl == 4 || rpl == 8)); }
 #endif
@@ -36,7 +39,11 @@ template <int D, int RPL>
 static KernelSet kset() {
   using Ly = Lay<D, RPL>;
   const void* spec = nullptr;
+#if defined(MRBO_AB_MIN) && defined(MRBO_AB_GENERIC)   // the generic kernel alone (cost, other rules)
+  spec = (const void*)&rollout_kernel<D, RPL, 0>;
+#else
   if constexpr (has_spec(D, RPL)) spec = (const void*)&rollout_kernel<D, RPL, 1>;
+#endif
 #ifdef MRBO_AB_MIN
   return KernelSet{spec, spec, (const void*)&eval_base_kernel<D, RPL>,
 #else
@@ -48,8 +55,8 @@ static KernelSet kset() {
 
 bool MRBO_SFX(kset_d)(int rpl, KernelSet& ks) {
 #ifdef MRBO_AB_MIN
-  if (rpl != 1) return false;
-  ks = kset<MRBO_D, 1>();
+  if (rpl != MRBO_AB_RPL) return false;
+  ks = kset<MRBO_D, MRBO_AB_RPL>();
   return true;
 #else
   if (rpl == 1) ks = kset<MRBO_D, 1>();
@@ -65,7 +72,10 @@ bool MRBO_SFX(kset_d)(int rpl, KernelSet& ks) {
 
 template <int RPL, int SPEC>
 static void launch_one(dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
-#ifdef MRBO_AB_MIN
+#if defined(MRBO_AB_MIN) && defined(MRBO_AB_GENERIC)
+  if constexpr (has_rpl(MRBO_D, RPL))
+    hipLaunchKernelGGL((rollout_kernel<MRBO_D, RPL, 0>), g, b, sm, st, kp);
+#elif defined(MRBO_AB_MIN)
   if constexpr (has_rpl(MRBO_D, RPL) && has_spec(MRBO_D, RPL))
     hipLaunchKernelGGL((rollout_kernel<MRBO_D, RPL, 1>), g, b, sm, st, kp);
 #else

@@ -18,6 +18,9 @@
 #ifndef MRBO_WAVES_PER_SIMD
 #define MRBO_WAVES_PER_SIMD 2
 #endif
+#ifndef MRBO_HESS16   // 1: the Hessian reduction's tail chunk as a 16-value reduction (A/B)
+#define MRBO_HESS16 0
+#endif
 // Everything below is compiled per fantasy capacity FMAX (-DMRBO_FMAX, default 6 = h ≤ 5; the
 // kernel units are also built with FMAX = 4 for h ≤ 3): an inline namespace per FMAX keeps the
 // two builds' kernels and helpers distinct symbols in one library.
@@ -30,6 +33,8 @@
 
 namespace mrbo {
 inline namespace MRBO_FNS {
+
+constexpr double PAD_FAR = 1e100;   // coordinate of padded data rows (WaveCtx::rowv)
 
 template <int D, int RPL>
 struct Lay {
@@ -183,6 +188,17 @@ struct WaveCtx {
   int N, Npad;
   Radial rad;
   unsigned long long tlast;
+  // Does row slot s hold a data point?  Padded rows (i ≥ N) sit at X0 = PAD_FAR (wave_setup), where
+  // every non-periodic radial function and both derivative factors are exactly 0 (exp underflows),
+  // and their c, w, E, P entries are 0 as well -- so for those kernels no select is needed: true at
+  // compile time in the Matérn-5/2 specialisation.  The Periodic kernel keeps the per-row mask.
+  __device__ __forceinline__ bool rowv(const KParams& kp, int s) const {
+#ifdef MRBO_NO_PAD_FAR
+    return valid[s];
+#else
+    return kp.kernel != KERNEL_PERIODIC ? true : valid[s];
+#endif
+  }
   // opaque lane index (see evaluate): per-lane addresses are rematerialised where used
   __device__ __forceinline__ int ln() const {
     int l = lane;
@@ -256,6 +272,20 @@ __device__ __forceinline__ const double (&tail8(const double (&a)[K]))[K - 8] {
   return *reinterpret_cast<const double(*)[K - 8]>(&a[8]);
 }
 
+// One 16-step block of a register-broadcast product.  MRBO_K1_SPLIT: K = 1 (the value product
+// L0⁻¹kx and the backward w = L0⁻ᵀY0) with two accumulators over the even and odd steps -- measured
+// 0.6 % SLOWER on C3 (round 5: the chain is not what the product waits on), so off by default.
+template <int K, int STRIDE>
+__device__ __forceinline__ void bcast_run(double (&acc)[K], const double (&bq)[K], unsigned addr) {
+#ifdef MRBO_K1_SPLIT
+  if constexpr (K == 1) {
+    BcastAsmSplit<STRIDE>::run(acc, bq, addr);
+    return;
+  }
+#endif
+  BcastAsm<K, STRIDE>::run(acc, bq, addr);
+}
+
 template <int K, int JSTRIDE>
 __device__ __forceinline__ void bcast_product_k(double (&acc)[K], const double (&v)[K], const double* lbase, int nrows) {
   const unsigned a0 = lds_addr(lbase);
@@ -268,8 +298,8 @@ __device__ __forceinline__ void bcast_product_k(double (&acc)[K], const double (
       if (p == 0) row_blocks<0>(v[c], bp[c], bp2[c]);
       else row_blocks<1>(v[c], bp[c], bp2[c]);
     }
-    BcastAsm<K, 8 * JSTRIDE>::run(acc, bp, a0 + 8u * 16u * p * JSTRIDE);
-    if (16 * (p + 2) < nrows) BcastAsm<K, 8 * JSTRIDE>::run(acc, bp2, a0 + 8u * 16u * (p + 2) * JSTRIDE);
+    bcast_run<K, 8 * JSTRIDE>(acc, bp, a0 + 8u * 16u * p * JSTRIDE);
+    if (16 * (p + 2) < nrows) bcast_run<K, 8 * JSTRIDE>(acc, bp2, a0 + 8u * 16u * (p + 2) * JSTRIDE);
   }
 }
 
@@ -282,6 +312,173 @@ __device__ __forceinline__ void bcast_product(double (&acc)[K], const double (&v
     bcast_product_k<K, JSTRIDE>(acc, v, lbase, nrows);
   }
 }
+
+// ---- folded triangular products (RPL = 1, N > 48) ------------------------------------------
+// L0⁻¹ is lower triangular, so DPP row q (lanes 16q..16q+15, output rows 16q..16q+15) needs only
+// the row blocks b ≤ q of the forward product and b ≥ q of the backward one: 10 of the 16
+// (row, block) pairs the four unfolded 16-step passes issue.  Three passes cover them: two plain
+// passes (forward blocks 0, 1; backward blocks 3, 2), then one pass in which a row that is already
+// finished works for another -- forward: row 1 takes block 3 of output rows 48.. (row 3's last
+// block), rows 2, 3 their block 2; backward: row 2 takes block 0 of output rows 0.. (row 0's last
+// block), rows 0, 1 their block 1 -- into a second accumulator f.  v_permlane32_swap then moves
+// the helper's partial sums by 32 lanes (row 1 ↔ row 3, row 2 ↔ row 0) beside the rows' own, and
+// two adds finish: 48 steps instead of 64.  The lanes of the idle row read one zero of the upper
+// triangle (a broadcast address on the bank half the helper row does not use), so their f is 0
+// and every read of the third pass is conflict-free.  The caller passes the LD = 65 square block.
+template <int K>
+__device__ __forceinline__ void fold_finish(double (&acc)[K], const double (&f)[K], bool fwd) {
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    int lo, hi;
+    dsplit(f[c], lo, hi);
+    // forward: swap(vdst = 0, f) -> [0 0 f0 f1] and [0 0 f2 f3] (f0 = 0);
+    // backward: swap(vdst = f, 0) -> [f0 f1 0 0] and [f2 f3 0 0] (f3 = 0)
+    const auto l = fwd ? __builtin_amdgcn_permlane32_swap(0, lo, false, false)
+                       : __builtin_amdgcn_permlane32_swap(lo, 0, false, false);
+    const auto h = fwd ? __builtin_amdgcn_permlane32_swap(0, hi, false, false)
+                       : __builtin_amdgcn_permlane32_swap(hi, 0, false, false);
+    acc[c] += djoin(l[0], h[0]);
+    acc[c] += djoin(l[1], h[1]);
+  }
+}
+
+// forward: acc[c] += Σ_{j ≤ i} L(i, j) v[c](j), L(i, j) at Lsq[j·65 + i]
+template <int K>
+__device__ __forceinline__ void bcast_fold_fwd_k(double (&acc)[K], const double (&v)[K], const double* Lsq, int lane) {
+  constexpr unsigned LD = WAVE + 1;
+  const unsigned a0 = lds_addr(Lsq + lane);
+  double b0[K], b1[K], b2[K], b3[K];
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+#ifdef MRBO_ROWBLOCKS2
+    row_blocks<0>(v[c], b0[c], b2[c]);
+    row_blocks<1>(v[c], b1[c], b3[c]);
+#else
+    row_blocks4(v[c], b0[c], b1[c], b2[c], b3[c]);
+#endif
+  }
+  const int q = lane >> 4;
+  double m[K], f[K];
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    m[c] = (q == 1) ? b3[c] : b2[c];
+    f[c] = 0.0;
+  }
+  // row 1: (48 + t, 48 + n) = own address + 32 + 16·LD; row 0: the zeros (15, 33 + n); rows 2, 3: block 2
+  const unsigned a3 = (q == 1) ? a0 + 8u * (48u * LD + 32u) : (q == 0) ? lds_addr(Lsq + 33 * LD + 15) : a0 + 8u * 32u * LD;
+#ifdef MRBO_FOLD3_MERGED   // A/B: +1.2 % on C3 (round 5), so off
+  if constexpr (K == 1) {   // the three passes in one software-pipelined statement
+    BcastAsm3<8 * LD>::run(acc, f, b0, b1, m, a0, a3);
+  } else
+#endif
+  {
+    bcast_run<K, 8 * LD>(acc, b0, a0);
+    bcast_run<K, 8 * LD>(acc, b1, a0 + 8u * 16u * LD);
+    bcast_run<K, 8 * LD>(f, m, a3);
+  }
+  fold_finish<K>(acc, f, true);
+}
+
+// backward: acc[c] += Σ_{k ≥ i} L(k, i) v[c](k), L(k, i) at Lsq[i·65 + k]
+template <int K>
+__device__ __forceinline__ void bcast_fold_bwd_k(double (&acc)[K], const double (&v)[K], const double* Lsq, int lane) {
+  constexpr unsigned LD = WAVE + 1;
+  const unsigned a0 = lds_addr(Lsq + lane * LD);
+  double b0[K], b1[K], b2[K], b3[K];
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+#ifdef MRBO_ROWBLOCKS2
+    row_blocks<0>(v[c], b0[c], b2[c]);
+    row_blocks<1>(v[c], b1[c], b3[c]);
+#else
+    row_blocks4(v[c], b0[c], b1[c], b2[c], b3[c]);
+#endif
+  }
+  const int q = lane >> 4;
+  double m[K], f[K];
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    m[c] = (q == 2) ? b0[c] : b1[c];
+    f[c] = 0.0;
+  }
+  // row 2: (n, t) of output row t = lane − 32; row 3: the zeros (17 + n, 63); rows 0, 1: block 1
+  const unsigned a3 = (q == 2) ? lds_addr(Lsq + (lane - 32) * LD) : (q == 3) ? lds_addr(Lsq + 63 * LD + 17) : a0 + 8u * 16u;
+#ifdef MRBO_FOLD3_MERGED
+  if constexpr (K == 1) {   // blocks 2 then 3 (at +16 steps), then the folded pass, in one statement
+    BcastAsm3<8>::run(acc, f, b2, b3, m, a0 + 8u * 32u, a3);
+  } else
+#endif
+  {
+    bcast_run<K, 8>(acc, b3, a0 + 8u * 48u);
+    bcast_run<K, 8>(acc, b2, a0 + 8u * 32u);
+    bcast_run<K, 8>(f, m, a3);
+  }
+  fold_finish<K>(acc, f, false);
+}
+
+// column chunks of at most 8 beyond K = 9 (the generated asm statements), as bcast_product
+template <int K>
+__device__ __forceinline__ void bcast_fold_fwd(double (&acc)[K], const double (&v)[K], const double* Lsq, int lane) {
+  if constexpr (K > 9) {
+    bcast_fold_fwd<8>(head8(acc), head8(v), Lsq, lane);
+    bcast_fold_fwd<K - 8>(tail8(acc), tail8(v), Lsq, lane);
+  } else {
+    bcast_fold_fwd_k<K>(acc, v, Lsq, lane);
+  }
+}
+template <int K>
+__device__ __forceinline__ void bcast_fold_bwd(double (&acc)[K], const double (&v)[K], const double* Lsq, int lane) {
+  if constexpr (K > 9) {
+    bcast_fold_bwd<8>(head8(acc), head8(v), Lsq, lane);
+    bcast_fold_bwd<K - 8>(tail8(acc), tail8(v), Lsq, lane);
+  } else {
+    bcast_fold_bwd_k<K>(acc, v, Lsq, lane);
+  }
+}
+
+// Sum n per-lane values fill(t), t < n (n runtime, wave-uniform), over the 64 lanes into red[t]:
+// chunks of 16, the last one in the smallest power of two that holds it -- a wave_reduce<K> costs
+// ≈ K + log2(64/K) exchanges, so a chunk of 6 values in wave_reduce<8> saves ≈ 30 VALU against
+// wave_reduce<16> (the Hessian's tail chunk: C3 −1 %).  Slots t ≥ n of a chunk hold junk.  t is a
+// compile-time constant in every call of fill.  MRBO_REDUCE16: every chunk of 16 (A/B).
+template <int CH, class F>
+__device__ __forceinline__ void wave_reduce_n(F&& fill, int n, double* red, int lane) {
+#pragma unroll
+  for (int ch = 0; ch < CH; ++ch) {
+    const int rem = n - 16 * ch;
+    if (rem <= 0) break;
+#ifndef MRBO_REDUCE16
+    if (rem <= 2) {
+      double v[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) v[q] = fill(16 * ch + q);
+      wave_reduce<2>(v, red + 16 * ch, lane);
+    } else if (rem <= 4) {
+      double v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = fill(16 * ch + q);
+      wave_reduce<4>(v, red + 16 * ch, lane);
+    } else if (rem <= 8) {
+      double v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = fill(16 * ch + q);
+      wave_reduce<8>(v, red + 16 * ch, lane);
+    } else
+#endif
+    {
+      double v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = fill(16 * ch + q);
+      wave_reduce<16>(v, red + 16 * ch, lane);
+    }
+  }
+}
+
+#ifdef MRBO_NO_FOLD
+constexpr bool FOLD = false;
+#else
+constexpr bool FOLD = true;
+#endif
 
 // The same product with this lane's L entries from global memory (L2-resident image):
 // step n of the block at lb[n·64].  All 64 steps of both row blocks of a pass are loaded into
@@ -384,7 +581,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
     for (int a = 0; a < D; ++a) { r[a] = x[a] - W.X0[s][a]; rho2 = fma(r[a], r[a], rho2); }
     if (rows_kept) {
       const double g1 = W.G12[3 * (lane + WAVE * s)];
-      const bool v = W.valid[s];
+      const bool v = W.rowv(kp, s);
       Bown[s][0] = 0.0;   // column 0 comes from the VALUE pass
 #pragma unroll
       for (int a = 0; a < D; ++a) Bown[s][1 + a] = v ? g1 * r[a] : 0.0;
@@ -402,7 +599,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
     } else
 #endif
     rad_eval(W.rad, rho2, psi, g1, g2);
-    const bool v = W.valid[s];
+    const bool v = W.rowv(kp, s);
     Bown[s][0] = v ? psi : 0.0;
 #pragma unroll
     for (int a = 0; a < D; ++a) Bown[s][1 + a] = v ? g1 * r[a] : 0.0;
@@ -450,6 +647,8 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
     // lane i reads L0⁻¹[64s+i][64t+j] at blk(s,t)·BLK + j·LD + i; rows j of block column t are
     // broadcast from register slot t.  Row slot s sums block columns t = 0..s in order.
     auto nrows = [&](int t) { const int n = N - WAVE * t; return n < WAVE ? n : WAVE; };
+    // RPL = 1 with N > 48: the folded three-pass products (bcast_fold_fwd / _bwd)
+    const bool fold = FOLD && Ly::SQ && N > 48;
     if (mode == EV_VALUE) {
 #pragma unroll
       for (int s = 0; s < RPL; ++s) {
@@ -457,7 +656,8 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
 #pragma unroll
         for (int t = 0; t <= s; ++t) {
           const double v1[1] = {Bown[t][0]};
-          bcast_product<1, Ly::LD>(a1, v1, W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
+          if (fold) bcast_fold_fwd<1>(a1, v1, W.Linv, lane);
+          else bcast_product<1, Ly::LD>(a1, v1, W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
         }
         acc[s][0] = a1[0];
       }
@@ -474,7 +674,8 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
           double vg[D];
 #pragma unroll
           for (int a = 0; a < D; ++a) vg[a] = Bown[t][1 + a];
-          bcast_product<D, Ly::LD>(ag, vg, W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
+          if (fold) bcast_fold_fwd<D>(ag, vg, W.Linv, lane);
+          else bcast_product<D, Ly::LD>(ag, vg, W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
         }
 #pragma unroll
         for (int a = 0; a < D; ++a) acc[s][1 + a] = ag[a];
@@ -484,8 +685,10 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
 #pragma unroll
       for (int s = 0; s < RPL; ++s)
 #pragma unroll
-        for (int t = 0; t <= s; ++t)
-          bcast_product<D1, Ly::LD>(acc[s], Bown[t], W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
+        for (int t = 0; t <= s; ++t) {
+          if (fold) bcast_fold_fwd<D1>(acc[s], Bown[t], W.Linv, lane);
+          else bcast_product<D1, Ly::LD>(acc[s], Bown[t], W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
+        }
     }
   } else {
     // GL (N ≤ 256): the same register broadcast with L0⁻¹ from L2: lane i reads (i, j) of block
@@ -535,19 +738,18 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
   }
   STAMP(W, 1);
   // ---- 3. per-lane products and wave reductions
-  if (do_val) {
-    double v[8];
+  if (do_val) {   // [|v|² = kx'K⁻¹kx, μ = kx·c (base parts), E_r·kx (r < nf)]: 2 + nf values
+    static_assert(2 + FMAX <= 8, "value reduction: one chunk");
+    wave_reduce_n<1>([&](int t) {
+      double s_ = 0.0;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = 0.0;
-#pragma unroll
-    for (int s = 0; s < RPL; ++s) {
-      v[0] = fma(acc[s][0], acc[s][0], v[0]);      // |v|² = kx'K⁻¹kx (base part)
-      v[1] = fma(lr.cb[s], Bown[s][0], v[1]);       // μ = kx·c (base part)
-#pragma unroll
-      for (int r = 0; r < FMAX; ++r)
-        if (r < nf) v[2 + r] = fma(Ev[s][r], Bown[s][0], v[2 + r]);
-    }
-    wave_reduce<8>(v, red + Ly::R_VAL, lane);
+      for (int s = 0; s < RPL; ++s) {
+        if (t == 0) s_ = fma(acc[s][0], acc[s][0], s_);
+        else if (t == 1) s_ = fma(lr.cb[s], Bown[s][0], s_);
+        else if (t - 2 < FMAX) s_ = fma(Ev[s][t - 2], Bown[s][0], s_);
+      }
+      return s_;
+    }, 2 + nf, red + Ly::R_VAL, lane);
   }
   if (all_cols) {
     // Gram entries (a ≤ b) except (0,0); GSTART takes them from the start tables
@@ -573,28 +775,21 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
       wave_reduce<16>(v, red + Ly::R_G + 16 * ch, lane);
     }
     // ∇μ and fantasy cross products for the gradient columns
+    // (fantasy rows ≥ nf carry nothing: D·(1 + nf) values)
+    wave_reduce_n<Ly::NMFC>([&](int t) {
+      double s_ = 0.0;
+      if (t < Ly::NMF) {
+        const int grp = t / D, a = t % D;  // grp 0: c ; grp r+1: E_r
+        if (grp == 0) {
 #pragma unroll
-    for (int ch = 0; ch < Ly::NMFC; ++ch) {
-      if (16 * ch >= D * (1 + nf)) break;   // fantasy rows ≥ nf carry nothing
-      double v[16];
+          for (int s = 0; s < RPL; ++s) s_ = fma(lr.cb[s], Bown[s][1 + a], s_);
+        } else {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int t = 16 * ch + q;
-        double s_ = 0.0;
-        if (t < Ly::NMF) {
-          const int grp = t / D, a = t % D;  // grp 0: c ; grp r+1: E_r
-          if (grp == 0) {
-#pragma unroll
-            for (int s = 0; s < RPL; ++s) s_ = fma(lr.cb[s], Bown[s][1 + a], s_);
-          } else if (grp - 1 < nf) {
-#pragma unroll
-            for (int s = 0; s < RPL; ++s) s_ = fma(Ev[s][grp - 1], Bown[s][1 + a], s_);
-          }
+          for (int s = 0; s < RPL; ++s) s_ = fma(Ev[s][grp - 1], Bown[s][1 + a], s_);
         }
-        v[q] = s_;
       }
-      wave_reduce<16>(v, red + Ly::R_MF + 16 * ch, lane);
-    }
+      return s_;
+    }, D * (1 + nf), red + Ly::R_MF, lane);
   }
   wave_sync();
   STAMP(W, 2);
@@ -779,6 +974,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
       // lane i (row slot s) reads L0⁻¹[64t+k][64s+i] at blk(t,s)·BLK + i·LD + k for block rows
       // t = s..RPL-1; rows k of Y are broadcast from register slot t
       auto nrows = [&](int t) { const int n = N - WAVE * t; return n < WAVE ? n : WAVE; };
+      const bool fold = FOLD && Ly::SQ && N > 48;
 #pragma unroll
       for (int s = 0; s < RPL; ++s) {
         if (rich) {
@@ -786,8 +982,10 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
 #pragma unroll
           for (int c = 0; c < D1; ++c) a7[c] = 0.0;
 #pragma unroll
-          for (int t = s; t < RPL; ++t)
-            bcast_product<D1, 1>(a7, acc[t], W.Linv + Ly::blk(t, s) * Ly::BLK + lane * Ly::LD, nrows(t));
+          for (int t = s; t < RPL; ++t) {
+            if (fold) bcast_fold_bwd<D1>(a7, acc[t], W.Linv, lane);
+            else bcast_product<D1, 1>(a7, acc[t], W.Linv + Ly::blk(t, s) * Ly::BLK + lane * Ly::LD, nrows(t));
+          }
           wv[s] = a7[0];
 #pragma unroll
           for (int a = 0; a < D; ++a) pv[s][a] = a7[1 + a];
@@ -796,7 +994,8 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
 #pragma unroll
           for (int t = s; t < RPL; ++t) {
             const double v1[1] = {acc[t][0]};
-            bcast_product<1, 1>(a1, v1, W.Linv + Ly::blk(t, s) * Ly::BLK + lane * Ly::LD, nrows(t));
+            if (fold) bcast_fold_bwd<1>(a1, v1, W.Linv, lane);
+            else bcast_product<1, 1>(a1, v1, W.Linv + Ly::blk(t, s) * Ly::BLK + lane * Ly::LD, nrows(t));
           }
           wv[s] = a1[0];
         }
@@ -873,32 +1072,41 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
     for (int s = 0; s < RPL; ++s) {
 #pragma unroll
       for (int a = 0; a < D; ++a) nv[s][a] = x[a] - W.X0[s][a];
-      const double coef = W.valid[s] ? (e.gmu * lr.cb[s] - gsig_over * lr.w[s]) : 0.0;
+      const double coef = W.rowv(kp, s) ? (e.gmu * lr.cb[s] - gsig_over * lr.w[s]) : 0.0;
       ca[s] = coef * W.G12[3 * (lane + WAVE * s) + 1];
       tb[s] = coef * W.G12[3 * (lane + WAVE * s)];
     }
     wave_sync();  // previous users of red are done (all lanes passed phase 4)
+    // NH + 1 values: full chunks of 16, then the tail in a chunk of 8 when it fits (d = 6: 16 + 6)
+    auto hval = [&](int t) {
+      double s_ = 0.0;
+      if (t < Ly::NH) {
+        int a = 0, rem = t;
 #pragma unroll
-    for (int ch = 0; ch < Ly::NHC; ++ch) {
+        for (int aa = 0; aa < D; ++aa) if (a == aa && rem >= D - aa) { rem -= D - aa; a = aa + 1; }
+        const int b = a + rem;
+#pragma unroll
+        for (int s = 0; s < RPL; ++s) s_ = fma(ca[s], nv[s][a] * nv[s][b], s_);
+      } else if (t == Ly::NH) {
+#pragma unroll
+        for (int s = 0; s < RPL; ++s) s_ += tb[s];
+      }
+      return s_;
+    };
+    constexpr int HTAIL = (Ly::NH + 1) % 16;
+    constexpr int HFULL = (HTAIL > 0 && HTAIL <= 8 && !MRBO_HESS16) ? (Ly::NH + 1) / 16 : Ly::NHC;
+#pragma unroll
+    for (int ch = 0; ch < HFULL; ++ch) {
       double vv[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int t = 16 * ch + q;
-        double s_ = 0.0;
-        if (t < Ly::NH) {
-          int a = 0, rem = t;
-#pragma unroll
-          for (int aa = 0; aa < D; ++aa) if (a == aa && rem >= D - aa) { rem -= D - aa; a = aa + 1; }
-          const int b = a + rem;
-#pragma unroll
-          for (int s = 0; s < RPL; ++s) s_ = fma(ca[s], nv[s][a] * nv[s][b], s_);
-        } else if (t == Ly::NH) {
-#pragma unroll
-          for (int s = 0; s < RPL; ++s) s_ += tb[s];
-        }
-        vv[q] = s_;
-      }
+      for (int q = 0; q < 16; ++q) vv[q] = hval(16 * ch + q);
       wave_reduce<16>(vv, red + 16 * ch, lane);
+    }
+    if constexpr (HFULL < Ly::NHC) {
+      double vv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) vv[q] = hval(16 * HFULL + q);
+      wave_reduce<8>(vv, red + 16 * HFULL, lane);
     }
   }
   wave_sync();
@@ -958,8 +1166,8 @@ __device__ __forceinline__ int condition(WaveCtx<D, RPL>& W, const KParams& kp, 
 #pragma unroll
   for (int s = 0; s < RPL; ++s) {
     const int i = lane + WAVE * s;
-    W.E[(long long)nf * NR + i] = W.valid[s] ? -lr.w[s] * inv : 0.0;
-    W.C[(long long)(S + 2) * NR + i] = W.valid[s] ? (lr.cb[s] - gam * lr.w[s]) : 0.0;
+    W.E[(long long)nf * NR + i] = W.rowv(kp, s) ? -lr.w[s] * inv : 0.0;
+    W.C[(long long)(S + 2) * NR + i] = W.rowv(kp, s) ? (lr.cb[s] - gam * lr.w[s]) : 0.0;
   }
   wave_sync();
   if (lane < nf) {
@@ -1282,7 +1490,7 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParam
     if constexpr (ROWS_KEPT) g1 = W.G12[3 * (lane + WAVE * s)];
     else rad_eval(W.rad, rho2, psi, g1, g2);
     const double cb = W.C[(long long)(S + 1) * NR + lane + WAVE * s];
-    v[0] += W.valid[s] ? fabs(cb) * fabs(g1) * fast_sqrt0(rho2) : 0.0;
+    v[0] += W.rowv(kp, s) ? fabs(cb) * fabs(g1) * fast_sqrt0(rho2) : 0.0;
   }
   if (lane < nf) {
     double rho2 = 0.0;
@@ -1450,7 +1658,15 @@ __device__ __forceinline__ void stage_start_tables(const KParams& kp, double* sm
   // this workgroup's global slice, the base Gram YᵀY (upper triangle) to gtab
   const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
   double* red = smem + tb.end + (long long)wv * Ly::WAVE_LDS;   // wave-area scratch
+  // One table for the launch: every workgroup computes bit-identical Y0 rows (same inputs, same
+  // code), so they all write the same values to the same slice -- a race between identical values,
+  // which any reader resolves to the same bits.  The per-workgroup slices (MRBO_YTAB_PER_WG) wrote
+  // 2.4 MB per C3 launch to HBM; the shared slice ends as one dirty copy per XCD L2.
+#ifdef MRBO_YTAB_PER_WG
   double* ytab = kp.ytab + (long long)blockIdx.x * ns * NR;
+#else
+  double* ytab = kp.ytab;
+#endif
   for (int k = wv; k < ns; k += nw) {
     double bv[Ly::D1], acc[Ly::D1];
     double rho2 = 0.0, r[D];
@@ -1816,7 +2032,7 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
     double psi, g1, g2;
     rad_eval(W.rad, rho2, psi, g1, g2);
 #pragma unroll
-    for (int a = 0; a < D; ++a) u[s][a] = W.valid[s] ? g1 * r[a] : 0.0;
+    for (int a = 0; a < D; ++a) u[s][a] = W.rowv(kp, s) ? g1 * r[a] : 0.0;
   }
   wave_sync();
 #pragma unroll
@@ -2140,7 +2356,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
         if (lane < D) {
           U[Ly::U_DX + lane] = kp.dual_y
               ? kp.dual_y[(long long)lane + D * ((j - 1) + (long long)h * (m + (long long)M * r))]
-              : dual_uniform(kp.seed, (long long)(kp.sample_offset + m) + (long long)kp.samples_total * r, j, lane);
+              : dual_uniform(kp.seed, (long long)(kp.sample_offset + m), j, lane);   // keyed by the global sample alone
         }
         wave_sync();
         // i == j: solve_dual_x(j) (rollout.jl:150-191) then pair (j, j-1);
@@ -2236,7 +2452,11 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
   W.XS = kp.xs_lds ? smem + tb.xs : kp.xstarts;
   W.KXB = Ly::SQ ? smem + tb.kxb : kp.kxb_g;
   W.GTAB = Ly::SQ ? smem + tb.gtab : kp.gtab_g;
+#ifdef MRBO_YTAB_PER_WG
   W.YTAB = kp.ytab + (long long)blockIdx.x * kp.nstarts * Ly::NR;
+#else
+  W.YTAB = kp.ytab;   // the launch's shared table (stage_start_tables)
+#endif
   W.B = wbase;
   W.red = wbase + Ly::BROWS * Ly::BS;
   W.U = W.red + Ly::REDN;
@@ -2259,6 +2479,13 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
     W.valid[s] = i < kp.N;
 #pragma unroll
     for (int a = 0; a < D; ++a) W.X0[s][a] = kp.X0[(long long)a * Ly::NR + i];
+#ifndef MRBO_NO_PAD_FAR
+    // padded rows far from every point (see WaveCtx::rowv): |x − X_i|² ≈ d·1e200 stays finite, and
+    // ψ, g1 = ψ'/ρ, g2 underflow to exactly 0 for the Matérn and SE kernels
+    if (!W.valid[s] && kp.kernel != KERNEL_PERIODIC)
+#pragma unroll
+      for (int a = 0; a < D; ++a) W.X0[s][a] = PAD_FAR;
+#endif
   }
   // zero this wave's LDS so that padded rows read as zeros
   for (int q = W.lane; q < Ly::WAVE_LDS; q += WAVE) wbase[q] = 0.0;
@@ -2311,9 +2538,33 @@ __global__ void __launch_bounds__((KBounds<D, RPL>::threads), (KBounds<D, RPL>::
 #ifdef MRBO_STAMPS
   W.tlast = __builtin_amdgcn_s_memtime();
 #endif
+#ifndef MRBO_QUEUE_SINGLE
+  // One queue per XCD over a contiguous eighth of the trajectories (chunk x = [x·T/8, (x+1)·T/8),
+  // its head at kp.queue[16·x], one 64-B line each): the waves of an XCD first drain the chunk of
+  // their own XCD (HW_REG_XCC_ID), then the others in turn.  Consecutive trajectories then finish
+  // on one XCD, so the 8-byte output rows (values, ∇θ, status, counters) fill whole cache lines
+  // in one L2: with one queue for the chip, neighbouring rows came from all 8 L2s and each wrote
+  // back its own partial line (C3: 17.6 MB written per launch for 7.1 MB of outputs).  Placement
+  // is used for speed only: any wave may take any chunk, every trajectory is taken exactly once.
+  int xcc = 0, visited = 0;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  int chunk = xcc & 7;
+#endif
   for (;;) {
     long long tr = 0;
+#ifdef MRBO_QUEUE_SINGLE
     if (W.lane == 0) tr = atomicAdd(kp.queue, 1);
+#else
+    if (W.lane == 0) {
+      for (;;) {
+        const long long lo = (long long)chunk * kp.T / 8, hi = (long long)(chunk + 1) * kp.T / 8;
+        const long long idx = lo + atomicAdd(kp.queue + 16 * chunk, 1);
+        if (idx < hi) { tr = idx; break; }
+        if (++visited == 8) { tr = kp.T; break; }
+        chunk = (chunk + 1) & 7;
+      }
+    }
+#endif
     tr = __shfl(tr, 0, WAVE);
     if (tr >= kp.T) break;
     if (kp.order) {   // caller's schedule (a permutation; an out-of-range entry falls back to tr)

@@ -236,7 +236,7 @@ MYOPIC_RULES = {"ei": (EI, 0.0), "poi": (POI, 0.0), "lcb": (LCB, 2.0)}   # :151-
 
 def run_myopic(function_name, output_dir, budget=100, trials=60, starts=64, seed=1906, device=0, log=print,
                rules=("ei", "poi", "lcb"), optimize=True, initial_observations=INITIAL_OBSERVATIONS,
-               reuse_surrogate=True, capacity=None):
+               reuse_surrogate=True, capacity=None, solve_margin=0.0):
     """myopic_bayesopt.jl's loop: per budget step xnext = multistart_base_solve!(sur, …; guesses =
     generate_initial_guesses(starts, lbs, ubs), θfixed) -- the deterministic multistart local solve of
     the analytic acquisition on the base surrogate (:224-233), here mrbo_base_solve on the device --
@@ -248,7 +248,12 @@ def run_myopic(function_name, output_dir, budget=100, trials=60, starts=64, seed
     reset! keeps the kernel, so each trial starts from the lengthscale the previous trial's last
     optimize! left (only the very first trial starts at Matern52()'s ℓ = 1), and past `capacity`
     observations condition! conditions a discarded resized copy (Surrogate.condition).  False: a
-    fresh surrogate with ℓ = 1 and capacity budget + initial per trial (the round-3 loop)."""
+    fresh surrogate with ℓ = 1 and capacity budget + initial per trial (the round-3 loop).
+
+    solve_margin (diagnostic, build-defined; 0 = the reference's box): the acquisition is solved on
+    the box shrunk by solve_margin·(ub − lb) per side -- a proxy for IPNewton's interior iterates
+    (rbf_optim.jl:24-30: a log barrier keeps them off the faces), used to test whether the
+    projected Newton's stops on the faces explain a difference."""
     from .rbf_optim import multistart_base_solve
     from .utils import generate_initial_guesses
     testfn = TESTFNS[function_name]()
@@ -290,7 +295,11 @@ def run_myopic(function_name, output_dir, budget=100, trials=60, starts=64, seed
             xnext = np.zeros(testfn.dim)
             for b in range(budget):
                 t0 = time.perf_counter()
-                multistart_base_solve(sur, xnext, lbs, ubs, guesses, [theta], device=device)
+                if solve_margin > 0.0:
+                    w = (ubs - lbs) * solve_margin
+                    multistart_base_solve(sur, xnext, lbs + w, ubs - w, guesses, [theta], device=device)
+                else:
+                    multistart_base_solve(sur, xnext, lbs, ubs, guesses, [theta], device=device)
                 times[b] = time.perf_counter() - t0
                 observed_best = float(np.min(sur.get_active_observations()))
                 regrets[b] = simple_regret(true_minimum, observed_best)

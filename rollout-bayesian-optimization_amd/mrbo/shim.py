@@ -128,6 +128,8 @@ def simulate_trajectory_mc_batch(T, tp, X0, inner_solve_xstarts, with_gradient=T
     gt = np.zeros((1, M, R), order="F") if with_gradient else None
     _launch(plan, X0, rn, xs, vals, gx, gt, status)
     _raise(status)
+    # per restart exactly the R = 1 method's reductions (_eto), so that the two call sequences agree
+    # bit for bit (numpy's axis reductions may sum in another order)
     etos = [_eto(vals[:, r], None if gx is None else gx[:, :, r], None if gt is None else gt[:, :, r])
             for r in range(R)]
     return etos, vals, gx, gt

@@ -4,7 +4,8 @@ with -DMRBO_AB_MIN (RPL = 1, the specialised kernel only: seconds instead of min
 flags, linked with the main build's host-API and GP-fit objects into mrbo/variants/libmrbo_<name>.so.
 Plans of other shapes fail to create in such a library.
 
-usage: python tools/ab_variant.py name:"-DFLAG ..." [name:"..."] ... [--dims 6] [--fmax 4]
+usage: python tools/ab_variant.py name:"-DFLAG ..." [name:"..."] ... [--dims 6] [--fmax 4] [--rpl 1]
+(C5: --dims 8 --fmax 6 --rpl 4)
 Run __graft_entry__.build() first (the api / gpfit objects come from its object directory).
 """
 import os
@@ -19,10 +20,14 @@ import __graft_entry__ as g  # noqa: E402
 
 def main():
     args = sys.argv[1:]
-    dims, fmax = [6], 4
+    dims, fmax, rpl = [6], 4, 1
     if "--dims" in args:
         i = args.index("--dims")
         dims = [int(x) for x in args[i + 1].split(",")]
+        del args[i:i + 2]
+    if "--rpl" in args:
+        i = args.index("--rpl")
+        rpl = int(args[i + 1])
         del args[i:i + 2]
     if "--fmax" in args:
         i = args.index("--fmax")
@@ -41,12 +46,12 @@ def main():
         objs = []
         for d in dims:
             obj = os.path.join(vdir, f"{name}_k{d}_f{fmax}.o")
-            defs = [f"-DMRBO_D={d}", "-DMRBO_AB_MIN"] + ([f"-DMRBO_FMAX={fmax}"] if fmax != 6 else [])
+            defs = [f"-DMRBO_D={d}", "-DMRBO_AB_MIN", f"-DMRBO_AB_RPL={rpl}"] + ([f"-DMRBO_FMAX={fmax}"] if fmax != 6 else [])
             cmd = [hipcc] + g.HIPCC_FLAGS + g.UNIT_FLAGS + shlex.split(flags) + defs + \
                   ["-c", "-o", obj, os.path.join(g.CSRC, "mrbo_kernels.hip")]
             procs.append((subprocess.Popen(cmd, stderr=subprocess.DEVNULL), name))
             objs.append(obj)
-        if "-DMRBO_STAMPS" in flags:   # the host side allocates and prints the stamp counters
+        if True:   # a fresh host API with the variant's flags (stamp counters, queue layout, ...)
             api = os.path.join(vdir, f"{name}_api.o")
             cmd = [hipcc] + g.HIPCC_FLAGS + shlex.split(flags) + ["-c", "-o", api, os.path.join(g.CSRC, "mrbo_api.hip")]
             procs.append((subprocess.Popen(cmd, stderr=subprocess.DEVNULL), name))

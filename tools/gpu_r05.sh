@@ -11,6 +11,9 @@
 #             set; a comma list of tools/bo_compare.py SETTINGS keys) -> bo_compare.jsonl
 #   sharded   C3 bench over the multi-rank path at one rank (--sharded: RCCL all-gather, device merge)
 #             beside the plain line, 10 steps each, no CPU baseline
+#   shim      tools/shim_rate.py at C3 (the Julia drop-in's call patterns)
+#   c2        C2 bench line (20 steps)
+#   c5cost    C5 + NonUniformCost at M = 256, R = 128 (one step)
 #   prof      rocprofv3 --kernel-trace --stats of the default bench (1 step) + FETCH_SIZE / WRITE_SIZE
 #             passes (tools/profile.sh), C3 and C3-MLE
 # Outputs under gpurun_out/<tag>/.
@@ -68,6 +71,16 @@ for l in open(sys.argv[1]):
       timeout -k 10 ${BO_TIMEOUT:-1000} python -u tools/bo_compare.py --trials ${BO_TRIALS:-40} --cases ${BO_CASES:-asserted} ${BO_ARGS:-} \
         --out "$out/bo_compare.jsonl" > /dev/null 2> "$out/bo_compare.err"
       rc=$?; grep "final gap" "$out/bo_compare.err" ;;
+    shim)
+      timeout -k 10 300 python -u tools/shim_rate.py --config C3 > "$out/shim_rate_c3.json" 2> "$out/shim_rate_c3.err"
+      rc=$?; cat "$out/shim_rate_c3.json" ;;
+    c2)
+      timeout -k 10 200 python -u bench.py --config C2 --no-cpu-baseline --steps 20 > "$out/bench_c2.json" 2> "$out/bench_c2.err"
+      rc=$?; tail -c 400 "$out/bench_c2.json" ;;
+    c5cost)
+      timeout -k 10 400 python -u bench.py --config C5 --cost --mc-per-gpu 256 --restarts 128 --steps 1 --warmup 1 --no-cpu-baseline \
+        > "$out/bench_c5_cost.json" 2> "$out/bench_c5_cost.err"
+      rc=$?; tail -c 400 "$out/bench_c5_cost.json" ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac
   echo "== $step rc=$rc $(date +%T)"

@@ -55,7 +55,22 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / n
 
-    rows = {}
+    # the C-ABI call alone (host pointers, staging included, no host reductions), batched shape
+    import ctypes
+    from mrbo import _lib
+    plan_b = shim.cached_plan(T.s, tp, T.θ[0], xs.shape[1], R=R)
+    X0 = np.asfortranarray(pb.x0s, dtype=np.float64)
+    rn = np.asfortranarray(tp.rnstream_sequence, dtype=np.float64)
+    vals, st = np.zeros((M, R), order="F"), np.zeros((M, R), dtype=np.int32, order="F")
+    gxb, gtb = np.zeros((d, M, R), order="F"), np.zeros((1, M, R), order="F")
+
+    def c_call(k):
+        shim._launch(plan_b, X0, rn, np.asfortranarray(xs), vals, gxb, gtb, st)
+
+    rows = {"batched_c_call_only": None}
+    s_c = timed(c_call, max(2, a.calls // 4))
+    rows["batched_c_call_only"] = {"trajectories_per_call": M * R, "ms_per_call": s_c * 1e3,
+                                   "trajectories_per_s": M * R / s_c}
     shim.release_plans()
     for name, fn, per in (("per_call_plan", fresh_call, M), ("cached_r1", r1_call, M), ("batched", batch_call, M * R)):
         n = a.calls if name != "batched" else max(2, a.calls // 4)
