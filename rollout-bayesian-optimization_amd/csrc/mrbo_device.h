@@ -257,6 +257,26 @@ __device__ __forceinline__ void wave_reduce(double (&v)[K], double* red, int lan
 #endif
 }
 
+// wave_reduce within each 32-lane half of the wave (half-wave mode: two trajectories per wave, one
+// per half): the same transpose steps from lane bit 4 down, no v_permlane32_swap; each half stores
+// its own K sums through its own red pointer.  K ≤ 16.
+template <int K>
+__device__ __forceinline__ void half_reduce(double (&v)[K], double* red, int lane) {
+  constexpr int S = (K == 1) ? 0 : (K == 2) ? 1 : (K == 4) ? 2 : (K == 8) ? 3 : 4;
+  static_assert((1 << S) == K && K <= 16, "half_reduce: K a power of two <= 16");
+  int idx = 0;
+  if constexpr (S >= 1) fold_step<16, K / 2>(v, lane, idx);
+  if constexpr (S >= 2) fold_step<8, K / 4>(v, lane, idx);
+  if constexpr (S >= 3) fold_step<4, K / 8>(v, lane, idx);
+  if constexpr (S >= 4) fold_step<2, K / 16>(v, lane, idx);
+  if constexpr (S < 1) v[0] = fold_all<16>(v[0]);
+  if constexpr (S < 2) v[0] = fold_all<8>(v[0]);
+  if constexpr (S < 3) v[0] = fold_all<4>(v[0]);
+  if constexpr (S < 4) v[0] = fold_all<2>(v[0]);
+  v[0] = fold_all<1>(v[0]);
+  red[idx] = v[0];
+}
+
 // Sum over the 64 lanes in EVERY lane, no LDS round trip: the butterfly of wave_reduce<1>
 // (each step adds the partner's value; a + b == b + a, so all lanes hold the same bits, those
 // wave_reduce<1> stores for lane 0).

@@ -20,6 +20,10 @@ struct KernelSet {
   bool gl;                  // L0⁻¹ in global memory: packed by columns, then packed by rows
   long long linv_dev;       // doubles of the device image
   int max_threads;          // launch bound (threads per workgroup)
+  // half-wave mode (N ≤ 32, d ≤ 4, h ≤ 3): rollout_kernel<D, 1, 1, 2>, two trajectories per wave
+  // (Matérn-5/2 + EI), with its per-wave LDS (two trajectory areas); null where not compiled
+  const void* rollout_half = nullptr;
+  size_t wave_bytes_half = 0;
 };
 
 // The host API sees every unit's entry points as weak references (MRBO_API_TU): a library

@@ -34,6 +34,13 @@ constexpr bool has_rpl(int d, int rpl) { return rpl == MRBO_AB_RPL; }
 constexpr bool has_rpl(int d, int rpl) { return rpl == 1 || rpl == 2 || (d <= 8 && (rpl == 4 || rpl == 8)); }
 #endif
 constexpr bool has_spec(int d, int rpl) { return d <= 8 && rpl <= 4; }
+// half-wave kernel rollout_kernel<D, 1, 1, 2> (two trajectories per wave, N ≤ 32): the FMAX = 4
+// units of d ≤ 4, Matérn-5/2 + EI (C1, C2)
+#if MRBO_FMAX == 4 && MRBO_D <= 4 && !(defined(MRBO_AB_MIN) && defined(MRBO_AB_GENERIC)) && !defined(MRBO_STAMPS)
+#define MRBO_HAS_HALF 1
+#else
+#define MRBO_HAS_HALF 0
+#endif
 
 template <int D, int RPL>
 static KernelSet kset() {
@@ -50,7 +57,12 @@ static KernelSet kset() {
   return KernelSet{(const void*)&rollout_kernel<D, RPL, 0>, spec, (const void*)&eval_base_kernel<D, RPL>,
 #endif
                    sizeof(double) * Ly::WAVE_LDS, Ly::SQ, Ly::BC && !Ly::SQ, Ly::LD, Ly::LINV_DOUBLES, Ly::GL,
-                   Ly::LINV_GLOBAL, KBounds<D, RPL>::threads};
+                   Ly::LINV_GLOBAL, KBounds<D, RPL>::threads
+#if MRBO_HAS_HALF
+                   , RPL == 1 ? (const void*)&rollout_kernel<D, 1, 1, 2> : nullptr,
+                   RPL == 1 ? 2 * sizeof(double) * Lay<D, 1, 2>::WAVE_LDS : 0
+#endif
+  };
 }
 
 bool MRBO_SFX(kset_d)(int rpl, KernelSet& ks) {
@@ -92,8 +104,15 @@ static void launch_rollout_spec(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t 
   else launch_one<8, SPEC>(g, b, sm, st, kp);
 }
 
+// spec: 0 generic, 1 Matérn-5/2 + EI, 2 the half-wave kernel (rows per lane 1)
 void MRBO_SFX(launch_rollout_d)(int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st,
                                        const KParams& kp) {
+#if MRBO_HAS_HALF
+  if (spec == 2) {
+    if (rpl == 1) hipLaunchKernelGGL((rollout_kernel<MRBO_D, 1, 1, 2>), g, b, sm, st, kp);
+    return;
+  }
+#endif
   if (spec) launch_rollout_spec<1>(rpl, g, b, sm, st, kp);
   else launch_rollout_spec<0>(rpl, g, b, sm, st, kp);
 }

@@ -36,11 +36,15 @@ inline namespace MRBO_FNS {
 
 constexpr double PAD_FAR = 1e100;   // coordinate of padded data rows (WaveCtx::rowv)
 
-template <int D, int RPL>
+template <int D, int RPL, int HW = 1>
 struct Lay {
   static constexpr int D1 = D + 1;
   static constexpr int BS = (D1 + 1) & ~1;         // B row stride in doubles (16-B aligned rows)
-  static constexpr int NR = RPL * WAVE;            // base-row capacity of the wave
+  static constexpr int NR = RPL * WAVE;            // base-row capacity (global arrays: X0, c0, tables)
+  // half-wave mode (HW = 2, N ≤ 32, RPL = 1): two trajectories per wave, lanes 32h..32h+31 own
+  // trajectory h; LANES lanes per trajectory, NRL rows of per-trajectory LDS state (E, C, G12)
+  static constexpr int LANES = WAVE / HW;
+  static constexpr int NRL = RPL * LANES;
   // L0⁻¹ layout (see LINV_DOUBLES below).  BC: register-broadcast triangular products over
   // square 64×64 blocks of L0⁻¹ in LDS (RPL = 1: one block; RPL = 2: the three blocks of the
   // lower block triangle), which also moves the base kernel rows out of LDS.  SQ (RPL = 1)
@@ -98,8 +102,8 @@ struct Lay {
   static constexpr int U_STAMP = U_HF + FMAX * (D + 2);   // cycle accumulators (MRBO_STAMPS)
   static constexpr int U_KC = U_STAMP + NSTAMP_SLOTS;             // launch constants (KC_*), see wave_setup
   static constexpr int U_SIZE = ((U_KC + 13) + 1) & ~1;
-  static constexpr int G12 = 3 * NR;                     // per-lane [g1, g2, Y0] of the base rows
-  static constexpr int EC = SQ ? (2 * FMAX + 1) * NR : 0;  // E (FMAX×NR) + C ((FMAX+1)×NR) in LDS
+  static constexpr int G12 = 3 * NRL;                    // per-lane [g1, g2, Y0] of the base rows
+  static constexpr int EC = SQ ? (2 * FMAX + 1) * NRL : 0;  // E (FMAX×NRL) + C ((FMAX+1)×NRL) in LDS
   static constexpr int WAVE_LDS = BROWS * BS + REDN + U_SIZE + G12 + EC;
   // L0⁻¹ in LDS, shared by the waves of a workgroup.  BC: dense zero-padded 64×64 blocks,
   // column-major with odd leading dimension LD = 65, so the column walk (forward product,
@@ -136,7 +140,7 @@ enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, 
 enum { KC_PSI0 = 0, KC_D2PSI0 = 1, KC_THETA = 2, KC_SIGTOL = 3, KC_GTOL = 4, KC_GCMU = 5, KC_GCSIG = 6,
        KC_GCD2 = 7, KC_XTOL = 8, KC_FTOL = 9, KC_HTOL = 10, KC_SN2 = 11,
        KC_BOX = 12 };   // max_a (ub_a − lb_a): the Newton step's length cap
-#define KCV(F) (W.U[Lay<D, RPL>::U_KC + KC_##F])
+#define KCV(F) (W.U[Lay<D, RPL, HW>::U_KC + KC_##F])
 
 // ∂_lane c(x) by unrolled select (lane < D; a runtime index would put gc in scratch)
 template <int D>
@@ -151,11 +155,11 @@ __device__ __forceinline__ double lane_pick(const double (&v)[D], int lane) {
 // each rounded to an even number of doubles; then the per-wave areas.  gtab[k] is the base
 // Gram of start k, (L0⁻¹B)ᵀ(L0⁻¹B) with B = [kx, ∇kx](x_k), upper triangle row-major; its
 // entry 0 is |L0⁻¹kx(x_k)|².
-template <int D, int RPL>
+template <int D, int RPL, int HW = 1>
 struct WgTables {
   long long xs, kxb, gtab, end;   // offsets in doubles from smem
   __device__ __forceinline__ WgTables(const KParams& kp) {
-    using Ly = Lay<D, RPL>;
+    using Ly = Lay<D, RPL, HW>;
     xs = Ly::LINV_DOUBLES;
     const long long nxs = kp.xs_lds ? (((long long)kp.nstarts * D + 1) & ~1LL) : 0;
     kxb = xs + nxs;
@@ -166,10 +170,11 @@ struct WgTables {
   }
 };
 
-template <int D, int RPL>
+template <int D, int RPL, int HW = 1>
 struct WaveCtx {
-  using Ly = Lay<D, RPL>;
-  int lane;
+  using Ly = Lay<D, RPL, HW>;
+  int lane;             // lane within the trajectory's lanes (0..LANES-1)
+  int half;             // HW = 2: which half of the wave (its trajectory); 0 otherwise
   double* B;            // LDS: BROWS × BS
   double* red;          // LDS: REDN
   double* U;            // LDS: U_SIZE
@@ -207,6 +212,58 @@ struct WaveCtx {
   }
 };
 
+// ---- cross-lane primitives of one trajectory's lanes ----------------------------------------
+// HW = 1: the whole wave.  HW = 2 (half-wave mode): the 32-lane half holding the trajectory -- its
+// reductions stop at lane bit 4, its ballots are its 32 bits, lane k of a half is lane k + 32·half
+template <int HW, int K>
+__device__ __forceinline__ void hw_reduce(double (&v)[K], double* red, int lane) {
+  if constexpr (HW == 1) wave_reduce<K>(v, red, lane);
+  else half_reduce<K>(v, red, lane);
+}
+template <int HW>
+__device__ __forceinline__ double hw_allreduce1(double v) {
+  if constexpr (HW == 1) {
+    return wave_allreduce1(v);
+  } else {
+    v = fold_all<16>(v);
+    v = fold_all<8>(v);
+    v = fold_all<4>(v);
+    v = fold_all<2>(v);
+    return fold_all<1>(v);
+  }
+}
+template <int HW>
+__device__ __forceinline__ unsigned long long hw_ballot(bool c, int half) {
+  const unsigned long long m = __ballot(c);
+  if constexpr (HW == 1) return m;
+  else return half ? (m >> 32) : (m & 0xffffffffull);
+}
+// value of lane k (k a compile-time or wave-uniform index) of this trajectory's lanes
+template <int HW>
+__device__ __forceinline__ double hw_readlane_d(double v, int k, int half) {
+  if constexpr (HW == 1) {
+    return readlane_d(v, k);
+  } else {
+    const double a = readlane_d(v, k), b = readlane_d(v, k + 32);
+    return half ? b : a;
+  }
+}
+template <int HW>
+__device__ __forceinline__ int hw_readlane_i(int v, int k, int half) {
+  if constexpr (HW == 1) {
+    return __builtin_amdgcn_readlane(v, k);
+  } else {
+    const int a = __builtin_amdgcn_readlane(v, k), b = __builtin_amdgcn_readlane(v, k + 32);
+    return half ? b : a;
+  }
+}
+// value of lane k of this trajectory's lanes for a per-trajectory (HW = 2: per-half, divergent) k
+template <int HW>
+__device__ __forceinline__ double hw_lane_d(double v, int k, int half) {
+  if constexpr (HW == 1) return readlane_d(v, k);
+  else return __shfl(v, k + 32 * half, WAVE);
+}
+
 // work counters per trajectory (NCOUNT, mrbo_device.h)
 struct Counters {
   int grad = 0, value = 0, hess = 0, rich = 0, pairs = 0;
@@ -222,7 +279,7 @@ struct Counters {
 #endif
 
 // Per-lane results of an evaluation that later phases (conditioning, adjoint) need.
-template <int D, int RPL>
+template <int D, int RPL, int HW = 1>
 struct LaneRes {
   double w[RPL];
   double P[RPL][D];
@@ -230,14 +287,14 @@ struct LaneRes {
 };
 
 #ifdef MRBO_STAMPS
-template <int D, int RPL>
-__device__ __forceinline__ void stamp_count(WaveCtx<D, RPL>& W, int k, unsigned long long v) {
-  if (W.lane == 0) reinterpret_cast<unsigned long long*>(W.U + Lay<D, RPL>::U_STAMP)[k] += v;
+template <int D, int RPL, int HW>
+__device__ __forceinline__ void stamp_count(WaveCtx<D, RPL, HW>& W, int k, unsigned long long v) {
+  if (W.lane == 0) reinterpret_cast<unsigned long long*>(W.U + Lay<D, RPL, HW>::U_STAMP)[k] += v;
 }
-template <int D, int RPL>
-__device__ __forceinline__ void stamp_region(WaveCtx<D, RPL>& W, int k) {
+template <int D, int RPL, int HW>
+__device__ __forceinline__ void stamp_region(WaveCtx<D, RPL, HW>& W, int k) {
   const unsigned long long now = __builtin_amdgcn_s_memtime();
-  if (W.lane == 0) reinterpret_cast<unsigned long long*>(W.U + Lay<D, RPL>::U_STAMP)[k] += now - W.tlast;
+  if (W.lane == 0) reinterpret_cast<unsigned long long*>(W.U + Lay<D, RPL, HW>::U_STAMP)[k] += now - W.tlast;
   W.tlast = now;
 }
 #endif
@@ -286,9 +343,29 @@ __device__ __forceinline__ void bcast_run(double (&acc)[K], const double (&bq)[K
   BcastAsm<K, STRIDE>::run(acc, bq, addr);
 }
 
-template <int K, int JSTRIDE>
+template <int K, int JSTRIDE, int HW = 1>
 __device__ __forceinline__ void bcast_product_k(double (&acc)[K], const double (&v)[K], const double* lbase, int nrows) {
   const unsigned a0 = lds_addr(lbase);
+  if constexpr (HW == 2) {
+    // half-wave mode (N ≤ 32): each half holds its trajectory's rows 0..31 in DPP rows 2h, 2h+1,
+    // so ONE v_permlane16_swap per dword yields block 0 of both halves ([r0 r0 r2 r2]) and block 1
+    // ([r1 r1 r3 r3]); no swap crosses the halves
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      if (16 * p >= nrows) break;
+      double bp[K];
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        int lo, hi;
+        dsplit(v[c], lo, hi);
+        const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        bp[c] = p == 0 ? djoin(a[0], b[0]) : djoin(a[1], b[1]);
+      }
+      bcast_run<K, 8 * JSTRIDE>(acc, bp, a0 + 8u * 16u * p * JSTRIDE);
+    }
+    return;
+  }
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     if (16 * p >= nrows) break;
@@ -303,13 +380,13 @@ __device__ __forceinline__ void bcast_product_k(double (&acc)[K], const double (
   }
 }
 
-template <int K, int JSTRIDE>
+template <int K, int JSTRIDE, int HW = 1>
 __device__ __forceinline__ void bcast_product(double (&acc)[K], const double (&v)[K], const double* lbase, int nrows) {
   if constexpr (K > 9) {
-    bcast_product<8, JSTRIDE>(head8(acc), head8(v), lbase, nrows);
-    bcast_product<K - 8, JSTRIDE>(tail8(acc), tail8(v), lbase, nrows);
+    bcast_product<8, JSTRIDE, HW>(head8(acc), head8(v), lbase, nrows);
+    bcast_product<K - 8, JSTRIDE, HW>(tail8(acc), tail8(v), lbase, nrows);
   } else {
-    bcast_product_k<K, JSTRIDE>(acc, v, lbase, nrows);
+    bcast_product_k<K, JSTRIDE, HW>(acc, v, lbase, nrows);
   }
 }
 
@@ -441,7 +518,7 @@ __device__ __forceinline__ void bcast_fold_bwd(double (&acc)[K], const double (&
 // ≈ K + log2(64/K) exchanges, so a chunk of 6 values in wave_reduce<8> saves ≈ 30 VALU against
 // wave_reduce<16> (the Hessian's tail chunk: C3 −1 %).  Slots t ≥ n of a chunk hold junk.  t is a
 // compile-time constant in every call of fill.  MRBO_REDUCE16: every chunk of 16 (A/B).
-template <int CH, class F>
+template <int HW, int CH, class F>
 __device__ __forceinline__ void wave_reduce_n(F&& fill, int n, double* red, int lane) {
 #pragma unroll
   for (int ch = 0; ch < CH; ++ch) {
@@ -452,24 +529,24 @@ __device__ __forceinline__ void wave_reduce_n(F&& fill, int n, double* red, int 
       double v[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) v[q] = fill(16 * ch + q);
-      wave_reduce<2>(v, red + 16 * ch, lane);
+      hw_reduce<HW, 2>(v, red + 16 * ch, lane);
     } else if (rem <= 4) {
       double v[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = fill(16 * ch + q);
-      wave_reduce<4>(v, red + 16 * ch, lane);
+      hw_reduce<HW, 4>(v, red + 16 * ch, lane);
     } else if (rem <= 8) {
       double v[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = fill(16 * ch + q);
-      wave_reduce<8>(v, red + 16 * ch, lane);
+      hw_reduce<HW, 8>(v, red + 16 * ch, lane);
     } else
 #endif
     {
       double v[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) v[q] = fill(16 * ch + q);
-      wave_reduce<16>(v, red + 16 * ch, lane);
+      hw_reduce<HW, 16>(v, red + 16 * ch, lane);
     }
   }
 }
@@ -521,8 +598,8 @@ __device__ __forceinline__ void gl_bcast_product(double (&acc)[K], const double 
   }
 }
 
-template <int D, int RPL>
-__device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL>& W, const KParams& kp);
+template <int D, int RPL, int HW>
+__device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL, HW>& W, const KParams& kp);
 
 // ================================================================================
 // eval(fs, x, θ; fantasy_index = S)  -- radial_basis_surrogates.jl:482-581
@@ -531,10 +608,10 @@ __device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL>& W, const KParams& 
 // back_after (GRAD / GRADC / GSTART of the Newton iteration): the projected-gradient test runs
 // here and, when the step continues, the BACK part (backward product, Hα) follows in the same
 // call with the forward state still in registers.  Returns 1 when that BACK part ran.
-template <int D, int RPL>
-__device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, int S, int mode, LaneRes<D, RPL>& lr,
+template <int D, int RPL, int HW>
+__device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& kp, int S, int mode, LaneRes<D, RPL, HW>& lr,
                                         int kst = 0, bool back_after = false) {
-  using Ly = Lay<D, RPL>;
+  using Ly = Lay<D, RPL, HW>;
   constexpr int D1 = Ly::D1, BS = Ly::BS, NR = Ly::NR;
   // Opaque copy of the lane index: keeps the per-lane LDS/global addresses derived from it
   // inside this evaluation instead of being hoisted (and held live in VGPRs) across the
@@ -558,9 +635,9 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
   double Ev[RPL][FMAX];
 #pragma unroll
   for (int s = 0; s < RPL; ++s) {
-    lr.cb[s] = W.C[(long long)(S + 1) * NR + lane + WAVE * s];
+    lr.cb[s] = W.C[(long long)(S + 1) * Ly::NRL + lane + WAVE * s];
 #pragma unroll
-    for (int r = 0; r < FMAX; ++r) Ev[s][r] = W.E[(long long)r * NR + lane + WAVE * s];   // unconditional
+    for (int r = 0; r < FMAX; ++r) Ev[s][r] = W.E[(long long)r * Ly::NRL + lane + WAVE * s];   // unconditional
 #pragma unroll
     for (int r = 0; r < FMAX; ++r) Ev[s][r] = (r < nf) ? Ev[s][r] : 0.0;
   }
@@ -648,7 +725,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
     // broadcast from register slot t.  Row slot s sums block columns t = 0..s in order.
     auto nrows = [&](int t) { const int n = N - WAVE * t; return n < WAVE ? n : WAVE; };
     // RPL = 1 with N > 48: the folded three-pass products (bcast_fold_fwd / _bwd)
-    const bool fold = FOLD && Ly::SQ && N > 48;
+    const bool fold = FOLD && Ly::SQ && HW == 1 && N > 48;
     if (mode == EV_VALUE) {
 #pragma unroll
       for (int s = 0; s < RPL; ++s) {
@@ -657,7 +734,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
         for (int t = 0; t <= s; ++t) {
           const double v1[1] = {Bown[t][0]};
           if (fold) bcast_fold_fwd<1>(a1, v1, W.Linv, lane);
-          else bcast_product<1, Ly::LD>(a1, v1, W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
+          else bcast_product<1, Ly::LD, HW>(a1, v1, W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
         }
         acc[s][0] = a1[0];
       }
@@ -675,7 +752,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
 #pragma unroll
           for (int a = 0; a < D; ++a) vg[a] = Bown[t][1 + a];
           if (fold) bcast_fold_fwd<D>(ag, vg, W.Linv, lane);
-          else bcast_product<D, Ly::LD>(ag, vg, W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
+          else bcast_product<D, Ly::LD, HW>(ag, vg, W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
         }
 #pragma unroll
         for (int a = 0; a < D; ++a) acc[s][1 + a] = ag[a];
@@ -687,7 +764,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
 #pragma unroll
         for (int t = 0; t <= s; ++t) {
           if (fold) bcast_fold_fwd<D1>(acc[s], Bown[t], W.Linv, lane);
-          else bcast_product<D1, Ly::LD>(acc[s], Bown[t], W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
+          else bcast_product<D1, Ly::LD, HW>(acc[s], Bown[t], W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
         }
     }
   } else {
@@ -740,7 +817,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
   // ---- 3. per-lane products and wave reductions
   if (do_val) {   // [|v|² = kx'K⁻¹kx, μ = kx·c (base parts), E_r·kx (r < nf)]: 2 + nf values
     static_assert(2 + FMAX <= 8, "value reduction: one chunk");
-    wave_reduce_n<1>([&](int t) {
+    wave_reduce_n<HW, 1>([&](int t) {
       double s_ = 0.0;
 #pragma unroll
       for (int s = 0; s < RPL; ++s) {
@@ -772,11 +849,11 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
         }
         v[q] = s_;
       }
-      wave_reduce<16>(v, red + Ly::R_G + 16 * ch, lane);
+      hw_reduce<HW, 16>(v, red + Ly::R_G + 16 * ch, lane);
     }
     // ∇μ and fantasy cross products for the gradient columns
     // (fantasy rows ≥ nf carry nothing: D·(1 + nf) values)
-    wave_reduce_n<Ly::NMFC>([&](int t) {
+    wave_reduce_n<HW, Ly::NMFC>([&](int t) {
       double s_ = 0.0;
       if (t < Ly::NMF) {
         const int grp = t / D, a = t % D;  // grp 0: c ; grp r+1: E_r
@@ -834,13 +911,13 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
   {
     const int ncol = D;
     // entry t = (r, c) per lane; d > 10 has more entries than lanes: lane, lane + 64, …
-    for (int t = lane; t < (FMAX * D <= WAVE ? WAVE : FMAX * D); t += WAVE) {
+    for (int t = lane; t < (FMAX * D <= Ly::LANES ? Ly::LANES : FMAX * D); t += Ly::LANES) {
       if (t >= nf * ncol) break;
       const int r = t / ncol, c = 1 + t % ncol;
       double y = red[Ly::R_MF + D + r * D + (c - 1)];
       for (int q = 0; q <= r; ++q) y = fma(U[Ly::U_DINV + r * FMAX + q], B[(Ly::FR0 + q) * BS + c], y);
       U[Ly::U_YFV + r * D1 + c] = y;
-      if constexpr (FMAX * D <= WAVE) break;
+      if constexpr (FMAX * D <= Ly::LANES) break;
     }
   }
   wave_sync();
@@ -861,7 +938,11 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
       for (int r = 0; r < nf; ++r) mu = fma(U[Ly::U_CF + (S + 1) * FMAX + r], B[(Ly::FR0 + r) * BS + c], mu);
       U[Ly::U_GMU + c - 1] = mu;
     };
-    if constexpr (Ly::NG <= 49) {   // d ≤ 8: Gram entries on lanes 1..NG-1, ∇μ on lanes 49..48+d
+    if constexpr (HW == 2) {        // half-wave (d ≤ 4): Gram on lanes 1..NG-1, ∇μ on lanes 16..15+d
+      static_assert(Ly::NG <= 16 && 16 + D <= 32, "half-wave Gram placement");
+      if (lane > 0 && lane < Ly::NG) gram_entry(lane);
+      if (lane >= 16 && lane < 16 + D) gmu_entry(lane - 15);
+    } else if constexpr (Ly::NG <= 49) {   // d ≤ 8: Gram entries on lanes 1..NG-1, ∇μ on lanes 49..48+d
       if (lane > 0 && lane < Ly::NG) gram_entry(lane);
       if (lane >= 49 && lane < 48 + D1) gmu_entry(lane - 48);
     } else {                        // wider: both as lane-strided loops
@@ -945,7 +1026,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
     // the Newton iteration's P_GRAD decision (newton below): g = −∇α, stop when stationary
     if (lane < D) U[Ly::U_NG + lane] = -U[Ly::U_GAL + lane];
     wave_sync();
-    if (!newton_pg_ok<D, RPL>(W, kp)) return 0;
+    if (!newton_pg_ok<D, RPL, HW>(W, kp)) return 0;
     STAMP(W, 12);
   }
   } else {   // EV_BACK: resume at the point of the preceding GRAD evaluation
@@ -974,7 +1055,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
       // lane i (row slot s) reads L0⁻¹[64t+k][64s+i] at blk(t,s)·BLK + i·LD + k for block rows
       // t = s..RPL-1; rows k of Y are broadcast from register slot t
       auto nrows = [&](int t) { const int n = N - WAVE * t; return n < WAVE ? n : WAVE; };
-      const bool fold = FOLD && Ly::SQ && N > 48;
+      const bool fold = FOLD && Ly::SQ && HW == 1 && N > 48;
 #pragma unroll
       for (int s = 0; s < RPL; ++s) {
         if (rich) {
@@ -984,7 +1065,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
 #pragma unroll
           for (int t = s; t < RPL; ++t) {
             if (fold) bcast_fold_bwd<D1>(a7, acc[t], W.Linv, lane);
-            else bcast_product<D1, 1>(a7, acc[t], W.Linv + Ly::blk(t, s) * Ly::BLK + lane * Ly::LD, nrows(t));
+            else bcast_product<D1, 1, HW>(a7, acc[t], W.Linv + Ly::blk(t, s) * Ly::BLK + lane * Ly::LD, nrows(t));
           }
           wv[s] = a7[0];
 #pragma unroll
@@ -995,7 +1076,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
           for (int t = s; t < RPL; ++t) {
             const double v1[1] = {acc[t][0]};
             if (fold) bcast_fold_bwd<1>(a1, v1, W.Linv, lane);
-            else bcast_product<1, 1>(a1, v1, W.Linv + Ly::blk(t, s) * Ly::BLK + lane * Ly::LD, nrows(t));
+            else bcast_product<1, 1, HW>(a1, v1, W.Linv + Ly::blk(t, s) * Ly::BLK + lane * Ly::LD, nrows(t));
           }
           wv[s] = a1[0];
         }
@@ -1051,13 +1132,13 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
   // w_f[q] = Σ_{r ≥ q} Dinv[r][q] Yf[r][0]  (and P_f)
   {
     const int ncol = rich ? D1 : 1;
-    for (int e = lane; e < (FMAX * D1 <= WAVE ? WAVE : FMAX * D1); e += WAVE) {   // d > 9: lane-strided
+    for (int e = lane; e < (FMAX * D1 <= Ly::LANES ? Ly::LANES : FMAX * D1); e += Ly::LANES) {   // d > 9: lane-strided
       if (e >= nf * ncol) break;
       const int q = e / ncol, c = e % ncol;
       double t = 0.0;
       for (int r = q; r < nf; ++r) t = fma(U[Ly::U_DINV + r * FMAX + q], U[Ly::U_YFV + r * D1 + c], t);
       if (c == 0) U[Ly::U_WF + q] = t; else U[Ly::U_PF + q * D + c - 1] = t;
-      if constexpr (FMAX * D1 <= WAVE) break;
+      if constexpr (FMAX * D1 <= Ly::LANES) break;
     }
   }
   if (mode == EV_DRAW) { wave_sync(); STAMP(W, 5); return 0; }
@@ -1100,18 +1181,18 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
       double vv[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) vv[q] = hval(16 * ch + q);
-      wave_reduce<16>(vv, red + 16 * ch, lane);
+      hw_reduce<HW, 16>(vv, red + 16 * ch, lane);
     }
     if constexpr (HFULL < Ly::NHC) {
       double vv[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) vv[q] = hval(16 * HFULL + q);
-      wave_reduce<8>(vv, red + 16 * HFULL, lane);
+      hw_reduce<HW, 8>(vv, red + 16 * HFULL, lane);
     }
   }
   wave_sync();
   STAMP(W, 6);
-  for (int he = lane; he < (Ly::NH <= WAVE ? WAVE : Ly::NH); he += WAVE) {   // d > 10: lane-strided
+  for (int he = lane; he < (Ly::NH <= Ly::LANES ? Ly::LANES : Ly::NH); he += Ly::LANES) {   // d > 10: lane-strided
     if (he >= Ly::NH) break;
     int a = 0, rem = he;
 #pragma unroll
@@ -1138,7 +1219,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
     }
     U[Ly::U_H + a * D + b] = hv;
     U[Ly::U_H + b * D + a] = hv;
-    if constexpr (Ly::NH <= WAVE) break;
+    if constexpr (Ly::NH <= Ly::LANES) break;
   }
   wave_sync();
   STAMP(W, 7);
@@ -1149,10 +1230,10 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL>& W, const KParams& kp, i
 // condition!(fs, x, y) -- radial_basis_surrogates.jl:431-441, after an EV_DRAW eval at x
 // on surface S = nf-1.  Appends the inverse-factor row and the new coefficient vector.
 // ================================================================================
-template <int D, int RPL>
-__device__ __forceinline__ int condition(WaveCtx<D, RPL>& W, const KParams& kp, int S, double yv, const double* gy,
-                         const LaneRes<D, RPL>& lr) {
-  using Ly = Lay<D, RPL>;
+template <int D, int RPL, int HW>
+__device__ __forceinline__ int condition(WaveCtx<D, RPL, HW>& W, const KParams& kp, int S, double yv, const double* gy,
+                         const LaneRes<D, RPL, HW>& lr) {
+  using Ly = Lay<D, RPL, HW>;
   constexpr int NR = Ly::NR;
   double* U = W.U;
   const int lane = W.ln();
@@ -1166,8 +1247,8 @@ __device__ __forceinline__ int condition(WaveCtx<D, RPL>& W, const KParams& kp, 
 #pragma unroll
   for (int s = 0; s < RPL; ++s) {
     const int i = lane + WAVE * s;
-    W.E[(long long)nf * NR + i] = W.rowv(kp, s) ? -lr.w[s] * inv : 0.0;
-    W.C[(long long)(S + 2) * NR + i] = W.rowv(kp, s) ? (lr.cb[s] - gam * lr.w[s]) : 0.0;
+    W.E[(long long)nf * Ly::NRL + i] = W.rowv(kp, s) ? -lr.w[s] * inv : 0.0;
+    W.C[(long long)(S + 2) * Ly::NRL + i] = W.rowv(kp, s) ? (lr.cb[s] - gam * lr.w[s]) : 0.0;
   }
   wave_sync();
   if (lane < nf) {
@@ -1195,9 +1276,9 @@ __device__ __forceinline__ int condition(WaveCtx<D, RPL>& W, const KParams& kp, 
 
 // gp_draw with gradient (r_b_s.jl:588-611): [y;∇y] = [μ;∇μ] + chol(Dk(0) − G)·z.
 // Every lane computes the (d+1)² Cholesky redundantly (wave-uniform registers).
-template <int D, int RPL>
-__device__ __forceinline__ int draw(WaveCtx<D, RPL>& W, const KParams& kp, const double* z, double& yv, double* gy) {
-  using Ly = Lay<D, RPL>;
+template <int D, int RPL, int HW>
+__device__ __forceinline__ int draw(WaveCtx<D, RPL, HW>& W, const KParams& kp, const double* z, double& yv, double* gy) {
+  using Ly = Lay<D, RPL, HW>;
   constexpr int D1 = Ly::D1;
   const double* U = W.U;
   double Lc[D1 * (D1 + 1) / 2];
@@ -1277,17 +1358,17 @@ __device__ __forceinline__ bool chol_packed(double (&A)[D * (D + 1) / 2], double
 // i.e. some free coordinate's |g_a| exceeds g_tol (NaN components count in neither form).  Lane
 // a < D tests coordinate a; the free set (bit a: coordinate a free, i.e. not at a bound with the
 // gradient pushing out of the box) is kept in U_SC + SC_FREE for the direction that follows.
-template <int D, int RPL>
-__device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL>& W, const KParams& kp) {
-  using Ly = Lay<D, RPL>;
+template <int D, int RPL, int HW>
+__device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL, HW>& W, const KParams& kp) {
+  using Ly = Lay<D, RPL, HW>;
   const double* U = W.U;
   const int lane = W.ln();
   const int a = lane < D ? lane : 0;
   const double xs = U[Ly::U_NX + a], gs = U[Ly::U_NG + a], lb = U[Ly::U_LB + a], ub = U[Ly::U_UB + a];
   const bool act = ((xs <= lb) & (gs > 0.0)) | ((xs >= ub) & (gs < 0.0));
   const bool fr = (lane < D) & !act;
-  const unsigned long long fm = __ballot(fr);
-  const unsigned long long big = __ballot(fr & (fabs(gs) > KCV(GTOL)));
+  const unsigned long long fm = hw_ballot<HW>(fr, W.half);
+  const unsigned long long big = hw_ballot<HW>(fr & (fabs(gs) > KCV(GTOL)), W.half);
   if (lane == 0) W.U[Ly::U_SC + SC_FREE] = (double)(unsigned)fm;
   return big != 0ull;
 }
@@ -1301,9 +1382,9 @@ __device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL>& W, const KParams& 
 // shifted matrix; the shift is formed by every lane from A0 alone), and p comes from lane 0 when
 // A0 factored, else from lane 32: the same values as the sequential retry, in the time of one
 // factorisation (the retry is taken at ~80-90 % of C3's directions).
-template <int D, int RPL>
-__device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KParams& kp) {
-  using Ly = Lay<D, RPL>;
+template <int D, int RPL, int HW>
+__device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL, HW>& W, const KParams& kp) {
+  using Ly = Lay<D, RPL, HW>;
   constexpr int NH = D * (D + 1) / 2;
   double* U = W.U;
   const int lane = W.ln();
@@ -1338,7 +1419,8 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
     hmax = fr[i] ? fmax(hmax, fabs(hii)) : hmax;
   }
   tau += 1e-8 * (1.0 + hmax);
-  const bool shifted = lane >= WAVE / 2;
+  constexpr int SPLIT = Lay<D, RPL, HW>::LANES / 2;   // the lanes that factor the shifted matrix
+  const bool shifted = lane >= SPLIT;
   double A[NH], idg[D];
 #pragma unroll
   for (int t = 0; t < NH; ++t) A[t] = A0[t];
@@ -1349,8 +1431,8 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
     idg[i] = 0.0;
   }
   const bool okl = chol_packed<D>(A, idg);
-  const bool ok0 = __builtin_amdgcn_readlane((int)okl, 0) != 0;
-  const bool ok1 = __builtin_amdgcn_readlane((int)okl, WAVE / 2) != 0;
+  const bool ok0 = hw_readlane_i<HW>((int)okl, 0, W.half) != 0;
+  const bool ok1 = hw_readlane_i<HW>((int)okl, SPLIT, W.half) != 0;
   STAMP(W, 13);
 #ifdef MRBO_STAMPS
   if (!ok0) stamp_count(W, STAMP_RETRY, 1);   // Gershgorin retries (taken at ~80 % of C3's Newton directions)
@@ -1386,7 +1468,7 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
   const double box = KCV(BOX);
   const double sc = (pn > box) ? box / pn : 1.0;
   wave_sync();
-  if (lane == (ok0 ? 0 : WAVE / 2)) {
+  if (lane == (ok0 ? 0 : SPLIT)) {
 #pragma unroll
     for (int a = 0; a < D; ++a) U[Ly::U_NP + a] = (pn > box) ? p[a] * sc : p[a];
   }
@@ -1398,9 +1480,9 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL>& W, const KPara
 // x_t = clamp(x + t p) -> U_X ; returns gᵀ(x_t - x).  Lane a < D computes coordinate a (its own
 // LDS loads and clamp, one store); the inner product is then summed in coordinate order from the
 // lanes' terms by readlane -- the same fused multiply-adds in the same order as a lane-uniform loop.
-template <int D, int RPL>
-__device__ __forceinline__ double newton_trial_point(WaveCtx<D, RPL>& W, double t) {
-  using Ly = Lay<D, RPL>;
+template <int D, int RPL, int HW>
+__device__ __forceinline__ double newton_trial_point(WaveCtx<D, RPL, HW>& W, double t) {
+  using Ly = Lay<D, RPL, HW>;
   double* U = W.U;
   const int lane = W.ln();
   const int a = lane < D ? lane : 0;
@@ -1411,7 +1493,7 @@ __device__ __forceinline__ double newton_trial_point(WaveCtx<D, RPL>& W, double 
   if (lane < D) U[Ly::U_X + lane] = xt;
   double dec = 0.0;
 #pragma unroll
-  for (int b = 0; b < D; ++b) dec = fma(readlane_d(ga, b), readlane_d(da, b), dec);
+  for (int b = 0; b < D; ++b) dec = fma(hw_readlane_d<HW>(ga, b, W.half), hw_readlane_d<HW>(da, b, W.half), dec);
   wave_sync();
   return dec;
 }
@@ -1422,9 +1504,9 @@ __device__ __forceinline__ double newton_trial_point(WaveCtx<D, RPL>& W, double 
 //   |∂_a σ| = |kxᵀK⁻¹∂_a kx| / σ ≤ √(kxᵀK⁻¹kx · ∂_a kxᵀK⁻¹∂_a kx) / σ ≤ √(ψ(0)(−ψ''(0))) / σ
 // (posterior variances of f and ∂_a f are ≥ 0).  A factor 4 covers rounding.  gμ = gσ = 0
 // (σ < σtol, or Φ and φ underflowed) makes ∇α zero or NaN, which also stops the iteration.
-template <int D, int RPL>
-__device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const KParams& kp) {
-  using Ly = Lay<D, RPL>;
+template <int D, int RPL, int HW>
+__device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL, HW>& W, const KParams& kp) {
+  using Ly = Lay<D, RPL, HW>;
   const double* U = W.U;
   const double gm = U[Ly::U_SC + SC_GMU], gs = U[Ly::U_SC + SC_GSIG];
   const double cabs = U[Ly::U_SC + SC_CABS], isig = U[Ly::U_SC + SC_ISIG];   // unconditional loads
@@ -1450,10 +1532,10 @@ __device__ __forceinline__ bool grad_certified(const WaveCtx<D, RPL>& W, const K
 // row (G12) and fantasy row (U_HF) is still in LDS -- the same bits a new radial evaluation
 // would give; only ρ is recomputed.
 // With a cost model (f = α/c, araw = α at x) every bound B on |∂α| becomes B/c + |α| max|∇c|/c².
-template <int D, int RPL, bool ROWS_KEPT = false>
-__device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParams& kp, int S, double gm, double gs,
+template <int D, int RPL, int HW, bool ROWS_KEPT = false>
+__device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL, HW>& W, const KParams& kp, int S, double gm, double gs,
                                                 double sig, double isig, double araw = 0.0) {
-  using Ly = Lay<D, RPL>;
+  using Ly = Lay<D, RPL, HW>;
   constexpr int NR = Ly::NR;
   const double* U = W.U;
   const int lane = W.ln();
@@ -1489,7 +1571,7 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParam
     double psi, g1, g2;
     if constexpr (ROWS_KEPT) g1 = W.G12[3 * (lane + WAVE * s)];
     else rad_eval(W.rad, rho2, psi, g1, g2);
-    const double cb = W.C[(long long)(S + 1) * NR + lane + WAVE * s];
+    const double cb = W.C[(long long)(S + 1) * Ly::NRL + lane + WAVE * s];
     v[0] += W.rowv(kp, s) ? fabs(cb) * fabs(g1) * fast_sqrt0(rho2) : 0.0;
   }
   if (lane < nf) {
@@ -1501,7 +1583,7 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParam
     else rad_eval(W.rad, rho2, psi, g1, g2);
     v[0] += fabs(U[Ly::U_CF + (S + 1) * FMAX + lane]) * fabs(g1) * fast_sqrt0(rho2);
   }
-  const double bmu = wave_allreduce1(v[0]);
+  const double bmu = hw_allreduce1<HW>(v[0]);
   return (fabs(gm) * bmu + bsig) * isc + add <= thr;
 }
 
@@ -1512,11 +1594,11 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL>& W, const KParam
 // step is taken.  Values and gradients are bit-identical to a FULL evaluation at the same
 // point (same code path), so the iterates are those of the eager iteration, and the work
 // counts equal the oracle's (rbo_oracle.c newton_solve).  Result: x in U_NX, f returned.
-template <int D, int RPL>
-__device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, int S, int k, Counters& nevals,
-                                         int& st, LaneRes<D, RPL>& lr, double f0, bool have_f0, double gm0 = 0.0,
+template <int D, int RPL, int HW>
+__device__ __forceinline__ double newton(WaveCtx<D, RPL, HW>& W, const KParams& kp, int S, int k, Counters& nevals,
+                                         int& st, LaneRes<D, RPL, HW>& lr, double f0, bool have_f0, double gm0 = 0.0,
                                          double gs0 = 0.0, double sig0 = 0.0, double a0 = 0.0) {
-  using Ly = Lay<D, RPL>;
+  using Ly = Lay<D, RPL, HW>;
   double* U = W.U;
   const int lane = W.ln();
   enum { P_VAL = 0, P_TRIAL = 1, P_GRAD = 2, P_HESS = 3 };
@@ -1533,7 +1615,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
   wave_sync();
   // a batched start whose cheap certificate failed: the tight one at x_start (gμ, gσ, σ of the
   // batched value) before any gradient work
-  if (have_f0 && kp.gcert_sig > 0.0 && tight_certified<D, RPL>(W, kp, S, gm0, gs0, sig0, 1.0 / sig0, a0)) {
+  if (have_f0 && kp.gcert_sig > 0.0 && tight_certified<D, RPL, HW>(W, kp, S, gm0, gs0, sig0, 1.0 / sig0, a0)) {
     wave_sync();
     return f0;
   }
@@ -1544,7 +1626,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
   int phase = have_f0 ? P_GRAD : P_VAL, mode = have_f0 ? (Ly::SQ ? EV_GSTART : EV_GRAD) : EV_VALUE, it = 0, ls = 0;
   double f = have_f0 ? f0 : 0.0, ft = 0.0, t = 1.0, dec = 0.0;
   for (;;) {
-    const int back = evaluate<D, RPL>(W, kp, S, mode, lr, k, FUSE_BACK && phase == P_GRAD);
+    const int back = evaluate<D, RPL, HW>(W, kp, S, mode, lr, k, FUSE_BACK && phase == P_GRAD);
     if (mode == EV_VALUE) ++nevals.value;
     else if (mode == EV_GRADC || mode == EV_GRAD || mode == EV_GSTART) ++nevals.grad;
     else ++nevals.hess;
@@ -1555,12 +1637,12 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
     }
     if (phase == P_HESS) {                 // Hα at x ready: step
       STAMP(W, 12);
-      const bool go = newton_direction<D, RPL>(W, kp);
+      const bool go = newton_direction<D, RPL, HW>(W, kp);
       STAMP(W, 13);
       if (!go) break;
       t = 1.0;
       ls = 0;
-      dec = newton_trial_point<D, RPL>(W, t);
+      dec = newton_trial_point<D, RPL, HW>(W, t);
       STAMP(W, 14);
       phase = P_TRIAL;
       mode = EV_VALUE;
@@ -1569,7 +1651,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
     if (phase == P_GRAD) {                 // ∇α at x ready
       if (lane < D) U[Ly::U_NG + lane] = -U[Ly::U_GAL + lane];
       wave_sync();
-      if (!newton_pg_ok<D, RPL>(W, kp)) break;     // stationary
+      if (!newton_pg_ok<D, RPL, HW>(W, kp)) break;     // stationary
       STAMP(W, 21);
       phase = P_HESS;
       mode = EV_BACK;
@@ -1584,7 +1666,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
         ++ls;
         if (ls >= kp.max_ls) break;                // no acceptable step
         t *= 0.5;
-        dec = newton_trial_point<D, RPL>(W, t);
+        dec = newton_trial_point<D, RPL, HW>(W, t);
         continue;
       }
       // accept x_t: lane a < D moves its coordinate; ‖Δx‖∞ from the lanes' |Δx_a| (max: order-free)
@@ -1593,7 +1675,7 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
       const double dxa = fabs(xt - U[Ly::U_NX + ca]);
       double dx = 0.0;
 #pragma unroll
-      for (int a = 0; a < D; ++a) dx = fmax(dx, readlane_d(dxa, a));
+      for (int a = 0; a < D; ++a) dx = fmax(dx, hw_readlane_d<HW>(dxa, a, W.half));
       const double df = fabs(ft - f);
       wave_sync();
       if (lane < D) U[Ly::U_NX + lane] = xt;
@@ -1608,9 +1690,9 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
     // decision point at x = U_NX (= U_X), whose VALUE evaluation is in U
     if (it >= kp.max_iters) break;
     if (f != f) break;
-    if (grad_certified<D, RPL>(W, kp)) break;     // ‖∇α‖ ≤ g_tol guaranteed: stationary
+    if (grad_certified<D, RPL, HW>(W, kp)) break;     // ‖∇α‖ ≤ g_tol guaranteed: stationary
     if (kp.gcert_sig > 0.0 &&
-        tight_certified<D, RPL, true>(W, kp, S, U[Ly::U_SC + SC_GMU], U[Ly::U_SC + SC_GSIG], U[Ly::U_SC + SC_SIG],
+        tight_certified<D, RPL, HW, true>(W, kp, S, U[Ly::U_SC + SC_GMU], U[Ly::U_SC + SC_GSIG], U[Ly::U_SC + SC_SIG],
                                       U[Ly::U_SC + SC_ISIG], kp.cost ? U[Ly::U_SC + SC_ARAW] : 0.0))
       break;
     STAMP(W, 20);
@@ -1626,11 +1708,11 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL>& W, const KParams& kp, 
 //   kxb[i][k] = ψ(|x_k − X_i|) (0 on padded rows);  per start, Y = L0⁻¹[kx, ∇kx](x_k):
 //   Y0 → this workgroup's global slice kp.ytab, base Gram YᵀY → gtab (LDS)
 // The per-wave areas (not yet initialised) serve as scratch for the squares.
-template <int D, int RPL>
+template <int D, int RPL, int HW>
 __device__ __forceinline__ void stage_start_tables(const KParams& kp, double* smem) {
-  using Ly = Lay<D, RPL>;
+  using Ly = Lay<D, RPL, HW>;
   constexpr int NR = Ly::NR;
-  const WgTables<D, RPL> tb(kp);
+  const WgTables<D, RPL, HW> tb(kp);
   const int ns = kp.nstarts;
   const double* xs = smem + tb.xs;
   double* kxb = smem + tb.kxb;
@@ -1714,12 +1796,12 @@ __device__ __forceinline__ void stage_start_tables(const KParams& kp, double* sm
 //   μ_k = c_S·kxb[:,k] + Σ_r c_r ψ(x_k, X_r),  Yf_r = E_r·kxb[:,k] + Σ_{q≤r} Dinv[r][q] ψ(x_k, X_q),
 //   σ_k² = ψ(0) − gtab[k][0] − Σ_r Yf_r²,  then α and the gradient certificate per lane.
 // Replaces nstarts value evaluations (and their wave-redundant EI) by one pass.
-template <int D, int RPL>
-__device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KParams& kp, int S, double& f_lane,
+template <int D, int RPL, int HW>
+__device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL, HW>& W, const KParams& kp, int S, double& f_lane,
                                                    double& gm_lane, double& gs_lane, double& sig_lane,
                                                    double& a_lane, unsigned long long& stopmask,
                                                    unsigned long long& xnanmask, bool& varneg) {
-  using Ly = Lay<D, RPL>;
+  using Ly = Lay<D, RPL, HW>;
   constexpr int NR = Ly::NR;
   const double* U = W.U;
   const int lane = W.ln();
@@ -1729,7 +1811,7 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   // even data rows, the upper half the odd ones, one permlane32 swap per value adds the halves,
   // and each half evaluates every other fantasy radial function.  Both halves then hold the
   // same per-start values; the ballots below read the lower half.
-  const bool split = ns <= 32;
+  const bool split = HW == 1 && ns <= 32;   // half-wave mode: each half takes every start itself
 #else
   const bool split = false;
 #endif
@@ -1743,7 +1825,7 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   double amu = 0.0, ae[FMAX];
 #pragma unroll
   for (int r = 0; r < FMAX; ++r) ae[r] = 0.0;
-  const double* cS = W.C + (long long)(S + 1) * NR;
+  const double* cS = W.C + (long long)(S + 1) * Ly::NRL;
   // all FMAX rows unconditionally (rows ≥ nf hold finite stale values, masked below): a load
   // under a condition would become a branch with a full LDS round trip per row.  Rows N..NR-1
   // of the tables are zero.
@@ -1759,7 +1841,7 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
       const int i = lane + WAVE * s2;
       cv[s2] = cS[i];
 #pragma unroll
-      for (int r = 0; r < FMAX; ++r) ev[s2][r] = W.E[(long long)r * NR + i];
+      for (int r = 0; r < FMAX; ++r) ev[s2][r] = W.E[(long long)r * Ly::NRL + i];
     }
     double* sums = W.SUMS;   // [ns][8]
     // the kernel-row table entries of the next pair of starts are loaded while this pair is
@@ -1812,7 +1894,7 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
       const double kv = W.KXB[i * ns + k];
       amu = fma(cS[i], kv, amu);
 #pragma unroll
-      for (int r = 0; r < FMAX; ++r) ae[r] = fma(W.E[(long long)r * NR + i], kv, ae[r]);
+      for (int r = 0; r < FMAX; ++r) ae[r] = fma(W.E[(long long)r * Ly::NRL + i], kv, ae[r]);
     }
     amu = swap_fold<32>(amu, amu);
 #pragma unroll
@@ -1823,7 +1905,7 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
       const double kv = W.KXB[i * ns + k];
       amu = fma(cS[i], kv, amu);
 #pragma unroll
-      for (int r = 0; r < FMAX; ++r) ae[r] = fma(W.E[(long long)r * NR + i], kv, ae[r]);
+      for (int r = 0; r < FMAX; ++r) ae[r] = fma(W.E[(long long)r * Ly::NRL + i], kv, ae[r]);
     }
   }
   double pf[FMAX];
@@ -1901,18 +1983,18 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL>& W, const KPa
   bool xn = false;
 #pragma unroll
   for (int a = 0; a < D; ++a) xn = xn || (x[a] != x[a]);
-  stopmask = __ballot(act && stop);
-  xnanmask = __ballot(act && xn);
-  varneg = __ballot(act && var < 0.0) != 0;
+  stopmask = hw_ballot<HW>(act && stop, W.half);
+  xnanmask = hw_ballot<HW>(act && xn, W.half);
+  varneg = hw_ballot<HW>(act && var < 0.0, W.half) != 0;
 }
 
 // multistart_base_solve!(fs, …) rbf_optim.jl:68-101 -> U[U_XB], over the starts k0 ≤ k < k1.
 // kp.base_solve: one start per launch item, whose (minimizer, minimum) is the output -- the
 // candidate list multistart_base_solve!(s::Surrogate, …) (:103-135) takes its findmin over.
-template <int D, int RPL>
-__device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp, int S, Counters& nevals,
-                                          LaneRes<D, RPL>& lr, int k0, int k1) {
-  using Ly = Lay<D, RPL>;
+template <int D, int RPL, int HW>
+__device__ __forceinline__ int multistart(WaveCtx<D, RPL, HW>& W, const KParams& kp, int S, Counters& nevals,
+                                          LaneRes<D, RPL, HW>& lr, int k0, int k1) {
+  using Ly = Lay<D, RPL, HW>;
   double* U = W.U;
   const int lane = W.ln();
   int st = 0;
@@ -1922,8 +2004,8 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
   {   // Σ|c| of surface S (base + fantasy coefficients) for the gradient certificate
     double v[1] = {0.0};
 #pragma unroll
-    for (int s = 0; s < RPL; ++s) v[0] += fabs(W.C[(long long)(S + 1) * Ly::NR + lane + WAVE * s]);
-    double cabs = wave_allreduce1(v[0]);
+    for (int s = 0; s < RPL; ++s) v[0] += fabs(W.C[(long long)(S + 1) * Ly::NRL + lane + WAVE * s]);
+    double cabs = hw_allreduce1<HW>(v[0]);
     for (int r = 0; r <= S; ++r) cabs += fabs(U[Ly::U_CF + (S + 1) * FMAX + r]);
     if (lane == 0) U[Ly::U_SC + SC_CABS] = cabs;
     wave_sync();
@@ -1933,7 +2015,7 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
   if (kp.batch) {
     bool varneg = false;
     STAMP(W, 16);
-    batch_start_values<D, RPL>(W, kp, S, f_lane, gm_lane, gs_lane, sig_lane, a_lane, stopmask, xnanmask, varneg);
+    batch_start_values<D, RPL, HW>(W, kp, S, f_lane, gm_lane, gs_lane, sig_lane, a_lane, stopmask, xnanmask, varneg);
     STAMP(W, 15);
     nevals.value += kp.nstarts;
     if (varneg) st |= 1;
@@ -1942,10 +2024,11 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
   // starts that need a Newton iteration, in index order (all of them without kp.batch)
   for (int k = k0; k < k1; ++k) {
     if ((stopmask >> k) & 1ull) continue;
-    const double fo = kp.batch ? newton<D, RPL>(W, kp, S, k, nevals, st, lr, readlane_d(f_lane, k), true,
-                                                readlane_d(gm_lane, k), readlane_d(gs_lane, k), readlane_d(sig_lane, k),
-                                                kp.cost ? readlane_d(a_lane, k) : 0.0)
-                               : newton<D, RPL>(W, kp, S, k, nevals, st, lr, 0.0, false);
+    const double fo = kp.batch ? newton<D, RPL, HW>(W, kp, S, k, nevals, st, lr, hw_lane_d<HW>(f_lane, k, W.half), true,
+                                                hw_lane_d<HW>(gm_lane, k, W.half), hw_lane_d<HW>(gs_lane, k, W.half),
+                                                hw_lane_d<HW>(sig_lane, k, W.half),
+                                                kp.cost ? hw_lane_d<HW>(a_lane, k, W.half) : 0.0)
+                               : newton<D, RPL, HW>(W, kp, S, k, nevals, st, lr, 0.0, false);
     if (kp.base_solve) {   // (Optim.minimizer(res), minimum(res)) of base_solve, rbf_optim.jl:127-128
       if (lane < D) kp.policy[(long long)k * D + lane] = U[Ly::U_NX + lane];
       if (lane == 0) kp.values[k] = fo;
@@ -1972,7 +2055,7 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
     // semantics (rbf_optim.jl:96-98): the first NaN f wins, else the first minimum; NaN x dropped
     const int ns = kp.nstarts;
     const bool mine = lane < ns && ((stopmask >> lane) & 1ull) && !((xnanmask >> lane) & 1ull);
-    const unsigned long long nanm = __ballot(mine && f_lane != f_lane);
+    const unsigned long long nanm = hw_ballot<HW>(mine && f_lane != f_lane, W.half);
     int win = -1;
     bool win_nan = false;
     if (nanm) {
@@ -1981,8 +2064,8 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
     } else if (!best_nan) {
       double m = mine ? f_lane : INFINITY;
 #pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) m = fmin(m, __shfl_xor(m, o, WAVE));
-      const unsigned long long eq = __ballot(mine && f_lane == m);
+      for (int o = Lay<D, RPL, HW>::LANES / 2; o >= 1; o >>= 1) m = fmin(m, __shfl_xor(m, o, WAVE));
+      const unsigned long long eq = hw_ballot<HW>(mine && f_lane == m, W.half);
       if (eq) {
         const int km = __builtin_ctzll(eq);
         if (best < 0 || m < bestf || (m == bestf && km < best)) win = km;
@@ -2009,10 +2092,10 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL>& W, const KParams& kp,
 // Reference: SpatialPerturbationSurrogate r_b_s.jl:652-694, DataPerturbation :711-757,
 // solve_dual_x rollout.jl:173-186, solve_dual_y :135-145, gather_g :199-215.
 // ================================================================================
-template <int D, int RPL>
-__device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& kp, int S, int q, int i_pol,
-                             const LaneRes<D, RPL>& lr) {
-  using Ly = Lay<D, RPL>;
+template <int D, int RPL, int HW>
+__device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL, HW>& W, const KParams& kp, int S, int q, int i_pol,
+                             const LaneRes<D, RPL, HW>& lr) {
+  using Ly = Lay<D, RPL, HW>;
   constexpr int NR = Ly::NR;
   double* U = W.U;
   double* red = W.red;
@@ -2055,7 +2138,7 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL>& W, const KParams& 
       }
       v[qq] = s_;
     }
-    wave_reduce<16>(v, red + 16 * ch, lane);
+    hw_reduce<HW, 16>(v, red + 16 * ch, lane);
   }
   wave_sync();
   if (lane > D) { STAMP(W, 9); return; }
@@ -2217,22 +2300,22 @@ __device__ __forceinline__ bool lu_det_solve(double (&A)[D][D], double* b, doubl
 }
 
 // set U_X to fantasy point j and run a RICH eval on surface j-1
-template <int D, int RPL>
-__device__ __forceinline__ void rich_eval_at(WaveCtx<D, RPL>& W, const KParams& kp, int j, LaneRes<D, RPL>& lr) {
-  using Ly = Lay<D, RPL>;
+template <int D, int RPL, int HW>
+__device__ __forceinline__ void rich_eval_at(WaveCtx<D, RPL, HW>& W, const KParams& kp, int j, LaneRes<D, RPL, HW>& lr) {
+  using Ly = Lay<D, RPL, HW>;
   wave_sync();
   const int lane = W.ln();
   if (lane < D) W.U[Ly::U_X + lane] = W.U[Ly::U_XF + j * D + lane];
   wave_sync();
-  evaluate<D, RPL>(W, kp, j - 1, EV_RICH, lr);
+  evaluate<D, RPL, HW>(W, kp, j - 1, EV_RICH, lr);
 }
 
 // ================================================================================
 // One trajectory.
 // ================================================================================
-template <int D, int RPL>
-__device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp, long long tr) {
-  using Ly = Lay<D, RPL>;
+template <int D, int RPL, int HW>
+__device__ __forceinline__ void trajectory(WaveCtx<D, RPL, HW>& W, const KParams& kp, long long tr) {
+  using Ly = Lay<D, RPL, HW>;
   constexpr int D1 = Ly::D1, NR = Ly::NR;
   double* U = W.U;
   const int lane = W.ln();
@@ -2240,7 +2323,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
   const int r = (int)(tr / M), m = (int)(tr % M);
   Counters nevals;
   int st = 0;
-  LaneRes<D, RPL> lr;
+  LaneRes<D, RPL, HW> lr;
 
   // surface -1 = the base surrogate; C[0] = c0
 #pragma unroll
@@ -2265,7 +2348,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
         wave_sync();
       } else {
 #ifndef MRBO_EXP_NO_NEWTON
-        st |= multistart<D, RPL>(W, kp, S, nevals, lr, bsolve ? (int)tr : 0, bsolve ? (int)tr + 1 : kp.nstarts);
+        st |= multistart<D, RPL, HW>(W, kp, S, nevals, lr, bsolve ? (int)tr : 0, bsolve ? (int)tr + 1 : kp.nstarts);
 #endif
         if (bsolve) {   // the start's minimizer and minimum were written by multistart
           if (lane == 0) kp.status[tr] = st & ~8;   // a NaN minimizer is the host's filter, not an error
@@ -2285,7 +2368,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
       }
     }
     if (kp.policy && lane < D) kp.policy[(long long)lane + D * (k + (long long)(h + 1) * (m + (long long)M * r))] = U[Ly::U_X + lane];
-    evaluate<D, RPL>(W, kp, S, EV_DRAW, lr);
+    evaluate<D, RPL, HW>(W, kp, S, EV_DRAW, lr);
     if (U[Ly::U_SC + SC_VAR] < 0.0) { st |= 1; break; }
     if (k == 0 && lane < D) U[Ly::U_GMU0 + lane] = U[Ly::U_GMU + lane];
     double yv, gy[D];
@@ -2301,11 +2384,11 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
       double z[D1];
 #pragma unroll
       for (int a = 0; a < D1; ++a) z[a] = kp.rn[(long long)m + (long long)M * a + (long long)M * D1 * k];
-      st |= draw<D, RPL>(W, kp, z, yv, gy);
+      st |= draw<D, RPL, HW>(W, kp, z, yv, gy);
       if (st) break;
     }
     wave_sync();
-    st |= condition<D, RPL>(W, kp, S, yv, gy, lr);
+    st |= condition<D, RPL, HW>(W, kp, S, yv, gy, lr);
     STAMP(W, 10);
     if (st) break;
   }
@@ -2345,7 +2428,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
     } else {
       grad_zero = false;
       // zero adjoint state
-      for (int q = lane; q < FMAX * D; q += WAVE) { U[Ly::U_ACC + q] = 0.0; U[Ly::U_XBAR + q] = 0.0; }
+      for (int q = lane; q < FMAX * D; q += Ly::LANES) { U[Ly::U_ACC + q] = 0.0; U[Ly::U_XBAR + q] = 0.0; }
       if (lane <= FMAX) U[Ly::U_YBAR + lane] = 0.0;
       wave_sync();
       if (lane == 0) U[Ly::U_YBAR + t] = 1.0;
@@ -2368,7 +2451,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
             for (int a = 0; a < D; ++a) xz = xz && (U[Ly::U_XBAR + (i - 1) * D + a] == 0.0);
             if (xz) continue;   // zero dual: contributes exactly nothing
           }
-          rich_eval_at<D, RPL>(W, kp, i, lr);   // recover_policy_solve(T, i) :114-124
+          rich_eval_at<D, RPL, HW>(W, kp, i, lr);   // recover_policy_solve(T, i) :114-124
           ++nevals.rich;
           if (i == j) {
             double Hm[D][D], xd[D], det;
@@ -2399,7 +2482,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
             wave_sync();
             if (zero) continue;
           }
-          adjoint_pair<D, RPL>(W, kp, i - 1, j - 1, i, lr);
+          adjoint_pair<D, RPL, HW>(W, kp, i - 1, j - 1, i, lr);
           ++nevals.pairs;
           wave_sync();
         }
@@ -2436,19 +2519,21 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL>& W, const KParams& kp
 // launch bounds: 2 waves per SIMD (256 VGPRs each) up to N = 128 at d ≤ 8; the N > 128 layouts
 // and d > 8 run one wave per SIMD, whose 512-entry register file (256 VGPRs + 256 AGPRs) holds the
 // multi-row / wide state (N ≤ 512 and d ≤ 16 compile, with scratch spills: coverage, not speed)
-template <int D, int RPL>
+template <int D, int RPL, int HW = 1>
 struct KBounds {
   static constexpr bool WIDE = (RPL > 2) || (D > 8);
   static constexpr int threads = WIDE ? 256 : 512;
   static constexpr int waves_per_simd = WIDE ? MRBO_WAVES_PER_SIMD_GL : MRBO_WAVES_PER_SIMD;
 };
 
-template <int D, int RPL>
-__device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp, double* smem, int wave_in_block) {
-  using Ly = Lay<D, RPL>;
-  W.lane = threadIdx.x & (WAVE - 1);
-  const WgTables<D, RPL> tb(kp);
-  double* wbase = smem + tb.end + (long long)wave_in_block * Ly::WAVE_LDS;
+template <int D, int RPL, int HW>
+__device__ __forceinline__ void wave_setup(WaveCtx<D, RPL, HW>& W, const KParams& kp, double* smem, int wave_in_block) {
+  using Ly = Lay<D, RPL, HW>;
+  W.lane = threadIdx.x & (Ly::LANES - 1);
+  W.half = HW == 2 ? (int)((threadIdx.x >> 5) & 1) : 0;
+  const WgTables<D, RPL, HW> tb(kp);
+  // one per-trajectory area per half in half-wave mode
+  double* wbase = smem + tb.end + ((long long)wave_in_block * HW + W.half) * Ly::WAVE_LDS;
   W.XS = kp.xs_lds ? smem + tb.xs : kp.xstarts;
   W.KXB = Ly::SQ ? smem + tb.kxb : kp.kxb_g;
   W.GTAB = Ly::SQ ? smem + tb.gtab : kp.gtab_g;
@@ -2466,7 +2551,7 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
   const long long slot = (long long)blockIdx.x * (blockDim.x / WAVE) + wave_in_block;
   if constexpr (Ly::SQ) W.E = W.G12 + Ly::G12;
   else W.E = kp.work + slot * kp.work_stride;
-  W.C = W.E + (long long)FMAX * Ly::NR;
+  W.C = W.E + (long long)FMAX * Ly::NRL;
   W.SUMS = W.E + (long long)(2 * FMAX + 1) * Ly::NR;   // packed layouts only (work_stride covers it)
   W.N = kp.N;
   W.Npad = kp.Npad;
@@ -2488,7 +2573,7 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
 #endif
   }
   // zero this wave's LDS so that padded rows read as zeros
-  for (int q = W.lane; q < Ly::WAVE_LDS; q += WAVE) wbase[q] = 0.0;
+  for (int q = W.lane; q < Ly::WAVE_LDS; q += Ly::LANES) wbase[q] = 0.0;
   wave_sync();
   if (W.lane == 0) {
     double* kc = W.U + Ly::U_KC;
@@ -2514,8 +2599,8 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL>& W, const KParams& kp
 // (every configuration of BASELINE.json).  The other kernels' and rules' code paths fold away,
 // which frees registers in the whole trajectory (VGPR spills 94 -> 33 at d = 6).  SPEC = 0
 // reads both from the launch parameters.
-template <int D, int RPL, int SPEC>
-__global__ void __launch_bounds__((KBounds<D, RPL>::threads), (KBounds<D, RPL>::waves_per_simd)) rollout_kernel(KParams kp_in) {
+template <int D, int RPL, int SPEC, int HW = 1>
+__global__ void __launch_bounds__((KBounds<D, RPL, HW>::threads), (KBounds<D, RPL, HW>::waves_per_simd)) rollout_kernel(KParams kp_in) {
   KParams kp = kp_in;   // a local copy: the fixed fields below propagate as constants
   if constexpr (SPEC == 1) {
     kp.kernel = KERNEL_MATERN52;
@@ -2524,16 +2609,16 @@ __global__ void __launch_bounds__((KBounds<D, RPL>::threads), (KBounds<D, RPL>::
   }
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // stage L0⁻¹ (and the inner-solve start points) once per workgroup (the only block barrier)
-  using Ly = Lay<D, RPL>;
+  using Ly = Lay<D, RPL, HW>;
   for (int q = threadIdx.x; q < (int)Ly::LINV_DOUBLES; q += blockDim.x) smem[q] = kp.Linv[q];
   if (kp.xs_lds)
     for (int q = threadIdx.x; q < kp.nstarts * D; q += blockDim.x) smem[Ly::LINV_DOUBLES + q] = kp.xstarts[q];
   __syncthreads();
   if constexpr (Ly::SQ) {
-    if (kp.batch) stage_start_tables<D, RPL>(kp, smem);
+    if (kp.batch) stage_start_tables<D, RPL, HW>(kp, smem);
   }
-  WaveCtx<D, RPL> W;
-  wave_setup<D, RPL>(W, kp, smem, threadIdx.x / WAVE);
+  WaveCtx<D, RPL, HW> W;
+  wave_setup<D, RPL, HW>(W, kp, smem, threadIdx.x / WAVE);
   wave_sync();
 #ifdef MRBO_STAMPS
   W.tlast = __builtin_amdgcn_s_memtime();
@@ -2565,18 +2650,18 @@ __global__ void __launch_bounds__((KBounds<D, RPL>::threads), (KBounds<D, RPL>::
       }
     }
 #endif
-    tr = __shfl(tr, 0, WAVE);
+    tr = __shfl(tr, 32 * W.half, WAVE);   // HW = 2: each half took its own trajectory
     if (tr >= kp.T) break;
     if (kp.order) {   // caller's schedule (a permutation; an out-of-range entry falls back to tr)
       const long long id = kp.order[tr];
       tr = (id >= 0 && id < kp.T) ? id : tr;
     }
-    trajectory<D, RPL>(W, kp, tr);
+    trajectory<D, RPL, HW>(W, kp, tr);
   }
 #ifdef MRBO_STAMPS
   if (kp.stamps && W.lane == 0)
     for (int k = 0; k < NSTAMP_SLOTS; ++k)
-      atomicAdd(kp.stamps + k, reinterpret_cast<unsigned long long*>(W.U + Lay<D, RPL>::U_STAMP)[k]);
+      atomicAdd(kp.stamps + k, reinterpret_cast<unsigned long long*>(W.U + Lay<D, RPL, HW>::U_STAMP)[k]);
 #endif
 }
 
@@ -2586,9 +2671,9 @@ __global__ void __launch_bounds__((KBounds<D, RPL>::threads), (KBounds<D, RPL>::
 //   gtab_g[k]   = base Gram YᵀY of Y = L0⁻¹[kx, ∇kx](x_k), upper triangle row-major (entry 0 is
 //                 |L0⁻¹kx|², the only entry batch_start_values reads).
 // The forward product walks the packed-by-columns image of L0⁻¹ (column j: rows j..Npad-1).
-template <int D, int RPL>
+template <int D, int RPL, int HW = 1>
 __global__ void __launch_bounds__(WAVE) start_tables_kernel(KParams kp) {
-  using Ly = Lay<D, RPL>;
+  using Ly = Lay<D, RPL, HW>;
   constexpr int NR = Ly::NR, D1 = Ly::D1;
   __shared__ double Bs[NR * D1];
   __shared__ double red[16 * ((Ly::NG + 15) / 16)];
@@ -2658,20 +2743,20 @@ __global__ void __launch_bounds__(WAVE) start_tables_kernel(KParams kp) {
 }
 
 // eval(s, x, θ) on the base surrogate for P points (fixture / primitive parity path)
-template <int D, int RPL>
-__global__ void __launch_bounds__((KBounds<D, RPL>::threads), (KBounds<D, RPL>::waves_per_simd)) eval_base_kernel(KParams kp) {
-  using Ly = Lay<D, RPL>;
+template <int D, int RPL, int HW = 1>
+__global__ void __launch_bounds__((KBounds<D, RPL, HW>::threads), (KBounds<D, RPL, HW>::waves_per_simd)) eval_base_kernel(KParams kp) {
+  using Ly = Lay<D, RPL, HW>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   for (int q = threadIdx.x; q < (int)Ly::LINV_DOUBLES; q += blockDim.x) smem[q] = kp.Linv[q];
   __syncthreads();
-  WaveCtx<D, RPL> W;
-  wave_setup<D, RPL>(W, kp, smem, threadIdx.x / WAVE);
+  WaveCtx<D, RPL, HW> W;
+  wave_setup<D, RPL, HW>(W, kp, smem, threadIdx.x / WAVE);
   const int lane = W.ln();
 #pragma unroll
   for (int s = 0; s < RPL; ++s) W.C[lane + WAVE * s] = kp.c0[lane + WAVE * s];
   if (lane == 0) W.U[Ly::U_FMIN] = kp.fmin_base;
   wave_sync();
-  LaneRes<D, RPL> lr;
+  LaneRes<D, RPL, HW> lr;
   const int stride = 3 + 4 * D + D * D;
   for (;;) {
     long long p = 0;
@@ -2680,7 +2765,7 @@ __global__ void __launch_bounds__((KBounds<D, RPL>::threads), (KBounds<D, RPL>::
     if (p >= kp.T) break;
     if (lane < D) W.U[Ly::U_X + lane] = kp.pts[p * D + lane];
     wave_sync();
-    evaluate<D, RPL>(W, kp, -1, EV_FULL, lr);
+    evaluate<D, RPL, HW>(W, kp, -1, EV_FULL, lr);
     double* o = kp.pts_out + p * stride;
     const double* U = W.U;
     if (lane == 0) { o[0] = U[Ly::U_SC + SC_MU]; o[1] = U[Ly::U_SC + SC_SIG]; o[2] = U[Ly::U_SC + SC_ALPHA]; }

@@ -208,6 +208,7 @@ def run(function_name, output_dir, budget=15, trials=60, starts=16, horizon=0, m
             ell_start = float(sur.ψ.lengthscale)
             initial_best = float(np.min(yinit))
             times, gaps, allocs, regrets, minobs = (np.zeros(budget) for _ in range(5))
+            repeats = np.zeros(budget, dtype=bool)
             for b in range(budget):
                 t0 = time.perf_counter()
                 xnext, _ = rollout_solve(sur, lbs, ubs, horizon, mc_samples, batch_size, starts, sgd_iterations,
@@ -226,7 +227,7 @@ def run(function_name, output_dir, budget=15, trials=60, starts=16, horizon=0, m
                 write_to_csv(os.path.join(directory, f"{acq}_{metric}"), data)
             results[(acq, trial)] = dict(times=times, gaps=gaps, simple_regret=regrets, minimum_observations=minobs,
                                          X=sur.get_active_covariates().copy(), y=sur.get_active_observations().copy(),
-                                         ell_start=ell_start, ell_end=float(sur.ψ.lengthscale))
+                                         ell_start=ell_start, ell_end=float(sur.ψ.lengthscale), repeats=repeats)
     return results
 
 
@@ -236,7 +237,7 @@ MYOPIC_RULES = {"ei": (EI, 0.0), "poi": (POI, 0.0), "lcb": (LCB, 2.0)}   # :151-
 
 def run_myopic(function_name, output_dir, budget=100, trials=60, starts=64, seed=1906, device=0, log=print,
                rules=("ei", "poi", "lcb"), optimize=True, initial_observations=INITIAL_OBSERVATIONS,
-               reuse_surrogate=True, capacity=None, solve_margin=0.0):
+               reuse_surrogate=True, capacity=None, solve_margin=0.0, no_repeat=False):
     """myopic_bayesopt.jl's loop: per budget step xnext = multistart_base_solve!(sur, …; guesses =
     generate_initial_guesses(starts, lbs, ubs), θfixed) -- the deterministic multistart local solve of
     the analytic acquisition on the base surrogate (:224-233), here mrbo_base_solve on the device --
@@ -253,8 +254,11 @@ def run_myopic(function_name, output_dir, budget=100, trials=60, starts=64, seed
     solve_margin (diagnostic, build-defined; 0 = the reference's box): the acquisition is solved on
     the box shrunk by solve_margin·(ub − lb) per side -- a proxy for IPNewton's interior iterates
     (rbf_optim.jl:24-30: a log barrier keeps them off the faces), used to test whether the
-    projected Newton's stops on the faces explain a difference."""
-    from .rbf_optim import multistart_base_solve
+    projected Newton's stops on the faces explain a difference.
+    no_repeat (diagnostic, build-defined; False = the reference's findmin): the best start whose
+    minimiser is not an observed point (within 1e-6 of a box width) is taken, to test whether
+    re-observing a point explains a difference; every trial records its repeated observations."""
+    from .rbf_optim import base_solve_batch, findmin_candidates, multistart_base_solve
     from .utils import generate_initial_guesses
     testfn = TESTFNS[function_name]()
     lbs, ubs = testfn.get_bounds()
@@ -292,15 +296,26 @@ def run_myopic(function_name, output_dir, budget=100, trials=60, starts=64, seed
             ell_start = float(sur.ψ.lengthscale)
             initial_best = float(np.min(yinit))
             times, gaps, allocs, regrets, minobs = (np.zeros(budget) for _ in range(5))
+            repeats = np.zeros(budget, dtype=bool)
             xnext = np.zeros(testfn.dim)
             for b in range(budget):
                 t0 = time.perf_counter()
-                if solve_margin > 0.0:
-                    w = (ubs - lbs) * solve_margin
+                w = (ubs - lbs) * solve_margin
+                if no_repeat:
+                    xs_, fs_, _ = base_solve_batch(sur, lbs + w, ubs - w, guesses, [theta], device=device)
+                    Xo = sur.X[:, :sur.observed]
+                    tol = 1e-6 * (ubs - lbs)[:, None]
+                    fresh = [i for i in range(xs_.shape[1])
+                             if not (np.abs(Xo - xs_[:, i:i + 1]) <= tol).all(axis=0).any()]
+                    pick = findmin_candidates(xs_[:, fresh], fs_[fresh]) if fresh else None
+                    xnext[:] = xs_[:, fresh[pick]] if fresh else xs_[:, findmin_candidates(xs_, fs_)]
+                elif solve_margin > 0.0:
                     multistart_base_solve(sur, xnext, lbs + w, ubs - w, guesses, [theta], device=device)
                 else:
                     multistart_base_solve(sur, xnext, lbs, ubs, guesses, [theta], device=device)
                 times[b] = time.perf_counter() - t0
+                Xo = sur.X[:, :sur.observed]
+                repeats[b] = bool((np.abs(Xo - xnext[:, None]) <= 1e-6 * (ubs - lbs)[:, None]).all(axis=0).any())
                 observed_best = float(np.min(sur.get_active_observations()))
                 regrets[b] = simple_regret(true_minimum, observed_best)
                 gaps[b] = gap(initial_best, observed_best, true_minimum)
@@ -314,7 +329,7 @@ def run_myopic(function_name, output_dir, budget=100, trials=60, starts=64, seed
                 write_to_csv(os.path.join(directory, f"{acq}_{metric}"), data)
             results[(acq, trial)] = dict(times=times, gaps=gaps, simple_regret=regrets, minimum_observations=minobs,
                                          X=sur.get_active_covariates().copy(), y=sur.get_active_observations().copy(),
-                                         ell_start=ell_start, ell_end=float(sur.ψ.lengthscale))
+                                         ell_start=ell_start, ell_end=float(sur.ψ.lengthscale), repeats=repeats)
     return results
 
 

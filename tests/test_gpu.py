@@ -232,6 +232,29 @@ def test_specialised_kernel_equals_generic(gpu, monkeypatch, name, M, R):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name,M,R", [("C1", 32, 4), ("C2", 64, 4)])
+def test_half_wave_kernel_equals_full_wave(gpu, monkeypatch, name, M, R):
+    """N ≤ 32, d ≤ 4, h ≤ 3 (C1, C2) run the half-wave kernel rollout_kernel<D, 1, 1, 2> (two
+    trajectories per wave, plan info spec = 2); MRBO_HALF=0 keeps the full-wave kernel.  The
+    32-lane reductions sum the same terms in another order, so: identical Newton work and
+    policy path, values to rtol 1e-12, gradients to 1e-10 (as spec vs generic)."""
+    g = _problem_arrays(name, M, R)
+    p_half = _plan(g)
+    assert p_half.info()["spec"] == 2
+    r_half = _run(p_half, g)
+    monkeypatch.setenv("MRBO_HALF", "0")
+    p_full = _plan(g)
+    assert p_full.info()["spec"] == 1
+    r_full = _run(p_full, g)
+    assert (r_half["status"] == 0).all() and (r_full["status"] == 0).all()
+    np.testing.assert_array_equal(r_half["evals"], r_full["evals"])
+    for k in ("values", "obs", "policy_x"):
+        np.testing.assert_allclose(r_half[k], r_full[k], rtol=1e-12, atol=1e-15, err_msg=k)
+    for k in ("grad_x", "grad_theta"):
+        _assert_grads_close(r_half[k], r_full[k], rtol=1e-10)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name,M,R", [("C3", 32, 4), ("C4", 8, 2)])
 def test_work_order_changes_nothing_but_the_schedule(gpu, name, M, R):
     """mrbo_plan_set_order only reorders the work queue: a reversed permutation and the

@@ -3,6 +3,8 @@
 # each running every variant once (bench.py C3, or BENCH_ARGS), so that clock drift between boxes
 # and over time falls on all variants alike.  Prints kernel ms per run and the per-variant median.
 # usage: [REPS=3] [BENCH_ARGS="--mle"] [TAG=x] bash tools/ab_rep.sh base fold ...
+# A variant lib+VAR=value runs libmrbo_<lib>.so with VAR=value in its environment; lib "main" is
+# the main build (mrbo/libmrbo.so).
 root=${GRAFT_REPO_ROOT:-$PWD}
 V=$root/rollout-bayesian-optimization_amd/mrbo/variants
 out=$root/gpurun_out/ab_rep${TAG:+_$TAG}
@@ -12,7 +14,11 @@ REPS=${REPS:-3}
 for rep in $(seq 1 "$REPS"); do
   for v in "$@"; do
     f=$out/${v}_$rep
-    MRBO_LIB=$V/libmrbo_$v.so timeout -k 10 120 python -u bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline $BENCH_ARGS \
+    lib=${v%%+*}; envs=""
+    [[ $v == *+* ]] && envs=${v#*+}
+    so=$V/libmrbo_$lib.so
+    [[ $lib == main ]] && so=$root/rollout-bayesian-optimization_amd/mrbo/libmrbo.so
+    env $envs MRBO_LIB=$so timeout -k 10 120 python -u bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline $BENCH_ARGS \
       > "$f.json" 2> "$f.err" || { echo "variant $v rep $rep failed"; tail -5 "$f.err"; exit 1; }
     python - "$f.json" "$v" "$rep" <<'PY'
 import json, sys

@@ -133,7 +133,7 @@ def trajectory_diagnostics(Xs, lbs, ubs, initial):
 
 
 def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incumbent=True, reuse=None,
-             run_budget=None, solve_margin=0.0):
+             run_budget=None, solve_margin=0.0, no_repeat=False):
     """One comparison case.  run_budget (myopic cases) overrides the steps each trial runs (default
     the reference's 100, whose last optimize! sets the next trial's starting lengthscale).
     reuse=None takes the surrogate semantics of the driver that produced the case's records: the
@@ -156,7 +156,7 @@ def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incu
             res = bayesopt.run_myopic(s["fn"], tmp, budget=rb, trials=trials, starts=s["starts"], seed=seed,
                                       rules=(s["rule"],), initial_observations=s["initial"], log=lg,
                                       reuse_surrogate=reuse, capacity=s["capacity"] if reuse else None,
-                                      solve_margin=solve_margin)
+                                      solve_margin=solve_margin, no_repeat=no_repeat)
         else:
             res = bayesopt.run(s["fn"], tmp, budget=s["budget"], trials=trials, starts=s["starts"], horizon=s["horizon"],
                                mc_samples=100, batch_size=s["batch"], sgd_iterations=50, optimize=True, seed=seed,
@@ -172,6 +172,9 @@ def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incu
     gcols = our_gap_columns(trials_res, true_minimum, len(trials_res[0]["gaps"]))
     lbs, ubs = testfn.get_bounds()
     diag = trajectory_diagnostics([r["X"] for r in trials_res], lbs, ubs, s["initial"])
+    if myopic:   # repeated observations per trial within the compared budget
+        nb = int(s["labels"][-1])
+        diag["repeats_per_trial_in_budget"] = float(np.mean([np.sum(r["repeats"][:nb]) for r in trials_res]))
     per_label = {lab: compare(our_column(gcols, lab, myopic), ref_column(case, lab)) for lab in s["labels"]}
     our_times = np.concatenate([r["times"] for r in trials_res])
     ref_times = np.array(case["times"], float)[:, :s["budget"]].ravel()
@@ -181,7 +184,8 @@ def run_case(key, case, trials, seed, log, solver="sga", eta=0.01, q3=True, incu
                                                                         eta=eta, seed=seed, q3_fmini_over_capacity=q3,
                                                                         incumbent_restart=incumbent,
                                                                         reuse_surrogate=reuse,
-                                                                        solve_margin=solve_margin),
+                                                                        solve_margin=solve_margin,
+                                                                        no_repeat=no_repeat),
             "gaps": per_label, "difference_detected": {lab: detected(v) for lab, v in per_label.items()},
             "ours_lengthscale": {"start_median": float(np.median([r["ell_start"] for r in trials_res])),
                                  "end_median": float(np.median([r["ell_end"] for r in trials_res])),
@@ -213,13 +217,15 @@ def main():
     ap.add_argument("--solve-margin", type=float, default=0.0,
                     help="diagnostic (myopic cases): solve the acquisition on the box shrunk by this fraction of "
                          "its width per side -- a proxy for IPNewton's interior iterates")
+    ap.add_argument("--no-repeat", action="store_true",
+                    help="diagnostic (myopic cases): take the best start whose minimiser is not an observed point")
     a = ap.parse_args()
     ref = load_reference()
     log = lambda m: print(m, file=sys.stderr, flush=True)
     for key in (ASSERTED if a.cases == "asserted" else a.cases.split(",")):
         eta = a.eta or (0.01 if a.solver == "sga" else 0.02)
         row = run_case(key, ref[key], a.trials, a.seed, log, solver=a.solver, eta=eta, q3=not a.no_q3, incumbent=not a.no_incumbent,
-                       reuse={"auto": None, "yes": True, "no": False}[a.reuse], solve_margin=a.solve_margin)
+                       reuse={"auto": None, "yes": True, "no": False}[a.reuse], solve_margin=a.solve_margin, no_repeat=a.no_repeat)
         line = json.dumps(row)
         print(line, flush=True)
         if a.out:
@@ -227,7 +233,7 @@ def main():
                 f.write(line + "\n")
         g = row["gaps"][SETTINGS[key]["labels"][-1]]
         log(f"{key} [{a.solver}{'' if not a.no_q3 else ', Q3 off'}{'' if not a.no_incumbent else ', no incumbent'}"
-            f"{'' if not a.solve_margin else f', margin {a.solve_margin:g}'}]: final gap ours {g['ours_mean']:.3f}±{g['ours_se']:.3f} ref {g['ref_mean']:.3f}±{g['ref_se']:.3f} "
+            f"{'' if not a.solve_margin else f', margin {a.solve_margin:g}'}{', no repeat' if a.no_repeat else ''}]: final gap ours {g['ours_mean']:.3f}±{g['ours_se']:.3f} ref {g['ref_mean']:.3f}±{g['ref_se']:.3f} "
             f"diff {g['diff_mean']:+.3f} [{g['diff_ci95'][0]:+.3f}, {g['diff_ci95'][1]:+.3f}] "
             f"MW p={g['mannwhitney_p']:.3f} ({row['difference_detected'][SETTINGS[key]['labels'][-1]]}); s/solve ours {row['seconds_per_solve']['ours_median']:.3f} "
             f"ref {row['seconds_per_solve']['ref_median']:.2f}; diag {row['ours_trajectory_diagnostics']}")

@@ -13,6 +13,7 @@
 #             beside the plain line, 10 steps each, no CPU baseline
 #   shim      tools/shim_rate.py at C3 (the Julia drop-in's call patterns)
 #   c2        C2 bench line (20 steps)
+#   myopic    myopic BO diagnostics: seeds, solve margins, no-repeat pick (4 cases, 60 trials)
 #   c5cost    C5 + NonUniformCost at M = 256, R = 128 (one step)
 #   prof      rocprofv3 --kernel-trace --stats of the default bench (1 step) + FETCH_SIZE / WRITE_SIZE
 #             passes (tools/profile.sh), C3 and C3-MLE
@@ -77,6 +78,22 @@ for l in open(sys.argv[1]):
     c2)
       timeout -k 10 200 python -u bench.py --config C2 --no-cpu-baseline --steps 20 > "$out/bench_c2.json" 2> "$out/bench_c2.err"
       rc=$?; tail -c 400 "$out/bench_c2.json" ;;
+    myopic)
+      # the myopic rows that closed less in round 4 (+ the Hartmann-6 EI control): other seeds,
+      # interior solves (margins) and the no-repeat pick, 60 trials each
+      cases=myopic_hartmann6d_poi,myopic_hartmann6d_lcb,myopic_sixhump_poi,myopic_hartmann6d_ei
+      rc=0
+      for v in "seed 1" "seed 2" "seed 3" "margin 0.01" "margin 0.05" "norepeat"; do
+        set -- $v
+        case $1 in
+          seed) args="--seed $2"; vt=seed$2 ;;
+          margin) args="--solve-margin $2"; vt=margin$2 ;;
+          norepeat) args="--no-repeat"; vt=norepeat ;;
+        esac
+        timeout -k 10 300 python -u tools/bo_compare.py --trials 60 --cases $cases $args \
+          --out "$out/bo_myopic_$vt.jsonl" > /dev/null 2> "$out/bo_myopic_$vt.err" || { rc=$?; break; }
+        grep "final gap" "$out/bo_myopic_$vt.err"
+      done ;;
     c5cost)
       timeout -k 10 400 python -u bench.py --config C5 --cost --mc-per-gpu 256 --restarts 128 --steps 1 --warmup 1 --no-cpu-baseline \
         > "$out/bench_c5_cost.json" 2> "$out/bench_c5_cost.err"
