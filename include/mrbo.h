@@ -275,7 +275,7 @@ double mrbo_last_gp_fit_ms(void);
 
 /* Launch geometry of a plan (no reference counterpart; measurement and FLOP accounting):
  * info[0..5] = rows per lane (1/2/4), workgroups, waves per workgroup, batched start values
- * (0/1), compile-time specialised kernel (0 generic, 1 Matérn-5/2 + EI, 2 its half-wave form: N ≤ 32, d ≤ 4, h ≤ 3), LDS bytes per workgroup.  Writes min(n, 6). */
+ * (0/1), compile-time specialised kernel (0 generic, 1 Matérn-5/2 + EI, 2 its half-wave form: N ≤ 32, d ≤ 4, h ≤ 3, 3 Matérn-5/2 + EI + quadratic cost), LDS bytes per workgroup.  Writes min(n, 6). */
 int mrbo_plan_info(const mrbo_plan_t* plan, int32_t* info, int32_t n);
 
 /* Work order of the plan's later mrbo_simulate_mc / mrbo_simulate_ghq launches (no reference

@@ -67,7 +67,8 @@ struct mrbo_plan {
   const int32_t* order = nullptr;   // mrbo_plan_set_order: caller-owned device permutation of M×R
   int wpg = 4, blocks = 0;
   size_t smem = 0;
-  int spec = 0;             // 1: rollout_kernel<D, RPL, 1> (Matérn-5/2 + EI fixed); 2: its half-wave form <D, 1, 1, 2>
+  int spec = 0;             // 1: rollout_kernel<D, RPL, 1> (Matérn-5/2 + EI fixed); 2: its half-wave form <D, 1, 1, 2>;
+                            // 3: <D, RPL, 2> (Matérn-5/2 + EI + quadratic cost)
   int fx = 0;               // 1: the FMAX = 4 kernel units (h ≤ 3, d ≤ 8)
   int xs_lds = 0;           // rollout launches stage xstarts in LDS (≤ 8 KB)
   int batch = 0;            // batched start-point values (start tables in LDS)
@@ -660,7 +661,12 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   // (MRBO_HALF=0 keeps the full-wave one, for A/B runs and tests)
   const char* half = getenv("MRBO_HALF");
   if (P->spec == 1 && ks.rollout_half && N <= 32 && ns <= 32 && !(half && half[0] == '0')) P->spec = 2;
-  const void* rk = P->spec == 2 ? ks.rollout_half : P->spec ? ks.rollout_spec : ks.rollout;
+  // Matérn-5/2 + EI + the quadratic cost (C5 --cost): its own specialisation where compiled
+  if (P->kernel == MRBO_KERNEL_MATERN52 && P->p.rule == MRBO_RULE_EI && P->p.cost == MRBO_COST_QUADRATIC &&
+      ks.rollout_cost && !(gen && gen[0] == '1'))
+    P->spec = 3;
+  const void* rk = P->spec == 3 ? ks.rollout_cost : P->spec == 2 ? ks.rollout_half : P->spec ? ks.rollout_spec
+                                                                                              : ks.rollout;
   const size_t wave_bytes = P->spec == 2 ? ks.wave_bytes_half : ks.wave_bytes;
   const int waves0 =
       pick_grid(rk, fixed, wave_bytes, prop.multiProcessorCount, wpg0, blocks0, smem0, 0, maxw);

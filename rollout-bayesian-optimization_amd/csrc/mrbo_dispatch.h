@@ -24,6 +24,8 @@ struct KernelSet {
   // (Matérn-5/2 + EI), with its per-wave LDS (two trajectory areas); null where not compiled
   const void* rollout_half = nullptr;
   size_t wave_bytes_half = 0;
+  // Matérn-5/2 + EI + quadratic NonUniformCost at compile time (rollout_kernel<D, RPL, 2>), or null
+  const void* rollout_cost = nullptr;
 };
 
 // The host API sees every unit's entry points as weak references (MRBO_API_TU): a library

@@ -36,7 +36,15 @@ constexpr bool has_rpl(int d, int rpl) { return rpl == 1 || rpl == 2 || (d <= 8 
 constexpr bool has_spec(int d, int rpl) { return d <= 8 && rpl <= 4; }
 // half-wave kernel rollout_kernel<D, 1, 1, 2> (two trajectories per wave, N ≤ 32): the FMAX = 4
 // units of d ≤ 4, Matérn-5/2 + EI (C1, C2)
-#if MRBO_FMAX == 4 && MRBO_D <= 4 && !(defined(MRBO_AB_MIN) && defined(MRBO_AB_GENERIC)) && !defined(MRBO_STAMPS)
+// Matérn-5/2 + EI + the quadratic NonUniformCost fixed at compile time, rollout_kernel<D, RPL, 2>:
+// the FMAX = 6 units of d ≤ 8 at N = 65..256 (C5 --cost); other cost plans run the generic kernel
+#if MRBO_FMAX == 6 && MRBO_D <= 8 && !defined(MRBO_AB_MIN) && !defined(MRBO_NO_COST_SPEC)
+#define MRBO_HAS_COST 1
+#else
+#define MRBO_HAS_COST 0
+#endif
+constexpr bool has_cost(int d, int rpl) { return MRBO_HAS_COST && d <= 8 && (rpl == 2 || rpl == 4); }
+#if MRBO_FMAX == 4 && MRBO_D <= 4 && !(defined(MRBO_AB_MIN) && (defined(MRBO_AB_GENERIC) || defined(MRBO_AB_COST))) && !defined(MRBO_STAMPS)
 #define MRBO_HAS_HALF 1
 #else
 #define MRBO_HAS_HALF 0
@@ -46,23 +54,30 @@ template <int D, int RPL>
 static KernelSet kset() {
   using Ly = Lay<D, RPL>;
   const void* spec = nullptr;
-#if defined(MRBO_AB_MIN) && defined(MRBO_AB_GENERIC)   // the generic kernel alone (cost, other rules)
+#if defined(MRBO_AB_MIN) && defined(MRBO_AB_COST)      // Matérn-5/2 + EI + quadratic cost alone
+  spec = (const void*)&rollout_kernel<D, RPL, 2>;
+#elif defined(MRBO_AB_MIN) && defined(MRBO_AB_GENERIC)   // the generic kernel alone (cost, other rules)
   spec = (const void*)&rollout_kernel<D, RPL, 0>;
 #else
   if constexpr (has_spec(D, RPL)) spec = (const void*)&rollout_kernel<D, RPL, 1>;
 #endif
 #ifdef MRBO_AB_MIN
-  return KernelSet{spec, spec, (const void*)&eval_base_kernel<D, RPL>,
+  KernelSet ks{spec, spec, (const void*)&eval_base_kernel<D, RPL>,
 #else
-  return KernelSet{(const void*)&rollout_kernel<D, RPL, 0>, spec, (const void*)&eval_base_kernel<D, RPL>,
+  KernelSet ks{(const void*)&rollout_kernel<D, RPL, 0>, spec, (const void*)&eval_base_kernel<D, RPL>,
 #endif
-                   sizeof(double) * Ly::WAVE_LDS, Ly::SQ, Ly::BC && !Ly::SQ, Ly::LD, Ly::LINV_DOUBLES, Ly::GL,
-                   Ly::LINV_GLOBAL, KBounds<D, RPL>::threads
+               sizeof(double) * Ly::WAVE_LDS, Ly::SQ, Ly::BC && !Ly::SQ, Ly::LD, Ly::LINV_DOUBLES, Ly::GL,
+               Ly::LINV_GLOBAL, KBounds<D, RPL>::threads};
 #if MRBO_HAS_HALF
-                   , RPL == 1 ? (const void*)&rollout_kernel<D, 1, 1, 2> : nullptr,
-                   RPL == 1 ? 2 * sizeof(double) * Lay<D, 1, 2>::WAVE_LDS : 0
+  if constexpr (RPL == 1) {
+    ks.rollout_half = (const void*)&rollout_kernel<D, 1, 1, 2>;
+    ks.wave_bytes_half = 2 * sizeof(double) * Lay<D, 1, 2>::WAVE_LDS;
+  }
 #endif
-  };
+#if MRBO_HAS_COST
+  if constexpr (has_cost(D, RPL)) ks.rollout_cost = (const void*)&rollout_kernel<D, RPL, 2>;
+#endif
+  return ks;
 }
 
 bool MRBO_SFX(kset_d)(int rpl, KernelSet& ks) {
@@ -84,7 +99,10 @@ bool MRBO_SFX(kset_d)(int rpl, KernelSet& ks) {
 
 template <int RPL, int SPEC>
 static void launch_one(dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
-#if defined(MRBO_AB_MIN) && defined(MRBO_AB_GENERIC)
+#if defined(MRBO_AB_MIN) && defined(MRBO_AB_COST)
+  if constexpr (has_rpl(MRBO_D, RPL))
+    hipLaunchKernelGGL((rollout_kernel<MRBO_D, RPL, 2>), g, b, sm, st, kp);
+#elif defined(MRBO_AB_MIN) && defined(MRBO_AB_GENERIC)
   if constexpr (has_rpl(MRBO_D, RPL))
     hipLaunchKernelGGL((rollout_kernel<MRBO_D, RPL, 0>), g, b, sm, st, kp);
 #elif defined(MRBO_AB_MIN)
@@ -104,12 +122,20 @@ static void launch_rollout_spec(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t 
   else launch_one<8, SPEC>(g, b, sm, st, kp);
 }
 
-// spec: 0 generic, 1 Matérn-5/2 + EI, 2 the half-wave kernel (rows per lane 1)
+// spec: 0 generic, 1 Matérn-5/2 + EI, 2 the half-wave kernel (rows per lane 1), 3 Matérn-5/2 + EI +
+// quadratic cost (rollout_kernel<D, RPL, 2>)
 void MRBO_SFX(launch_rollout_d)(int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st,
                                        const KParams& kp) {
 #if MRBO_HAS_HALF
   if (spec == 2) {
     if (rpl == 1) hipLaunchKernelGGL((rollout_kernel<MRBO_D, 1, 1, 2>), g, b, sm, st, kp);
+    return;
+  }
+#endif
+#if MRBO_HAS_COST
+  if (spec == 3) {
+    if (rpl == 2) hipLaunchKernelGGL((rollout_kernel<MRBO_D, 2, 2>), g, b, sm, st, kp);
+    else if (rpl == 4) hipLaunchKernelGGL((rollout_kernel<MRBO_D, 4, 2>), g, b, sm, st, kp);
     return;
   }
 #endif

@@ -588,6 +588,131 @@ __device__ __forceinline__ void gl_bcast_product_k(double (&acc)[K], const doubl
   }
 }
 
+// Rows 16q..16q+15 of the 64×64 L2 block at lb (lane offset applied): 16 loads into l.
+__device__ __forceinline__ void gl_load_q(double (&l)[16], const double* lb, int q) {
+#pragma unroll
+  for (int u = 0; u < 16; ++u) l[u] = lb[(16 * q + u) * WAVE];
+}
+
+template <int K>
+__device__ __forceinline__ void gl_quarter(double (&acc)[K], const double (&b)[K], const double (&l)[16]) {
+  if constexpr (K > 9) {
+    gl_quarter<8>(head8(acc), head8(b), l);
+    gl_quarter<K - 8>(tail8(acc), tail8(b), l);
+  } else {
+    BcastRegAsm<K, 0>::run(acc, b, head8(l));
+    BcastRegAsm<K, 8>::run(acc, b, tail8(l));
+  }
+}
+
+// The blocks t = t0..t1 of one row slot as ONE software-pipelined chain (MRBO_GL_CHAIN): the same
+// quarters in the same order as gl_bcast_product (rows 0-15, 32-47, 16-31, 48-63 of each block,
+// blocks in t order: bit-identical sums), with two 16-row buffers -- each quarter's loads are
+// issued one quarter ahead, the next block's first two quarters during this block's last two.
+// gl_bcast_product waits for all 32 rows of a half-block before its first FMA, and the inline
+// FMA blocks are scheduling barriers, so at one wave per SIMD that L2 round trip was exposed
+// twice per block.  lb[t]: block base (lane offset applied), nr[t] = min(64, N − 64t).
+template <int K, int NT>
+__device__ __forceinline__ void gl_chain(double (&acc)[K], const double (&v)[NT][K], const double* const (&lb)[NT],
+                                         const int (&nr)[NT], int t0, int t1) {
+  double la[16], lc[16];
+  gl_load_q(la, lb[t0], 0);
+  if (nr[t0] > 32) gl_load_q(lc, lb[t0], 2);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (t < t0 || t > t1 || nr[t] <= 0) continue;
+    double b0[K], b2[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) row_blocks<0>(v[t][c], b0[c], b2[c]);
+    gl_quarter<K>(acc, b0, la);                              // rows 0-15
+    if (nr[t] > 16) gl_load_q(la, lb[t], 1);
+    if (nr[t] > 32) gl_quarter<K>(acc, b2, lc);             // rows 32-47
+    if (nr[t] > 48) gl_load_q(lc, lb[t], 3);
+    double b1[K], b3[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) row_blocks<1>(v[t][c], b1[c], b3[c]);
+    if (nr[t] > 16) gl_quarter<K>(acc, b1, la);             // rows 16-31
+    const bool more = t + 1 <= t1 && t + 1 < NT && nr[t + 1 < NT ? t + 1 : t] > 0;
+    if (more) gl_load_q(la, lb[t + 1 < NT ? t + 1 : t], 0);
+    if (nr[t] > 48) gl_quarter<K>(acc, b3, lc);             // rows 48-63
+    if (more && nr[t + 1 < NT ? t + 1 : t] > 32) gl_load_q(lc, lb[t + 1 < NT ? t + 1 : t], 2);
+  }
+}
+
+// The single-column (K = 1) products over the L2 blocks -- the value pass's forward product and
+// the backward w = L0⁻ᵀY0 -- as ONE stream of 16-row quarters with MRBO_K1_NB − 1 quarters of
+// loads in flight (MRBO_K1_STREAM).  A K = 1 quarter is 16 dependent FMAs, far shorter than an L2
+// round trip at one wave per SIMD, so gl_bcast_product<1> waited on every half-block's loads.
+// Same quarters, same order, same single accumulation chain per row slot: bit-identical sums.
+// FWD: out[s] = Σ_{t ≤ s} L0⁻¹(s,t) v[t] from the forward copy; else out[s] = Σ_{t ≥ s} of the
+// backward copy's block (t,s) times v[t].  base: the copy's first block, lane offset applied.
+#ifndef MRBO_K1_NB
+#define MRBO_K1_NB 4
+#endif
+template <int RPL, bool FWD>
+struct K1Seq {
+  static constexpr int NP = RPL * (RPL + 1) / 2, NQ = 4 * NP;
+  // pair p → (s, t): FWD s-major with t = 0..s; backward s-major with t = s..RPL-1
+  static constexpr int ps(int p) {
+    int s = 0;
+    for (;;) {
+      const int n = FWD ? s + 1 : RPL - s;
+      if (p < n) return s;
+      p -= n;
+      ++s;
+    }
+  }
+  static constexpr int pt(int p) {
+    int s = 0;
+    for (;;) {
+      const int n = FWD ? s + 1 : RPL - s;
+      if (p < n) return FWD ? p : s + p;
+      p -= n;
+      ++s;
+    }
+  }
+  static constexpr int blk(int p) {   // block index of pair p in the packed block triangle
+    const int s = ps(p), t = pt(p);
+    return FWD ? s * (s + 1) / 2 + t : t * (t + 1) / 2 + s;
+  }
+  static constexpr int qrow(int i) { return (i & 1) * 2 + ((i >> 1) & 1); }   // quarters 0, 2, 1, 3
+  static constexpr bool last_of_s(int p) { return p + 1 == NP || ps(p + 1) != ps(p); }
+};
+
+template <int RPL, bool FWD>
+__device__ __forceinline__ void gl_k1_stream(double (&out)[RPL], const double (&v)[RPL], const double* base, int N) {
+  using S = K1Seq<RPL, FWD>;
+  constexpr int NB = MRBO_K1_NB;
+  double rb[RPL][4];   // row blocks 0..3 of v[t], broadcast to every 16-lane row
+#pragma unroll
+  for (int t = 0; t < RPL; ++t) row_blocks4(v[t], rb[t][0], rb[t][1], rb[t][2], rb[t][3]);
+  double buf[NB][16];
+  auto load = [&](double (&l)[16], int i) {
+    const double* lb = base + (long long)S::blk(i >> 2) * WAVE * WAVE + 16 * S::qrow(i & 3) * WAVE;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) l[u] = lb[u * WAVE];
+  };
+#pragma unroll
+  for (int j = 0; j < NB - 1; ++j)
+    if (j < S::NQ) load(buf[j], j);
+  double acc[1] = {0.0};
+#pragma unroll
+  for (int i = 0; i < S::NQ; ++i) {
+    if (i + NB - 1 < S::NQ) load(buf[(i + NB - 1) % NB], i + NB - 1);
+    const int p = i >> 2, q = S::qrow(i & 3), t = S::pt(p);
+    const int nr = N - WAVE * t;
+    if (16 * q < nr) {
+      const double b[1] = {rb[t][q]};
+      BcastRegAsm<1, 0>::run(acc, b, head8(buf[i % NB]));
+      BcastRegAsm<1, 8>::run(acc, b, tail8(buf[i % NB]));
+    }
+    if ((i & 3) == 3 && S::last_of_s(p)) {
+      out[S::ps(p)] = acc[0];
+      acc[0] = 0.0;
+    }
+  }
+}
+
 template <int K>
 __device__ __forceinline__ void gl_bcast_product(double (&acc)[K], const double (&v)[K], const double* lb, int nrows) {
   if constexpr (K > 9) {
@@ -772,7 +897,61 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
     // (s,t) at blk(s,t)·4096 + j·64 + i, 16 steps' entries loaded ahead into registers
     auto nrows = [&](int t) { const int n = N - WAVE * t; return n < WAVE ? n : WAVE; };
     const double* L0 = W.Linv + lane;
+#ifdef MRBO_GL_CHAIN
+    int nr[RPL];
+#pragma unroll
+    for (int t = 0; t < RPL; ++t) nr[t] = nrows(t);
     if (mode == EV_VALUE) {
+      double v1[RPL][1];
+#pragma unroll
+      for (int t = 0; t < RPL; ++t) v1[t][0] = Bown[t][0];
+#pragma unroll
+      for (int s = 0; s < RPL; ++s) {
+        const double* lb[RPL];
+#pragma unroll
+        for (int t = 0; t < RPL; ++t) lb[t] = L0 + Ly::blk(s, t <= s ? t : s) * WAVE * WAVE;
+        double a1[1] = {0.0};
+        gl_chain<1, RPL>(a1, v1, lb, nr, 0, s);
+        acc[s][0] = a1[0];
+      }
+    } else if (mode == EV_GRADC) {
+      double vg[RPL][D];
+#pragma unroll
+      for (int t = 0; t < RPL; ++t)
+#pragma unroll
+        for (int a = 0; a < D; ++a) vg[t][a] = Bown[t][1 + a];
+#pragma unroll
+      for (int s = 0; s < RPL; ++s) {
+        const double* lb[RPL];
+#pragma unroll
+        for (int t = 0; t < RPL; ++t) lb[t] = L0 + Ly::blk(s, t <= s ? t : s) * WAVE * WAVE;
+        double ag[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) ag[a] = 0.0;
+        gl_chain<D, RPL>(ag, vg, lb, nr, 0, s);
+#pragma unroll
+        for (int a = 0; a < D; ++a) acc[s][1 + a] = ag[a];
+        acc[s][0] = W.G12[3 * (lane + WAVE * s) + 2];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < RPL; ++s) {
+        const double* lb[RPL];
+#pragma unroll
+        for (int t = 0; t < RPL; ++t) lb[t] = L0 + Ly::blk(s, t <= s ? t : s) * WAVE * WAVE;
+        gl_chain<D1, RPL>(acc[s], Bown, lb, nr, 0, s);
+      }
+    }
+#else
+    if (mode == EV_VALUE) {
+#ifdef MRBO_K1_STREAM
+      double v1[RPL], o1[RPL];
+#pragma unroll
+      for (int t = 0; t < RPL; ++t) v1[t] = Bown[t][0];
+      gl_k1_stream<RPL, true>(o1, v1, L0, N);
+#pragma unroll
+      for (int s = 0; s < RPL; ++s) acc[s][0] = o1[s];
+#else
 #pragma unroll
       for (int s = 0; s < RPL; ++s) {
         double a1[1] = {0.0};
@@ -783,6 +962,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
         }
         acc[s][0] = a1[0];
       }
+#endif
     } else if (mode == EV_GRADC) {
 #pragma unroll
       for (int s = 0; s < RPL; ++s) {
@@ -807,6 +987,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
         for (int t = 0; t <= s; ++t)
           gl_bcast_product<D1>(acc[s], Bown[t], L0 + Ly::blk(s, t) * WAVE * WAVE, nrows(t));
     }
+#endif
   }
 
   if (do_val) {   // Y0 kept for a deferred GRADC / BACK evaluation
@@ -1086,6 +1267,41 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
       // blk(t,s)·4096 + k·64 + i; rows k of Y from register slot t
       auto nrows = [&](int t) { const int n = N - WAVE * t; return n < WAVE ? n : WAVE; };
       const double* LT = W.LinvT + lane;
+#ifdef MRBO_GL_CHAIN
+      int nr[RPL];
+#pragma unroll
+      for (int t = 0; t < RPL; ++t) nr[t] = nrows(t);
+      double y1[RPL][1];
+#pragma unroll
+      for (int t = 0; t < RPL; ++t) y1[t][0] = acc[t][0];
+#pragma unroll
+      for (int s = 0; s < RPL; ++s) {
+        const double* lb[RPL];
+#pragma unroll
+        for (int t = 0; t < RPL; ++t) lb[t] = LT + Ly::blk(t >= s ? t : s, s) * WAVE * WAVE;
+        if (rich) {
+          double a7[D1];
+#pragma unroll
+          for (int c = 0; c < D1; ++c) a7[c] = 0.0;
+          gl_chain<D1, RPL>(a7, acc, lb, nr, s, RPL - 1);
+          wv[s] = a7[0];
+#pragma unroll
+          for (int a = 0; a < D; ++a) pv[s][a] = a7[1 + a];
+        } else {
+          double a1[1] = {0.0};
+          gl_chain<1, RPL>(a1, y1, lb, nr, s, RPL - 1);
+          wv[s] = a1[0];
+        }
+      }
+#else
+#ifdef MRBO_K1_STREAM
+      if (!rich) {
+        double y1[RPL];
+#pragma unroll
+        for (int t = 0; t < RPL; ++t) y1[t] = acc[t][0];
+        gl_k1_stream<RPL, false>(wv, y1, LT, N);
+      } else
+#endif
 #pragma unroll
       for (int s = 0; s < RPL; ++s) {
         if (rich) {
@@ -1107,6 +1323,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
           wv[s] = a1[0];
         }
       }
+#endif
     }
     // fantasy part: + Σ_r E[r][i] Yf[r]
 #pragma unroll
@@ -2606,6 +2823,10 @@ __global__ void __launch_bounds__((KBounds<D, RPL, HW>::threads), (KBounds<D, RP
     kp.kernel = KERNEL_MATERN52;
     kp.rule = RULE_EI;
     kp.cost = COST_NONE;
+  } else if constexpr (SPEC == 2) {   // the same with the quadratic NonUniformCost weighting (C5 --cost)
+    kp.kernel = KERNEL_MATERN52;
+    kp.rule = RULE_EI;
+    kp.cost = COST_QUADRATIC;
   }
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // stage L0⁻¹ (and the inner-solve start points) once per workgroup (the only block barrier)

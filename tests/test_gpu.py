@@ -232,6 +232,30 @@ def test_specialised_kernel_equals_generic(gpu, monkeypatch, name, M, R):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name,M,R,ell", [("C4", 16, 2, 0.5), ("C5", 16, 2, 20.0)])
+def test_cost_kernel_equals_generic(gpu, monkeypatch, name, M, R, ell):
+    """Matérn-5/2 + EI + the quadratic NonUniformCost at N = 65..256 run rollout_kernel<D, RPL, 2>
+    (plan info spec = 3, the rule, kernel and cost fixed at compile time); MRBO_GENERIC_KERNEL=1
+    runs the generic kernel.  Same bars as the Matérn-5/2 + EI specialisation."""
+    g = _problem_arrays(name, M, R, ell=ell)
+    w = tuple(np.linspace(0.5, 1.5, g["X"].shape[0]))
+    opts = dict(cost="quadratic", cost_c0=1.0, cost_w=w)
+    p_spec = _plan(g, **opts)
+    assert p_spec.info()["spec"] == 3
+    r_spec = _run(p_spec, g)
+    monkeypatch.setenv("MRBO_GENERIC_KERNEL", "1")
+    p_gen = _plan(g, **opts)
+    assert p_gen.info()["spec"] == 0
+    r_gen = _run(p_gen, g)
+    assert (r_spec["status"] == 0).all() and (r_gen["status"] == 0).all()
+    np.testing.assert_array_equal(r_spec["evals"], r_gen["evals"])
+    for k in ("values", "obs", "policy_x"):
+        np.testing.assert_allclose(r_spec[k], r_gen[k], rtol=1e-12, atol=1e-15, err_msg=k)
+    for k in ("grad_x", "grad_theta"):
+        _assert_grads_close(r_spec[k], r_gen[k], rtol=1e-10)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name,M,R", [("C1", 32, 4), ("C2", 64, 4)])
 def test_half_wave_kernel_equals_full_wave(gpu, monkeypatch, name, M, R):
     """N ≤ 32, d ≤ 4, h ≤ 3 (C1, C2) run the half-wave kernel rollout_kernel<D, 1, 1, 2> (two

@@ -82,7 +82,8 @@ def test_full_restart_vs_oracle(gpu, oracle, name, R, ell, kind, htol):
         assert st["coverage"]["nonzero_grads"] >= 0.5, st
 
 
-@pytest.mark.parametrize("name,M,R,ell", [("C2", 64, 4, None), ("C3", 64, 4, None), ("C5", 16, 1, 20.0)])
+@pytest.mark.parametrize("name,M,R,ell", [("C2", 64, 4, None), ("C3", 64, 4, None), ("C4", 16, 2, 0.5),
+                                          ("C5", 16, 1, 20.0)])
 @pytest.mark.parametrize("kind", ["quadratic", "loglinear"])
 def test_cost_weighted_vs_oracle(gpu, oracle, name, M, R, ell, kind):
     """NonUniformCost (cost_functions.jl:5-20; the build's α/c(x) inner-solve rule, parity unpinned
