@@ -304,6 +304,21 @@ __device__ __forceinline__ double sconst() {
   return djoin(lo, hi);
 }
 
+// a·b + c with c a lane-uniform constant held in an SGPR pair (sconst): one VOP3 v_fma_f64 with the
+// SGPR operand.  A plain fma() with an SGPR addend is shrunk by the compiler to v_fmac_f64, whose
+// addend is also its destination, so every Horner step copied its coefficient into a VGPR pair
+// first (two v_mov_b32 per step, three VALU instructions per polynomial term).  Not volatile: the
+// scheduler moves it like any arithmetic.  MRBO_NO_FMA_SC: plain fma (A/B).
+__device__ __forceinline__ double fma_sc(double a, double b, double c) {
+#ifdef MRBO_NO_FMA_SC
+  return fma(a, b, c);
+#else
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+  return d;
+#endif
+}
+
 // exp(x), inlined: the device library's algorithm and coefficients in the same operation order
 // (Cody–Waite reduction by ln2, degree-11 polynomial, 2^k by v_ldexp_f64, overflow / underflow
 // selects), so results are bit-identical to exp() -- without a call's prologue (scratch save of
@@ -315,14 +330,14 @@ __device__ __forceinline__ double fexp(double x) {
   double c10 = sconst<0xfca7ab0cu, 0x3e928af3u>();
   asm volatile("" : "+v"(c10));   // one of the first step's two constants must live in VGPRs
   double p = fma(sconst<0x6a5dcb37u, 0x3e5ade15u>(), r, c10);
-  p = fma(r, p, sconst<0x623fde64u, 0x3ec71deeu>());
-  p = fma(r, p, sconst<0x7c89e6b0u, 0x3efa0199u>());
-  p = fma(r, p, sconst<0x14761f6eu, 0x3f2a01a0u>());
-  p = fma(r, p, sconst<0x1852b7b0u, 0x3f56c16cu>());
-  p = fma(r, p, sconst<0x11122322u, 0x3f811111u>());
-  p = fma(r, p, sconst<0x555502a1u, 0x3fa55555u>());
-  p = fma(r, p, sconst<0x55555511u, 0x3fc55555u>());
-  p = fma(r, p, sconst<0x0000000bu, 0x3fe00000u>());
+  p = fma_sc(r, p, sconst<0x623fde64u, 0x3ec71deeu>());
+  p = fma_sc(r, p, sconst<0x7c89e6b0u, 0x3efa0199u>());
+  p = fma_sc(r, p, sconst<0x14761f6eu, 0x3f2a01a0u>());
+  p = fma_sc(r, p, sconst<0x1852b7b0u, 0x3f56c16cu>());
+  p = fma_sc(r, p, sconst<0x11122322u, 0x3f811111u>());
+  p = fma_sc(r, p, sconst<0x555502a1u, 0x3fa55555u>());
+  p = fma_sc(r, p, sconst<0x55555511u, 0x3fc55555u>());
+  p = fma_sc(r, p, sconst<0x0000000bu, 0x3fe00000u>());
   p = fma(r, p, 1.0);
   p = fma(r, p, 1.0);
   double e = __builtin_ldexp(p, (int)k);
@@ -509,34 +524,34 @@ __device__ __forceinline__ PhiPair ei_phi_Phi(double z) {
   {
     double pe_h = sconst<0xf1ab7ccbu, 0x3dd09a8bu>();
     asm volatile("" : "+v"(pe_h));
-    pe_h = fma(t2, pe_h, sconst<0x73fda30du, 0x3e06db11u>());
-    pe_h = fma(t2, pe_h, sconst<0xf4266242u, 0xbe427e42u>());
-    pe_h = fma(t2, pe_h, sconst<0x1ed381c5u, 0xbe672292u>());
-    pe_h = fma(t2, pe_h, sconst<0xb901a919u, 0x3ec385e7u>());
-    pe_h = fma(t2, pe_h, sconst<0x645605dcu, 0xbf066e11u>());
+    pe_h = fma_sc(t2, pe_h, sconst<0x73fda30du, 0x3e06db11u>());
+    pe_h = fma_sc(t2, pe_h, sconst<0xf4266242u, 0xbe427e42u>());
+    pe_h = fma_sc(t2, pe_h, sconst<0x1ed381c5u, 0xbe672292u>());
+    pe_h = fma_sc(t2, pe_h, sconst<0xb901a919u, 0x3ec385e7u>());
+    pe_h = fma_sc(t2, pe_h, sconst<0x645605dcu, 0xbf066e11u>());
     double pe_l = sconst<0xfbfa9e67u, 0x3f427e65u>();
     asm volatile("" : "+v"(pe_l));
-    pe_l = fma(t2, pe_l, sconst<0xc891e642u, 0xbf7143c4u>());
-    pe_l = fma(t2, pe_l, sconst<0xf77381b3u, 0xbfa8ff5eu>());
-    pe_l = fma(t2, pe_l, sconst<0x0c35056au, 0xbfbd7683u>());
-    pe_l = fma(t2, pe_l, sconst<0x284b1971u, 0xbf859e2cu>());
-    pe_l = fma(t2, pe_l, sconst<0x9a0ee914u, 0x3ff3e0a9u>());
+    pe_l = fma_sc(t2, pe_l, sconst<0xc891e642u, 0xbf7143c4u>());
+    pe_l = fma_sc(t2, pe_l, sconst<0xf77381b3u, 0xbfa8ff5eu>());
+    pe_l = fma_sc(t2, pe_l, sconst<0x0c35056au, 0xbfbd7683u>());
+    pe_l = fma_sc(t2, pe_l, sconst<0x284b1971u, 0xbf859e2cu>());
+    pe_l = fma_sc(t2, pe_l, sconst<0x9a0ee914u, 0x3ff3e0a9u>());
     const double pe_ = fma(u6, pe_h, pe_l);
     pe = pe_;
     double po_h = sconst<0x617fb329u, 0xbe1406aau>();
     asm volatile("" : "+v"(po_h));
-    po_h = fma(t2, po_h, sconst<0xdb5ecc9au, 0x3e4d421du>());
-    po_h = fma(t2, po_h, sconst<0x3786431fu, 0xbe79e096u>());
-    po_h = fma(t2, po_h, sconst<0xc09ddffau, 0x3ea42eb1u>());
-    po_h = fma(t2, po_h, sconst<0x97b263b0u, 0xbecffe87u>());
-    po_h = fma(t2, po_h, sconst<0x306b92a0u, 0x3ef97053u>());
+    po_h = fma_sc(t2, po_h, sconst<0xdb5ecc9au, 0x3e4d421du>());
+    po_h = fma_sc(t2, po_h, sconst<0x3786431fu, 0xbe79e096u>());
+    po_h = fma_sc(t2, po_h, sconst<0xc09ddffau, 0x3ea42eb1u>());
+    po_h = fma_sc(t2, po_h, sconst<0x97b263b0u, 0xbecffe87u>());
+    po_h = fma_sc(t2, po_h, sconst<0x306b92a0u, 0x3ef97053u>());
     double po_l = sconst<0x5777da87u, 0xbf1fda8au>();
     asm volatile("" : "+v"(po_l));
-    po_l = fma(t2, po_l, sconst<0xf98105c2u, 0xbf33cf36u>());
-    po_l = fma(t2, po_l, sconst<0x67477473u, 0x3f938ec6u>());
-    po_l = fma(t2, po_l, sconst<0x6045eed1u, 0x3fb68610u>());
-    po_l = fma(t2, po_l, sconst<0xec6b3bb9u, 0x3fb8f702u>());
-    po_l = fma(t2, po_l, sconst<0x20ea5946u, 0xbfc1ebd2u>());
+    po_l = fma_sc(t2, po_l, sconst<0xf98105c2u, 0xbf33cf36u>());
+    po_l = fma_sc(t2, po_l, sconst<0x67477473u, 0x3f938ec6u>());
+    po_l = fma_sc(t2, po_l, sconst<0x6045eed1u, 0x3fb68610u>());
+    po_l = fma_sc(t2, po_l, sconst<0xec6b3bb9u, 0x3fb8f702u>());
+    po_l = fma_sc(t2, po_l, sconst<0x20ea5946u, 0xbfc1ebd2u>());
     const double po_ = fma(u6, po_h, po_l);
     po = po_;
   }
@@ -545,31 +560,31 @@ __device__ __forceinline__ PhiPair ei_phi_Phi(double z) {
   {
     double pe_ = sconst<0xf1ab7ccbu, 0x3dd09a8bu>();
     asm volatile("" : "+v"(pe_));
-    pe_ = fma(t2, pe_, sconst<0x73fda30du, 0x3e06db11u>());
-    pe_ = fma(t2, pe_, sconst<0xf4266242u, 0xbe427e42u>());
-    pe_ = fma(t2, pe_, sconst<0x1ed381c5u, 0xbe672292u>());
-    pe_ = fma(t2, pe_, sconst<0xb901a919u, 0x3ec385e7u>());
-    pe_ = fma(t2, pe_, sconst<0x645605dcu, 0xbf066e11u>());
-    pe_ = fma(t2, pe_, sconst<0xfbfa9e67u, 0x3f427e65u>());
-    pe_ = fma(t2, pe_, sconst<0xc891e642u, 0xbf7143c4u>());
-    pe_ = fma(t2, pe_, sconst<0xf77381b3u, 0xbfa8ff5eu>());
-    pe_ = fma(t2, pe_, sconst<0x0c35056au, 0xbfbd7683u>());
-    pe_ = fma(t2, pe_, sconst<0x284b1971u, 0xbf859e2cu>());
-    pe_ = fma(t2, pe_, sconst<0x9a0ee914u, 0x3ff3e0a9u>());
+    pe_ = fma_sc(t2, pe_, sconst<0x73fda30du, 0x3e06db11u>());
+    pe_ = fma_sc(t2, pe_, sconst<0xf4266242u, 0xbe427e42u>());
+    pe_ = fma_sc(t2, pe_, sconst<0x1ed381c5u, 0xbe672292u>());
+    pe_ = fma_sc(t2, pe_, sconst<0xb901a919u, 0x3ec385e7u>());
+    pe_ = fma_sc(t2, pe_, sconst<0x645605dcu, 0xbf066e11u>());
+    pe_ = fma_sc(t2, pe_, sconst<0xfbfa9e67u, 0x3f427e65u>());
+    pe_ = fma_sc(t2, pe_, sconst<0xc891e642u, 0xbf7143c4u>());
+    pe_ = fma_sc(t2, pe_, sconst<0xf77381b3u, 0xbfa8ff5eu>());
+    pe_ = fma_sc(t2, pe_, sconst<0x0c35056au, 0xbfbd7683u>());
+    pe_ = fma_sc(t2, pe_, sconst<0x284b1971u, 0xbf859e2cu>());
+    pe_ = fma_sc(t2, pe_, sconst<0x9a0ee914u, 0x3ff3e0a9u>());
     pe = pe_;
     double po_ = sconst<0x617fb329u, 0xbe1406aau>();
     asm volatile("" : "+v"(po_));
-    po_ = fma(t2, po_, sconst<0xdb5ecc9au, 0x3e4d421du>());
-    po_ = fma(t2, po_, sconst<0x3786431fu, 0xbe79e096u>());
-    po_ = fma(t2, po_, sconst<0xc09ddffau, 0x3ea42eb1u>());
-    po_ = fma(t2, po_, sconst<0x97b263b0u, 0xbecffe87u>());
-    po_ = fma(t2, po_, sconst<0x306b92a0u, 0x3ef97053u>());
-    po_ = fma(t2, po_, sconst<0x5777da87u, 0xbf1fda8au>());
-    po_ = fma(t2, po_, sconst<0xf98105c2u, 0xbf33cf36u>());
-    po_ = fma(t2, po_, sconst<0x67477473u, 0x3f938ec6u>());
-    po_ = fma(t2, po_, sconst<0x6045eed1u, 0x3fb68610u>());
-    po_ = fma(t2, po_, sconst<0xec6b3bb9u, 0x3fb8f702u>());
-    po_ = fma(t2, po_, sconst<0x20ea5946u, 0xbfc1ebd2u>());
+    po_ = fma_sc(t2, po_, sconst<0xdb5ecc9au, 0x3e4d421du>());
+    po_ = fma_sc(t2, po_, sconst<0x3786431fu, 0xbe79e096u>());
+    po_ = fma_sc(t2, po_, sconst<0xc09ddffau, 0x3ea42eb1u>());
+    po_ = fma_sc(t2, po_, sconst<0x97b263b0u, 0xbecffe87u>());
+    po_ = fma_sc(t2, po_, sconst<0x306b92a0u, 0x3ef97053u>());
+    po_ = fma_sc(t2, po_, sconst<0x5777da87u, 0xbf1fda8au>());
+    po_ = fma_sc(t2, po_, sconst<0xf98105c2u, 0xbf33cf36u>());
+    po_ = fma_sc(t2, po_, sconst<0x67477473u, 0x3f938ec6u>());
+    po_ = fma_sc(t2, po_, sconst<0x6045eed1u, 0x3fb68610u>());
+    po_ = fma_sc(t2, po_, sconst<0xec6b3bb9u, 0x3fb8f702u>());
+    po_ = fma_sc(t2, po_, sconst<0x20ea5946u, 0xbfc1ebd2u>());
     po = po_;
   }
 #endif
