@@ -236,7 +236,9 @@ def test_specialised_kernel_equals_generic(gpu, monkeypatch, name, M, R):
 def test_cost_kernel_equals_generic(gpu, monkeypatch, name, M, R, ell):
     """Matérn-5/2 + EI + the quadratic NonUniformCost at N = 65..256 run rollout_kernel<D, RPL, 2>
     (plan info spec = 3, the rule, kernel and cost fixed at compile time); MRBO_GENERIC_KERNEL=1
-    runs the generic kernel.  Same bars as the Matérn-5/2 + EI specialisation."""
+    runs the generic kernel.  Same bars as the Matérn-5/2 + EI specialisation, except policy points
+    to 1e-10: C4 at ℓ = 0.5 takes ≈ 500 Newton steps per trajectory under α/c, and a Newton endpoint
+    carries the few-ulp differences of the two schedules amplified by the step (measured 2.3e-12)."""
     g = _problem_arrays(name, M, R, ell=ell)
     w = tuple(np.linspace(0.5, 1.5, g["X"].shape[0]))
     opts = dict(cost="quadratic", cost_c0=1.0, cost_w=w)
@@ -249,8 +251,8 @@ def test_cost_kernel_equals_generic(gpu, monkeypatch, name, M, R, ell):
     r_gen = _run(p_gen, g)
     assert (r_spec["status"] == 0).all() and (r_gen["status"] == 0).all()
     np.testing.assert_array_equal(r_spec["evals"], r_gen["evals"])
-    for k in ("values", "obs", "policy_x"):
-        np.testing.assert_allclose(r_spec[k], r_gen[k], rtol=1e-12, atol=1e-15, err_msg=k)
+    for k, rtol in (("values", 1e-12), ("obs", 1e-12), ("policy_x", 1e-10)):
+        np.testing.assert_allclose(r_spec[k], r_gen[k], rtol=rtol, atol=1e-15, err_msg=k)
     for k in ("grad_x", "grad_theta"):
         _assert_grads_close(r_spec[k], r_gen[k], rtol=1e-10)
 

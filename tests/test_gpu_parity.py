@@ -98,7 +98,10 @@ def test_cost_weighted_vs_oracle(gpu, oracle, name, M, R, ell, kind):
     pts = np.asfortranarray(g["xstarts"][:, :8] * 0.9 + 0.05 * g["x0s"][:, :1])
     np.testing.assert_allclose(p.eval_base(pts), oracle.eval_base(_osur(oracle, g), pts, cost=cost, lbs=g["lbs"],
                                                                   ubs=g["ubs"]), rtol=1e-9, atol=1e-12)
-    _end_to_end(oracle, f"{name} cost={kind} ({M} x {R})", g, M, cost=cost, plan_opts=opts)
+    # C4 at ℓ = 0.5 runs ≈ 500 Newton steps per trajectory: its line-search counts differ by
+    # rounding on identical paths, so per-trajectory work equality is not asserted there (as in
+    # test_end_to_end_vs_oracle)
+    _end_to_end(oracle, f"{name} cost={kind} ({M} x {R})", g, M, cost=cost, plan_opts=opts, work_exact=name != "C4")
 
 
 def test_device_moments_merge_equals_eto_reduce(gpu):
