@@ -179,6 +179,29 @@ __device__ __forceinline__ void row_blocks4(double v, double& b0, double& b1, do
   b3 = djoin(c1[1], d1[1]);
 }
 
+// The three broadcast operands of a folded product (bcast_fold_fwd / _bwd) in 3 swaps and 2 copies
+// per dword, instead of all four blocks (row_blocks4: 3 swaps, 3 copies) plus a per-row select of
+// the folded pass's operand (2 v_cndmask per double).  With a0 = [r0 r0 r2 r2], a1 = [r1 r1 r3 r3]
+// from the first swap, v_permlane32_swap(a1, a0) gives X = [r1 r1 r0 r0] and Y = [r3 r3 r2 r2]:
+//   forward:  Y is the folded operand (row 1: block 3, rows 2, 3: block 2, row 0 idle) and the
+//             self-swap of X gives blocks 1 and 0;
+//   backward: X is the folded operand (rows 0, 1: block 1, row 2: block 0, row 3 idle) and the
+//             self-swap of Y gives blocks 3 and 2.
+__device__ __forceinline__ void fold_blocks(double v, bool fwd, double& p0, double& p1, double& m) {
+  int lo, hi;
+  dsplit(v, lo, hi);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);   // [r0 r0 r2 r2], [r1 r1 r3 r3]
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const auto xl = __builtin_amdgcn_permlane32_swap(a[1], a[0], false, false);   // X, Y (low dwords)
+  const auto xh = __builtin_amdgcn_permlane32_swap(b[1], b[0], false, false);
+  const int sl = fwd ? xl[0] : xl[1], sh = fwd ? xh[0] : xh[1];   // the pair to self-swap
+  const auto cl = __builtin_amdgcn_permlane32_swap(sl, sl, false, false);
+  const auto ch = __builtin_amdgcn_permlane32_swap(sh, sh, false, false);
+  p0 = djoin(cl[1], ch[1]);   // forward: block 0; backward: block 2
+  p1 = djoin(cl[0], ch[0]);   // forward: block 1; backward: block 3
+  m = fwd ? djoin(xl[1], xh[1]) : djoin(xl[0], xh[0]);
+}
+
 // The value of lane (l & 31) + 32·H in every lane l: one v_permlane32_swap per dword of the
 // register with itself leaves the lower half's values in both halves of the first result and the
 // upper half's in both halves of the second (H a compile-time constant after unrolling).

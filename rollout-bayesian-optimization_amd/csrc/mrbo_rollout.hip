@@ -424,21 +424,17 @@ template <int K>
 __device__ __forceinline__ void bcast_fold_fwd_k(double (&acc)[K], const double (&v)[K], const double* Lsq, int lane) {
   constexpr unsigned LD = WAVE + 1;
   const unsigned a0 = lds_addr(Lsq + lane);
-  double b0[K], b1[K], b2[K], b3[K];
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-#ifdef MRBO_ROWBLOCKS2
-    row_blocks<0>(v[c], b0[c], b2[c]);
-    row_blocks<1>(v[c], b1[c], b3[c]);
-#else
-    row_blocks4(v[c], b0[c], b1[c], b2[c], b3[c]);
-#endif
-  }
   const int q = lane >> 4;
-  double m[K], f[K];
+  double b0[K], b1[K], m[K], f[K];
 #pragma unroll
   for (int c = 0; c < K; ++c) {
-    m[c] = (q == 1) ? b3[c] : b2[c];
+#ifdef MRBO_FOLD_SELECT   // round-5 first form: all four blocks, then a per-row select
+    double b2, b3;
+    row_blocks4(v[c], b0[c], b1[c], b2, b3);
+    m[c] = (q == 1) ? b3 : b2;
+#else
+    fold_blocks(v[c], true, b0[c], b1[c], m[c]);
+#endif
     f[c] = 0.0;
   }
   // row 1: (48 + t, 48 + n) = own address + 32 + 16·LD; row 0: the zeros (15, 33 + n); rows 2, 3: block 2
@@ -461,21 +457,17 @@ template <int K>
 __device__ __forceinline__ void bcast_fold_bwd_k(double (&acc)[K], const double (&v)[K], const double* Lsq, int lane) {
   constexpr unsigned LD = WAVE + 1;
   const unsigned a0 = lds_addr(Lsq + lane * LD);
-  double b0[K], b1[K], b2[K], b3[K];
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-#ifdef MRBO_ROWBLOCKS2
-    row_blocks<0>(v[c], b0[c], b2[c]);
-    row_blocks<1>(v[c], b1[c], b3[c]);
-#else
-    row_blocks4(v[c], b0[c], b1[c], b2[c], b3[c]);
-#endif
-  }
   const int q = lane >> 4;
-  double m[K], f[K];
+  double b2[K], b3[K], m[K], f[K];
 #pragma unroll
   for (int c = 0; c < K; ++c) {
-    m[c] = (q == 2) ? b0[c] : b1[c];
+#ifdef MRBO_FOLD_SELECT
+    double b0, b1;
+    row_blocks4(v[c], b0, b1, b2[c], b3[c]);
+    m[c] = (q == 2) ? b0 : b1;
+#else
+    fold_blocks(v[c], false, b2[c], b3[c], m[c]);
+#endif
     f[c] = 0.0;
   }
   // row 2: (n, t) of output row t = lane − 32; row 3: the zeros (17 + n, 63); rows 0, 1: block 1
