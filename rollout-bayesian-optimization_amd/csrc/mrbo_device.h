@@ -350,6 +350,23 @@ __device__ __forceinline__ double fexp(double x) {
   const double k = __builtin_rint(x * sconst<0x652b82feu, 0x3ff71547u>());            // x·log2(e)
   double r = fma(sconst<0xfefa39efu, 0xbfe62e42u>(), k, x);                          // − k·ln2_hi
   r = fma(sconst<0x3b39803fu, 0xbc7abc9eu>(), k, r);                                 // − k·ln2_lo
+#ifdef MRBO_EXP_ESTRIN
+  // the same degree-11 polynomial P(r) = Σ c_k r^k (c0 = c1 = 1) in Estrin form: pairs
+  // b_j = c_{2j} + c_{2j+1} r, then q = b + r²·b', then P = q0 + r⁴(q1 + r⁴ q2) -- dependent
+  // depth 5 instead of 11, three more multiplies; not bit-identical to the device library's exp
+  const double r2 = r * r, r4 = r2 * r2;
+  double c10e = sconst<0xfca7ab0cu, 0x3e928af3u>();
+  asm volatile("" : "+v"(c10e));
+  const double b5 = fma(sconst<0x6a5dcb37u, 0x3e5ade15u>(), r, c10e);                 // c10 + c11 r
+  const double b4 = fma_sc(r, sconst<0x623fde64u, 0x3ec71deeu>(), sconst<0x7c89e6b0u, 0x3efa0199u>());   // c8 + c9 r
+  const double b3 = fma_sc(r, sconst<0x14761f6eu, 0x3f2a01a0u>(), sconst<0x1852b7b0u, 0x3f56c16cu>());
+  const double b2 = fma_sc(r, sconst<0x11122322u, 0x3f811111u>(), sconst<0x555502a1u, 0x3fa55555u>());
+  const double b1 = fma_sc(r, sconst<0x55555511u, 0x3fc55555u>(), sconst<0x0000000bu, 0x3fe00000u>());
+  const double b0 = r + 1.0;
+  const double q2 = fma(b5, r2, b4), q1 = fma(b3, r2, b2), q0 = fma(b1, r2, b0);
+  const double p = fma(fma(q2, r4, q1), r4, q0);
+  double e = __builtin_ldexp(p, (int)k);
+#else
   double c10 = sconst<0xfca7ab0cu, 0x3e928af3u>();
   asm volatile("" : "+v"(c10));   // one of the first step's two constants must live in VGPRs
   double p = fma(sconst<0x6a5dcb37u, 0x3e5ade15u>(), r, c10);
@@ -364,6 +381,7 @@ __device__ __forceinline__ double fexp(double x) {
   p = fma(r, p, 1.0);
   p = fma(r, p, 1.0);
   double e = __builtin_ldexp(p, (int)k);
+#endif
   e = (x > sconst<0u, 0x40900000u>()) ? __builtin_inf() : e;   // x > 1024
   e = (x < sconst<0u, 0xc090cc00u>()) ? 0.0 : e;               // x < −1075
   return e;
