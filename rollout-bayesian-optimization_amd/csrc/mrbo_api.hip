@@ -636,6 +636,12 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
       if (ks.gl) {     // backward copy (after all forward blocks): (i, j) at i·64 + j
         const size_t nblk = (size_t)P->RPL * (P->RPL + 1) / 2;
         packed[(nblk + blk) * 64 * 64 + (size_t)(i % 64) * 64 + j % 64] = Li[i + (size_t)N * j];
+        // the LDS-resident blocks (gl_lds_slot) once more, after both copies, in the LD = 65
+        // layout of the LDS kernels ((i, j) at j·65 + i), staged into LDS by every workgroup
+        const int nlb = (int)(ks.linv_doubles / (64 * 65));
+        const int slot = gl_lds_slot((int)blk);
+        if (slot >= 0 && slot < nlb)
+          packed[2 * nblk * 64 * 64 + (size_t)slot * 64 * 65 + (size_t)(j % 64) * 65 + i % 64] = Li[i + (size_t)N * j];
       }
     }
   hipDeviceProp_t prop;

@@ -32,6 +32,23 @@ constexpr int WAVE = 64;
 constexpr int MAXD = 16;   // widest input dimension of a cost model (mrbo_plan_create check)
 enum { COST_NONE = 0, COST_QUADRATIC = 1, COST_LOGLINEAR = 2 };   // mrbo_cost_t
 
+// N ≤ 256 (L0⁻¹ from L2, four rows per lane): blocks (1,0), (2,0), (2,1) of the block triangle
+// (packed indices 1, 3, 4) are also staged in workgroup LDS, in the LD = 65 layout of the N ≤ 128
+// kernel; their products read LDS instead of L2 (device and host agree through gl_lds_slot).
+// MRBO_GL_LDS_BLOCKS=0: every block from L2.  The chained / streamed A/B variants read L2 only.
+#ifndef MRBO_GL_LDS_BLOCKS
+#define MRBO_GL_LDS_BLOCKS 3
+#endif
+#if defined(MRBO_GL_CHAIN) || defined(MRBO_K1_STREAM)
+constexpr int GL_LDS_BLOCKS = 0;
+#else
+constexpr int GL_LDS_BLOCKS = MRBO_GL_LDS_BLOCKS;
+#endif
+static_assert(GL_LDS_BLOCKS >= 0 && GL_LDS_BLOCKS <= 3, "LDS-resident L2-layout blocks: 0..3");
+__host__ __device__ constexpr int gl_lds_slot(int b) {
+  return (b == 1 && GL_LDS_BLOCKS > 0) ? 0 : (b == 3 && GL_LDS_BLOCKS > 1) ? 1 : (b == 4 && GL_LDS_BLOCKS > 2) ? 2 : -1;
+}
+
 // evaluation modes (wave-uniform).  The front part (kernel rows, forward product, Gram, μ, σ,
 // EI and its gradient) runs in every mode but BACK; the back part (backward product w, and
 // the Hessian for FULL / RICH / BACK) resumes from state the front part left in LDS.

@@ -120,10 +120,16 @@ struct Lay {
   // by columns for the forward product, by rows for the backward one -- so that both row walks
   // are coalesced 512-byte loads
   static constexpr bool GL = (RPL > 2);
-  static constexpr long long LINV_DOUBLES = GL ? 0 : (((BC ? (long long)NBLK * BLK : linv_size(NR)) + 1) & ~1LL);
+  // GL with RPL = 4: NLB of the ten blocks (gl_lds_slot, mrbo_device.h) also live in workgroup LDS
+  // in the BC layout, shared by the workgroup's waves and read by the LDS register broadcast
+  // instead of from L2 (both directions, as the BC layout); the others stay L2-fed
+  static constexpr int NLB = (GL && RPL == 4) ? GL_LDS_BLOCKS : 0;
+  static constexpr long long LINV_DOUBLES = GL ? (long long)NLB * BLK : (((BC ? (long long)NBLK * BLK : linv_size(NR)) + 1) & ~1LL);
   // device image; GL: the NBLK blocks twice, 64×64 each with the lane index fastest -- forward
   // copy (i, j) at j·64 + i, backward copy (k, i) at k·64 + i -- zero-padded
-  static constexpr long long LINV_GLOBAL = GL ? 2LL * NBLK * WAVE * WAVE : LINV_DOUBLES;
+  static constexpr long long LINV_GLOBAL = GL ? 2LL * NBLK * WAVE * WAVE + (long long)NLB * BLK : LINV_DOUBLES;
+  // where the LDS staging copy starts in the device image (GL: after the two global copies)
+  static constexpr long long LINV_LDS_SRC = GL ? 2LL * NBLK * WAVE * WAVE : 0;
 };
 // scalar slots in U_SC
 enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, SC_GSIG = 6, SC_GMUMU = 7,
@@ -180,6 +186,7 @@ struct WaveCtx {
   double* U;            // LDS: U_SIZE
   const double* Linv;   // L0⁻¹: LDS blocks (BC) or the forward copy of the global blocks (GL)
   const double* LinvT;  // GL: the backward copy of the global L0⁻¹ blocks
+  const double* LinvL;  // GL: the LDS-resident blocks (Lay::NLB of them, BC layout), or null
   const double* XS;     // inner-solve start points: LDS copy (kp.xs_lds) or kp.xstarts
   const double* KXB;    // ψ(|clamp(x_k) − X_i|) (kp.batch): LDS [NR][nstarts]; packed layouts: global [nstarts][NR]
   const double* GTAB;   // [nstarts][NG]: base Gram of the start points (kp.batch; LDS, global for packed)
@@ -715,6 +722,22 @@ __device__ __forceinline__ void gl_bcast_product(double (&acc)[K], const double 
   }
 }
 
+// One block of an L2-fed (GL) product, from LDS where the block is LDS-resident (gl_lds_slot) and
+// from L2 otherwise.  Both walks sum rows 0-15, 32-47, 16-31, 48-63 in order: bit-identical.
+// Forward: block (s, t), lane i reads (i, j); backward: block (t, s) of the backward copy, lane i
+// reads (k, i) -- in LDS the same BC block walked with stride 1 from lane·LD.
+template <int K, int LD, int NLB>
+__device__ __forceinline__ void gl_block(double (&acc)[K], const double (&v)[K], const double* Lg, const double* LinvL,
+                                         int b, bool fwd, int lane, int nrows) {
+  const int li = NLB > 0 ? gl_lds_slot(b) : -1;
+  if (li >= 0) {
+    if (fwd) bcast_product<K, LD>(acc, v, LinvL + (long long)li * WAVE * LD + lane, nrows);
+    else bcast_product<K, 1>(acc, v, LinvL + (long long)li * WAVE * LD + lane * LD, nrows);
+  } else {
+    gl_bcast_product<K>(acc, v, Lg + (long long)b * WAVE * WAVE + lane, nrows);
+  }
+}
+
 template <int D, int RPL, int HW>
 __device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL, HW>& W, const KParams& kp);
 
@@ -950,7 +973,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
 #pragma unroll
         for (int t = 0; t <= s; ++t) {
           const double v1[1] = {Bown[t][0]};
-          gl_bcast_product<1>(a1, v1, L0 + Ly::blk(s, t) * WAVE * WAVE, nrows(t));
+          gl_block<1, Ly::LD, Ly::NLB>(a1, v1, W.Linv, W.LinvL, Ly::blk(s, t), true, lane, nrows(t));
         }
         acc[s][0] = a1[0];
       }
@@ -966,7 +989,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
           double vg[D];
 #pragma unroll
           for (int a = 0; a < D; ++a) vg[a] = Bown[t][1 + a];
-          gl_bcast_product<D>(ag, vg, L0 + Ly::blk(s, t) * WAVE * WAVE, nrows(t));
+          gl_block<D, Ly::LD, Ly::NLB>(ag, vg, W.Linv, W.LinvL, Ly::blk(s, t), true, lane, nrows(t));
         }
 #pragma unroll
         for (int a = 0; a < D; ++a) acc[s][1 + a] = ag[a];
@@ -977,7 +1000,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
       for (int s = 0; s < RPL; ++s)
 #pragma unroll
         for (int t = 0; t <= s; ++t)
-          gl_bcast_product<D1>(acc[s], Bown[t], L0 + Ly::blk(s, t) * WAVE * WAVE, nrows(t));
+          gl_block<D1, Ly::LD, Ly::NLB>(acc[s], Bown[t], W.Linv, W.LinvL, Ly::blk(s, t), true, lane, nrows(t));
     }
 #endif
   }
@@ -1301,7 +1324,8 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
 #pragma unroll
           for (int c = 0; c < D1; ++c) a7[c] = 0.0;
 #pragma unroll
-          for (int t = s; t < RPL; ++t) gl_bcast_product<D1>(a7, acc[t], LT + Ly::blk(t, s) * WAVE * WAVE, nrows(t));
+          for (int t = s; t < RPL; ++t)
+            gl_block<D1, Ly::LD, Ly::NLB>(a7, acc[t], W.LinvT, W.LinvL, Ly::blk(t, s), false, lane, nrows(t));
           wv[s] = a7[0];
 #pragma unroll
           for (int a = 0; a < D; ++a) pv[s][a] = a7[1 + a];
@@ -1310,7 +1334,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
 #pragma unroll
           for (int t = s; t < RPL; ++t) {
             const double v1[1] = {acc[t][0]};
-            gl_bcast_product<1>(a1, v1, LT + Ly::blk(t, s) * WAVE * WAVE, nrows(t));
+            gl_block<1, Ly::LD, Ly::NLB>(a1, v1, W.LinvT, W.LinvL, Ly::blk(t, s), false, lane, nrows(t));
           }
           wv[s] = a1[0];
         }
@@ -2757,6 +2781,7 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL, HW>& W, const KParams
   W.G12 = W.U + Ly::U_SIZE;
   W.Linv = Ly::GL ? kp.Linv : smem;
   W.LinvT = kp.Linv + (long long)Ly::NBLK * WAVE * WAVE;   // GL: backward copy
+  W.LinvL = smem;                                            // GL: LDS-resident blocks
   const long long slot = (long long)blockIdx.x * (blockDim.x / WAVE) + wave_in_block;
   if constexpr (Ly::SQ) W.E = W.G12 + Ly::G12;
   else W.E = kp.work + slot * kp.work_stride;
@@ -2823,7 +2848,7 @@ __global__ void __launch_bounds__((KBounds<D, RPL, HW>::threads), (KBounds<D, RP
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // stage L0⁻¹ (and the inner-solve start points) once per workgroup (the only block barrier)
   using Ly = Lay<D, RPL, HW>;
-  for (int q = threadIdx.x; q < (int)Ly::LINV_DOUBLES; q += blockDim.x) smem[q] = kp.Linv[q];
+  for (int q = threadIdx.x; q < (int)Ly::LINV_DOUBLES; q += blockDim.x) smem[q] = kp.Linv[Ly::LINV_LDS_SRC + q];
   if (kp.xs_lds)
     for (int q = threadIdx.x; q < kp.nstarts * D; q += blockDim.x) smem[Ly::LINV_DOUBLES + q] = kp.xstarts[q];
   __syncthreads();
@@ -2960,7 +2985,7 @@ template <int D, int RPL, int HW = 1>
 __global__ void __launch_bounds__((KBounds<D, RPL, HW>::threads), (KBounds<D, RPL, HW>::waves_per_simd)) eval_base_kernel(KParams kp) {
   using Ly = Lay<D, RPL, HW>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  for (int q = threadIdx.x; q < (int)Ly::LINV_DOUBLES; q += blockDim.x) smem[q] = kp.Linv[q];
+  for (int q = threadIdx.x; q < (int)Ly::LINV_DOUBLES; q += blockDim.x) smem[q] = kp.Linv[Ly::LINV_LDS_SRC + q];
   __syncthreads();
   WaveCtx<D, RPL, HW> W;
   wave_setup<D, RPL, HW>(W, kp, smem, threadIdx.x / WAVE);
