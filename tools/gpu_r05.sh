@@ -14,6 +14,7 @@
 #   shim      tools/shim_rate.py at C3 (the Julia drop-in's call patterns)
 #   c2        C2 bench line (20 steps)
 #   myopic    myopic BO diagnostics: seeds, solve margins, no-repeat pick (4 cases, 60 trials)
+#   c5        C5 at ℓ = 1 (2 048 × 512) and ℓ = 20 (64 × 64)
 #   c5cost    C5 + NonUniformCost at M = 256, R = 128 (one step)
 #   prof      rocprofv3 --kernel-trace --stats of the default bench (1 step) + FETCH_SIZE / WRITE_SIZE
 #             passes (tools/profile.sh), C3 and C3-MLE
@@ -93,6 +94,15 @@ for l in open(sys.argv[1]):
         timeout -k 10 300 python -u tools/bo_compare.py --trials 60 --cases $cases $args \
           --out "$out/bo_myopic_$vt.jsonl" > /dev/null 2> "$out/bo_myopic_$vt.err" || { rc=$?; break; }
         grep "final gap" "$out/bo_myopic_$vt.err"
+      done ;;
+    c5)
+      timeout -k 10 300 python -u bench.py --config C5 --mc-per-gpu 2048 --steps 2 --warmup 1 --no-cpu-baseline \
+        > "$out/bench_c5.json" 2> "$out/bench_c5.err" && \
+      timeout -k 10 300 python -u bench.py --config C5 --mc-per-gpu 64 --restarts 64 --ell 20 --steps 3 --warmup 1 --no-cpu-baseline \
+        > "$out/bench_c5_l20.json" 2> "$out/bench_c5_l20.err"
+      rc=$?
+      for f in "$out"/bench_c5.json "$out"/bench_c5_l20.json; do
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1].split('/')[-1], d['value'], d['roofline']['frac'], d['roofline']['kernel_ms'], d['work_per_traj'])" "$f"
       done ;;
     c5cost)
       timeout -k 10 400 python -u bench.py --config C5 --cost --mc-per-gpu 256 --restarts 128 --steps 1 --warmup 1 --no-cpu-baseline \
