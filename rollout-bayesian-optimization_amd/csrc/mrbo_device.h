@@ -45,8 +45,17 @@ constexpr int GL_LDS_BLOCKS = 0;
 constexpr int GL_LDS_BLOCKS = MRBO_GL_LDS_BLOCKS;
 #endif
 static_assert(GL_LDS_BLOCKS >= 0 && GL_LDS_BLOCKS <= 3, "LDS-resident L2-layout blocks: 0..3");
+#ifdef MRBO_GL_LDS_DIAG
+// A/B: the diagonal blocks (0,0), (1,1), (2,2) instead, walked by the folded LDS products
+constexpr int GL_LDS_B0 = 0, GL_LDS_B1 = 2, GL_LDS_B2 = 5;
+constexpr bool GL_LDS_FOLD = true;
+#else
+constexpr int GL_LDS_B0 = 1, GL_LDS_B1 = 3, GL_LDS_B2 = 4;
+constexpr bool GL_LDS_FOLD = false;
+#endif
 __host__ __device__ constexpr int gl_lds_slot(int b) {
-  return (b == 1 && GL_LDS_BLOCKS > 0) ? 0 : (b == 3 && GL_LDS_BLOCKS > 1) ? 1 : (b == 4 && GL_LDS_BLOCKS > 2) ? 2 : -1;
+  return (b == GL_LDS_B0 && GL_LDS_BLOCKS > 0) ? 0 : (b == GL_LDS_B1 && GL_LDS_BLOCKS > 1) ? 1
+       : (b == GL_LDS_B2 && GL_LDS_BLOCKS > 2) ? 2 : -1;
 }
 
 // evaluation modes (wave-uniform).  The front part (kernel rows, forward product, Gram, μ, σ,

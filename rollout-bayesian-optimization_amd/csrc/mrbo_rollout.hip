@@ -731,8 +731,15 @@ __device__ __forceinline__ void gl_block(double (&acc)[K], const double (&v)[K],
                                          int b, bool fwd, int lane, int nrows) {
   const int li = NLB > 0 ? gl_lds_slot(b) : -1;
   if (li >= 0) {
-    if (fwd) bcast_product<K, LD>(acc, v, LinvL + (long long)li * WAVE * LD + lane, nrows);
-    else bcast_product<K, 1>(acc, v, LinvL + (long long)li * WAVE * LD + lane * LD, nrows);
+    const double* sq = LinvL + (long long)li * WAVE * LD;
+    if (GL_LDS_FOLD) {   // a diagonal block: the folded three-pass products of the N ≤ 64 kernel
+      if (fwd) bcast_fold_fwd<K>(acc, v, sq, lane);
+      else bcast_fold_bwd<K>(acc, v, sq, lane);
+    } else if (fwd) {
+      bcast_product<K, LD>(acc, v, sq + lane, nrows);
+    } else {
+      bcast_product<K, 1>(acc, v, sq + lane * LD, nrows);
+    }
   } else {
     gl_bcast_product<K>(acc, v, Lg + (long long)b * WAVE * WAVE + lane, nrows);
   }
