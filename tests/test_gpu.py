@@ -281,6 +281,32 @@ def test_half_wave_kernel_equals_full_wave(gpu, monkeypatch, name, M, R):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("d,N,h", [(1, 7, 1), (2, 20, 2), (2, 29, 3)])
+def test_half_wave_kernel_ragged_sizes(gpu, monkeypatch, d, N, h):
+    """The half-wave kernel at ragged N (rows N..31 of each half padded), h = 1..3 on Ackley(d) at
+    the design-spacing lengthscale: the same bars as the full-wave comparison.  The default library
+    carries the FMAX = 4 units (and so the half-wave kernel) for d = 1, 2 of the d ≤ 4 it is built
+    for (__graft_entry__.F4_DIMS).  A plan with more than 32 inner starts keeps the full-wave kernel
+    (one lane per start in a half)."""
+    ell = 0.6 * 65.536 * N ** (-1.0 / d)
+    g = _problem_arrays(None, 32, 2, testfn="ackley", d=d, N=N, h=h, ell=ell)
+    p_half = _plan(g)
+    assert p_half.info()["spec"] == 2
+    r_half = _run(p_half, g)
+    monkeypatch.setenv("MRBO_HALF", "0")
+    r_full = _run(_plan(g), g)
+    assert (r_half["status"] == 0).all() and (r_full["status"] == 0).all()
+    np.testing.assert_array_equal(r_half["evals"], r_full["evals"])
+    for k in ("values", "obs", "policy_x"):
+        np.testing.assert_allclose(r_half[k], r_full[k], rtol=1e-12, atol=1e-15, err_msg=k)
+    for k in ("grad_x", "grad_theta"):
+        _assert_grads_close(r_half[k], r_full[k], rtol=1e-10)
+    monkeypatch.delenv("MRBO_HALF")
+    xs = np.asfortranarray(np.tile(g["xstarts"], (1, 3))[:, :33])
+    assert _plan(dict(g, xstarts=xs)).info()["spec"] == 1
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name,M,R", [("C3", 32, 4), ("C4", 8, 2)])
 def test_work_order_changes_nothing_but_the_schedule(gpu, name, M, R):
     """mrbo_plan_set_order only reorders the work queue: a reversed permutation and the
