@@ -281,13 +281,12 @@ def test_half_wave_kernel_equals_full_wave(gpu, monkeypatch, name, M, R):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d,N,h", [(1, 7, 1), (2, 20, 2), (2, 29, 3)])
+@pytest.mark.parametrize("d,N,h", [(1, 7, 1), (2, 20, 2), (3, 24, 2), (4, 32, 3)])
 def test_half_wave_kernel_ragged_sizes(gpu, monkeypatch, d, N, h):
     """The half-wave kernel at ragged N (rows N..31 of each half padded), h = 1..3 on Ackley(d) at
-    the design-spacing lengthscale: the same bars as the full-wave comparison.  The default library
-    carries the FMAX = 4 units (and so the half-wave kernel) for d = 1, 2 of the d ≤ 4 it is built
-    for (__graft_entry__.F4_DIMS).  A plan with more than 32 inner starts keeps the full-wave kernel
-    (one lane per start in a half)."""
+    the design-spacing lengthscale: the same bars as the full-wave comparison (the default library
+    carries the FMAX = 4 units, which hold the half-wave kernel, for d = 1..4: __graft_entry__.F4_DIMS).
+    A plan with more than 32 inner starts keeps the full-wave kernel (one lane per start in a half)."""
     ell = 0.6 * 65.536 * N ** (-1.0 / d)
     g = _problem_arrays(None, 32, 2, testfn="ackley", d=d, N=N, h=h, ell=ell)
     p_half = _plan(g)
