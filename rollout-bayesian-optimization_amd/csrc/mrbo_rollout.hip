@@ -873,6 +873,13 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
     auto nrows = [&](int t) { const int n = N - WAVE * t; return n < WAVE ? n : WAVE; };
     // RPL = 1 with N > 48: the folded three-pass products (bcast_fold_fwd / _bwd)
     const bool fold = FOLD && Ly::SQ && HW == 1 && N > 48;
+    // N ≤ 128 (two rows per lane): the diagonal blocks (s, s) by the same folded products
+    // (MRBO_BC_DIAG_FOLD, A/B)
+#ifdef MRBO_BC_DIAG_FOLD
+    constexpr bool DFOLD = !Ly::SQ && HW == 1;
+#else
+    constexpr bool DFOLD = false;
+#endif
     if (mode == EV_VALUE) {
 #pragma unroll
       for (int s = 0; s < RPL; ++s) {
@@ -881,6 +888,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
         for (int t = 0; t <= s; ++t) {
           const double v1[1] = {Bown[t][0]};
           if (fold) bcast_fold_fwd<1>(a1, v1, W.Linv, lane);
+          else if (DFOLD && s == t && nrows(t) > 48) bcast_fold_fwd<1>(a1, v1, W.Linv + Ly::blk(s, t) * Ly::BLK, lane);
           else bcast_product<1, Ly::LD, HW>(a1, v1, W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
         }
         acc[s][0] = a1[0];
@@ -899,6 +907,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
 #pragma unroll
           for (int a = 0; a < D; ++a) vg[a] = Bown[t][1 + a];
           if (fold) bcast_fold_fwd<D>(ag, vg, W.Linv, lane);
+          else if (DFOLD && s == t && nrows(t) > 48) bcast_fold_fwd<D>(ag, vg, W.Linv + Ly::blk(s, t) * Ly::BLK, lane);
           else bcast_product<D, Ly::LD, HW>(ag, vg, W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
         }
 #pragma unroll
@@ -911,6 +920,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
 #pragma unroll
         for (int t = 0; t <= s; ++t) {
           if (fold) bcast_fold_fwd<D1>(acc[s], Bown[t], W.Linv, lane);
+          else if (DFOLD && s == t && nrows(t) > 48) bcast_fold_fwd<D1>(acc[s], Bown[t], W.Linv + Ly::blk(s, t) * Ly::BLK, lane);
           else bcast_product<D1, Ly::LD, HW>(acc[s], Bown[t], W.Linv + Ly::blk(s, t) * Ly::BLK + lane, nrows(t));
         }
     }
@@ -1259,6 +1269,11 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
       // t = s..RPL-1; rows k of Y are broadcast from register slot t
       auto nrows = [&](int t) { const int n = N - WAVE * t; return n < WAVE ? n : WAVE; };
       const bool fold = FOLD && Ly::SQ && HW == 1 && N > 48;
+#ifdef MRBO_BC_DIAG_FOLD
+      constexpr bool DFOLD = !Ly::SQ && HW == 1;
+#else
+      constexpr bool DFOLD = false;
+#endif
 #pragma unroll
       for (int s = 0; s < RPL; ++s) {
         if (rich) {
@@ -1268,6 +1283,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
 #pragma unroll
           for (int t = s; t < RPL; ++t) {
             if (fold) bcast_fold_bwd<D1>(a7, acc[t], W.Linv, lane);
+            else if (DFOLD && s == t && nrows(t) > 48) bcast_fold_bwd<D1>(a7, acc[t], W.Linv + Ly::blk(t, s) * Ly::BLK, lane);
             else bcast_product<D1, 1, HW>(a7, acc[t], W.Linv + Ly::blk(t, s) * Ly::BLK + lane * Ly::LD, nrows(t));
           }
           wv[s] = a7[0];
@@ -1279,6 +1295,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
           for (int t = s; t < RPL; ++t) {
             const double v1[1] = {acc[t][0]};
             if (fold) bcast_fold_bwd<1>(a1, v1, W.Linv, lane);
+            else if (DFOLD && s == t && nrows(t) > 48) bcast_fold_bwd<1>(a1, v1, W.Linv + Ly::blk(t, s) * Ly::BLK, lane);
             else bcast_product<1, 1, HW>(a1, v1, W.Linv + Ly::blk(t, s) * Ly::BLK + lane * Ly::LD, nrows(t));
           }
           wv[s] = a1[0];
