@@ -13,7 +13,11 @@
 #include <utility>
 
 #include "mrbo_device.h"
+#ifdef MRBO_BCAST_HEADER   // A/B: an alternative generated header (tools/gen_bcast_asm.py BCAST_OUT=…)
+#include MRBO_BCAST_HEADER
+#else
 #include "bcast_asm.h"
+#endif
 
 #ifndef MRBO_WAVES_PER_SIMD
 #define MRBO_WAVES_PER_SIMD 2
