@@ -208,6 +208,21 @@ struct WaveCtx {
   // every non-periodic radial function and both derivative factors are exactly 0 (exp underflows),
   // and their c, w, E, P entries are 0 as well -- so for those kernels no select is needed: true at
   // compile time in the Matérn-5/2 specialisation.  The Periodic kernel keeps the per-row mask.
+  // base covariate a of row slot s.  MRBO_X0_GLOBAL (A/B, N ≤ 256 layout): read from the L2-resident
+  // device copy at each use instead of holding 4·d registers per lane across the trajectory
+  __device__ __forceinline__ double x0(const KParams& kp, int s, int a) const {
+#ifdef MRBO_X0_GLOBAL
+    if constexpr (Ly::GL) {
+      const double v = kp.X0[(long long)a * Ly::NR + lane + WAVE * s];
+#ifndef MRBO_NO_PAD_FAR
+      return (valid[s] || kp.kernel == KERNEL_PERIODIC) ? v : PAD_FAR;
+#else
+      return v;
+#endif
+    }
+#endif
+    return X0[s][a];
+  }
   __device__ __forceinline__ bool rowv(const KParams& kp, int s) const {
 #ifdef MRBO_NO_PAD_FAR
     return valid[s];
@@ -806,7 +821,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
   for (int s = 0; s < RPL; ++s) {
     double r[D], rho2 = 0.0;
 #pragma unroll
-    for (int a = 0; a < D; ++a) { r[a] = x[a] - W.X0[s][a]; rho2 = fma(r[a], r[a], rho2); }
+    for (int a = 0; a < D; ++a) { r[a] = x[a] - W.x0(kp, s, a); rho2 = fma(r[a], r[a], rho2); }
     if (rows_kept) {
       const double g1 = W.G12[3 * (lane + WAVE * s)];
       const bool v = W.rowv(kp, s);
@@ -1413,7 +1428,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
 #pragma unroll
     for (int s = 0; s < RPL; ++s) {
 #pragma unroll
-      for (int a = 0; a < D; ++a) nv[s][a] = x[a] - W.X0[s][a];
+      for (int a = 0; a < D; ++a) nv[s][a] = x[a] - W.x0(kp, s, a);
       const double coef = W.rowv(kp, s) ? (e.gmu * lr.cb[s] - gsig_over * lr.w[s]) : 0.0;
       ca[s] = coef * W.G12[3 * (lane + WAVE * s) + 1];
       tb[s] = coef * W.G12[3 * (lane + WAVE * s)];
@@ -1828,7 +1843,7 @@ __device__ __forceinline__ bool tight_certified(WaveCtx<D, RPL, HW>& W, const KP
   for (int s = 0; s < RPL; ++s) {
     double rho2 = 0.0;
 #pragma unroll
-    for (int a = 0; a < D; ++a) { const double r = x[a] - W.X0[s][a]; rho2 = fma(r, r, rho2); }
+    for (int a = 0; a < D; ++a) { const double r = x[a] - W.x0(kp, s, a); rho2 = fma(r, r, rho2); }
     double psi, g1, g2;
     if constexpr (ROWS_KEPT) g1 = W.G12[3 * (lane + WAVE * s)];
     else rad_eval(W.rad, rho2, psi, g1, g2);
@@ -2372,7 +2387,7 @@ __device__ __forceinline__ void adjoint_pair(WaveCtx<D, RPL, HW>& W, const KPara
   for (int s = 0; s < RPL; ++s) {
     double r[D], rho2 = 0.0;
 #pragma unroll
-    for (int a = 0; a < D; ++a) { r[a] = Xq[a] - W.X0[s][a]; rho2 = fma(r[a], r[a], rho2); }
+    for (int a = 0; a < D; ++a) { r[a] = Xq[a] - W.x0(kp, s, a); rho2 = fma(r[a], r[a], rho2); }
     double psi, g1, g2;
     rad_eval(W.rad, rho2, psi, g1, g2);
 #pragma unroll
