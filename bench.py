@@ -38,6 +38,15 @@ METRIC = "rollout trajectories/sec (MC samples × restarts) at horizon h=3, n=64
 KERNEL_BOUNDS = ([0.1], [5.0])   # optimize!(sur, lowerbounds=kernel_lbs, ...) nonmyopic_bayesopt.jl:230,285
 
 
+
+def kernel_label(d, info):
+    """The rollout kernel's name as rocprofv3 prints it: plan info spec 0 = generic <D, RPL, 0>,
+    1 = Matérn-5/2 + EI <D, RPL, 1>, 2 = the half-wave kernel <D, 1, 1, 2>, 3 = Matérn-5/2 + EI +
+    quadratic cost <D, RPL, 2>; the unit's fantasy capacity names the namespace (fmax4 / fmax6)."""
+    rpl, spec = info["rpl"], info["spec"]
+    targs = {0: f"{d}, {rpl}, 0, 1", 1: f"{d}, {rpl}, 1, 1", 2: f"{d}, 1, 1, 2", 3: f"{d}, {rpl}, 2, 1"}[spec]
+    return f"mrbo::fmax{info['fmax']}::rollout_kernel<{targs}>"
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -348,7 +357,7 @@ def main():
                    "schedule": "longest first (first step's work counters)" if longest_first else "index order"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": f"rollout_kernel<{d},{info['rpl']},{info['spec']}>", "kernel_ms": kms, "flops_per_launch": fl,
+                     "kernel": kernel_label(d, info), "kernel_ms": kms, "flops_per_launch": fl,
                      "kernel_ms_launches": len(kernel_ms),   # the plan keeps the last 64 launches' events
                      "launch": info,
                      "note": "compute-bound fp64: peak = the dense fp64 matrix peak, equal to the fp64 vector "

@@ -10,6 +10,8 @@
  *                          rollout.jl:279-340 -- batched over R restarts (the x0 batch of the
  *                          outer ascent, utils.jl:97-106 / stochastic_solve utils.jl:235-265)
  *   mrbo_eto_reduce        the mean / std(n-1) tail of simulate_trajectory_mc, rollout.jl:328-339
+ *   mrbo_stochastic_solve  stochastic_solve utils.jl:235-265 (eswavs + StandardSGA / Adam update!)
+ *                          over a restart batch, the whole ascent in one call
  *   mrbo_eval_base         eval(s::Surrogate, x, θ) radial_basis_surrogates.jl:224-310 (μ, σ, ∇, Hα)
  *   mrbo_rnstream          gen_low_discrepancy_sequence utils.jl:65-74 (Sobol→Box–Muller(log10))
  *   mrbo_initial_guesses   generate_initial_guesses utils.jl:145-153
@@ -120,9 +122,12 @@ typedef struct {
   double sigma_tol;     /* EI / POI σtol (decision_rules.jl:84, :102) = 1e-8     */
   uint64_t seed;        /* δx for solve_dual_y (rollout.jl:133) when dual_y_dx == NULL */
   int32_t sample_offset;/* global index of this plan's first MC sample (multi-GPU shard), 0 */
-  int32_t samples_total;/* global MC samples per restart (0 → M); informational: the δx     */
-                        /* counter RNG is keyed by the global sample index alone (round 5),*/
-                        /* so restart r of a launch equals an R = 1 launch at its x0       */
+  int32_t samples_total;/* DEPRECATED, ignored (kept for the struct layout).  The δx counter */
+                        /* RNG is keyed by the global sample index sample_offset + m alone */
+                        /* (round 5), so all R restarts of a launch share the δx of sample */
+                        /* m, and restart r equals an R = 1 launch at its x0.  The         */
+                        /* reference draws a fresh rand(dim) per solve_dual_y call         */
+                        /* (rollout.jl:133): restarts are NOT decorrelated. */
   int32_t cost;         /* mrbo_cost_t: NonUniformCost weighting of the inner-solve rule      */
   double cost_c0;       /* cost family parameter c0                                          */
   const double* cost_w; /* d weights, HOST (NULL with MRBO_COST_NONE)                        */
@@ -200,6 +205,40 @@ int mrbo_adam_step(mrbo_plan_t* plan, const double* eto, double* x0s, int32_t* a
                    double sample_size, double eta, double beta1, double beta2, double eps, uint32_t flags,
                    void* stream);
 
+/* The reference's outer loop in ONE call: stochastic_solve(; optimizer, surrogate, tp, es, start)
+ * (utils.jl:235-265) for the plan's R restarts at once -- the columns of x0s, e.g. the
+ * generate_batch points (utils.jl:97-106) -- on the plan's surrogate, TrajectoryParameters and
+ * inner starts.  Each iteration is [mrbo_simulate_mc at the current x0s, mrbo_eto_reduce,
+ * mrbo_sga_step (StandardSGA update!, optimizers.jl:16-22) or mrbo_adam_step (Adam update!,
+ * optimizers.jl:49-74)], at most opts->iterations (the reference: 50) times.  A restart stops
+ * for good when its eswavs test (utils.jl:114-123) fires, as the reference's `break`; the call
+ * returns once no restart is active (read back a few iterations behind the launches: the
+ * iterations queued after the last stop find x0 unchanged and reproduce the same outputs) or the
+ * budget is spent.  No host round trip per iteration, one plan, no plan rebuild.
+ *   x0s      d×R in: the starts, out: get_starting_point(tpc) of every restart
+ *   rnstream, xstarts, dual_y_dx   as mrbo_simulate_mc (dual_y_dx may be NULL)
+ *   eto      R×W or NULL: the ETO rows (mrbo_eto_reduce's layout) of the last launch -- for a
+ *            stopped restart, those at its final point
+ *   active   R or NULL: 1 where eswavs never stopped the restart within the budget
+ *   result   int32[3]: iterations launched, the iteration after which no restart was active (or
+ *            the iterations launched), the OR of every launch's trajectory status bits (non-zero:
+ *            the reference would have thrown -- the Julia method throws)
+ * Arrays are device pointers unless MRBO_FLAG_HOST_POINTERS (then staged once for the whole
+ * ascent); synchronises `stream` before returning.                                            */
+typedef enum { MRBO_OPT_SGA = 0, MRBO_OPT_ADAM = 1 } mrbo_optimizer_t;
+typedef struct {
+  int32_t optimizer;    /* mrbo_optimizer_t                                                  */
+  int32_t iterations;   /* ≥ 1; the reference's loop: 50                                      */
+  double eta;           /* StandardSGA η (default 0.01) / Adam η (default 0.001)              */
+  double beta1;         /* Adam β1 (0.9); ignored by StandardSGA                              */
+  double beta2;         /* Adam β2 (0.999)                                                    */
+  double eps;           /* Adam ε (1e-8)                                                      */
+  double sample_size;   /* eswavs sample size: global MC samples per restart (0 → the plan's M) */
+} mrbo_solve_opts_t;
+int mrbo_stochastic_solve(mrbo_plan_t* plan, double* x0s, const double* rnstream, const double* xstarts,
+                          const double* dual_y_dx, const mrbo_solve_opts_t* opts, double* eto, int32_t* active,
+                          int32_t* result, uint32_t flags, void* stream);
+
 /* Shard moments for the multi-GPU exchange: moments R×(2+2d+2) = [Σα, M2α, Σ∇x(d), M2∇x(d), Σ∇θ, M2∇θ]
  * over the first M_local samples of each restart (the outputs keep the plan's M as the restart
  * stride; 1 ≤ M_local ≤ M), M2 = Σ(x − x̄_local)² by two passes.  Ranks all-gather
@@ -274,8 +313,9 @@ int mrbo_kernel_times(mrbo_plan_t* plan, int32_t n, double* ms);
 double mrbo_last_gp_fit_ms(void);
 
 /* Launch geometry of a plan (no reference counterpart; measurement and FLOP accounting):
- * info[0..5] = rows per lane (1/2/4), workgroups, waves per workgroup, batched start values
- * (0/1), compile-time specialised kernel (0 generic, 1 Matérn-5/2 + EI, 2 its half-wave form: N ≤ 32, d ≤ 4, h ≤ 3, 3 Matérn-5/2 + EI + quadratic cost), LDS bytes per workgroup.  Writes min(n, 6). */
+ * info[0..6] = rows per lane (1/2/4), workgroups, waves per workgroup, batched start values
+ * (0/1), compile-time specialised kernel (0 generic, 1 Matérn-5/2 + EI, 2 its half-wave form: N ≤ 32, d ≤ 4, h ≤ 3, 3 Matérn-5/2 + EI + quadratic cost), LDS bytes per workgroup,
+ * fantasy capacity of the kernel unit (4: the FMAX = 4 units of h ≤ 3, d ≤ 8; else 6).  Writes min(n, 7). */
 int mrbo_plan_info(const mrbo_plan_t* plan, int32_t* info, int32_t n);
 
 /* Work order of the plan's later mrbo_simulate_mc / mrbo_simulate_ghq launches (no reference

@@ -59,7 +59,7 @@ struct mrbo_plan {
   double* dubs = nullptr;
   double* dcost = nullptr;  // NonUniformCost table [lb (d), ub − lb (d), w (d)] (cost models only)
   double* dwork = nullptr;
-  double* dytab = nullptr;  // batched starts: per-workgroup Y0(x_start) slices (square layout)
+  double* dytab = nullptr;  // batched starts: the launch's Y0(x_start) table (square layout, ytab_kernel)
   double* dkxb = nullptr;   // batched starts, packed layouts: global start tables (start_tables_kernel)
   double* dgtab = nullptr;
   long long work_stride = 0;
@@ -82,6 +82,12 @@ struct mrbo_plan {
   // MRBO_FLAG_HOST_POINTERS staging: device buffers kept across calls, one slot per staged
   // argument in call order, grown on demand and freed with the plan
   std::vector<std::pair<void*, size_t>> stage;
+  // mrbo_stochastic_solve: the outer ascent's device state (one slot per buffer, grown on demand),
+  // a pinned ring of per-iteration checks read back behind the launches, and its events
+  std::vector<std::pair<void*, size_t>> solve;
+  static constexpr int NCHK = 8;
+  int32_t* hchk = nullptr;   // pinned, 2 × NCHK: [status bits of the iteration, restarts still active]
+  hipEvent_t chk_ev[NCHK] = {};
 };
 
 namespace {
@@ -119,6 +125,16 @@ bool get_kset(int d, int rpl, int fx, KernelSet& ks) {
 void launch_tables(int d, int rpl, int fx, int nstarts, hipStream_t st, const KParams& kp) {
 #define K6(DD) case DD: launch_tables_d##DD(rpl, nstarts, st, kp); return;
 #define K4(DD) case DD: launch_tables_d##DD##_f4(rpl, nstarts, st, kp); return;
+  if (fx) { switch (d) { MRBO_FOR_DF4(K4) default: return; } }
+  switch (d) { MRBO_FOR_D(K6) default: return; }
+#undef K6
+#undef K4
+}
+
+// the Y0 table of the square layouts (rpl 1) with batched starts, before a rollout launch
+void launch_ytab(int d, int fx, int spec, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
+#define K6(DD) case DD: launch_ytab_d##DD(spec, b, sm, st, kp); return;
+#define K4(DD) case DD: launch_ytab_d##DD##_f4(spec, b, sm, st, kp); return;
   if (fx) { switch (d) { MRBO_FOR_DF4(K4) default: return; } }
   switch (d) { MRBO_FOR_D(K6) default: return; }
 #undef K6
@@ -297,6 +313,35 @@ __global__ void __launch_bounds__(64) merge_kernel(const double* moments, int ns
   double* e = eto + (size_t)W * r;
   e[c0] = sm / n;
   e[c1] = n > 1.0 ? sqrt(q / (n - 1.0)) : __builtin_nan("");
+}
+
+// mrbo_stochastic_solve's per-iteration check: the OR of the launch's trajectory status bits and
+// the count of restarts still active after the step, into chk[0..1] (one workgroup)
+__global__ void __launch_bounds__(256) solve_check_kernel(const int* status, long long T, const int* active, int R,
+                                                         int* chk) {
+  __shared__ int sb[256], sa[256];
+  int b = 0, a = 0;
+  for (long long t = threadIdx.x; t < T; t += blockDim.x) b |= status[t];
+  for (int r = threadIdx.x; r < R; r += blockDim.x) a += active[r] != 0;
+  sb[threadIdx.x] = b;
+  sa[threadIdx.x] = a;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      sb[threadIdx.x] |= sb[threadIdx.x + w];
+      sa[threadIdx.x] += sa[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    chk[0] = sb[0];
+    chk[1] = sa[0];
+  }
+}
+
+__global__ void __launch_bounds__(64) fill_int_kernel(int* a, int n, int v) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i < n) a[i] = v;
 }
 
 // ---- host Sobol (Joe-Kuo directions, Gray code, zero point skipped) ---------------------
@@ -704,7 +749,7 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
             hipMalloc(&P->dubs, sizeof(double) * d) == hipSuccess &&
             hipMalloc(&P->dwork, sizeof(double) * (size_t)slots * P->work_stride) == hipSuccess &&
             (!P->batch || !ks.square ||
-             hipMalloc(&P->dytab, sizeof(double) * (size_t)P->blocks * ns * P->NR) == hipSuccess) &&
+             hipMalloc(&P->dytab, sizeof(double) * (size_t)ns * P->NR) == hipSuccess) &&
             (!P->batch || ks.square ||
              (hipMalloc(&P->dkxb, sizeof(double) * (size_t)P->NR * ns) == hipSuccess &&
               hipMalloc(&P->dgtab, sizeof(double) * (size_t)ns * ng) == hipSuccess)) &&
@@ -742,7 +787,12 @@ int mrbo_plan_destroy(mrbo_plan_t* P) {
     if (b) (void)hipFree(b);
   for (auto& b : P->stage)
     if (b.first) (void)hipFree(b.first);
+  for (auto& b : P->solve)
+    if (b.first) (void)hipFree(b.first);
+  if (P->hchk) (void)hipHostFree(P->hchk);
   for (hipEvent_t e : P->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : P->chk_ev)
     if (e) (void)hipEventDestroy(e);
   delete P;
   return MRBO_OK;
@@ -802,6 +852,10 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
     kp.kxb_g = P->dkxb;
     kp.gtab_g = P->dgtab;
     launch_tables(d, P->RPL, P->fx, P->p.nstarts, st, kp);
+    HIP_TRY(hipGetLastError());
+  }
+  if (P->batch && P->RPL == 1) {   // square layout: the launch's Y0(x_start) table, written once
+    launch_ytab(d, P->fx, P->spec, dim3(P->wpg * WAVE), P->smem, st, kp);
     HIP_TRY(hipGetLastError());
   }
   const int slot = (int)(P->nlaunch % mrbo_plan::NEV);
@@ -928,6 +982,119 @@ int mrbo_merge_moments(mrbo_plan_t* P, int32_t nshards, const double* moments, c
   hipLaunchKernelGGL(merge_kernel, dim3((nthr + 63) / 64), dim3(64), 0, (hipStream_t)stream, moments, (int)nshards, cnt,
                      R, d, eto);
   HIP_TRY(hipGetLastError());
+  return MRBO_OK;
+}
+
+// slot k of the plan's outer-ascent buffers, at least `bytes` (contents kept only while large enough)
+static void* solve_slot(mrbo_plan_t* P, size_t k, size_t bytes) {
+  auto& pool = P->solve;
+  if (pool.size() <= k) pool.resize(k + 1, {nullptr, 0});
+  auto& b = pool[k];
+  if (b.second < bytes) {
+    if (b.first) (void)hipFree(b.first);
+    b = {nullptr, 0};
+    if (hipMalloc(&b.first, bytes) != hipSuccess) return nullptr;
+    b.second = bytes;
+  }
+  return b.first;
+}
+
+int mrbo_stochastic_solve(mrbo_plan_t* P, double* x0s, const double* rnstream, const double* xstarts,
+                          const double* dual_y_dx, const mrbo_solve_opts_t* o, double* eto, int32_t* active,
+                          int32_t* result, uint32_t flags, void* stream) {
+  if (!P || !x0s || !rnstream || !xstarts || !o || !result) return fail(MRBO_ERR_ARG, "null argument");
+  if (o->iterations < 1) return fail(MRBO_ERR_ARG, "iterations=%d: at least one", o->iterations);
+  if (o->optimizer != MRBO_OPT_SGA && o->optimizer != MRBO_OPT_ADAM)
+    return fail(MRBO_ERR_ARG, "optimizer=%d unknown", o->optimizer);
+  if (flags & ~(uint32_t)MRBO_FLAG_HOST_POINTERS) return fail(MRBO_ERR_ARG, "flags: only MRBO_FLAG_HOST_POINTERS");
+  if (hipSetDevice(P->device) != hipSuccess) return fail(MRBO_ERR_HIP, "hipSetDevice");
+  hipStream_t st = (hipStream_t)stream;
+  const bool host = flags & MRBO_FLAG_HOST_POINTERS;
+  const int d = P->d, M = P->p.M, R = P->p.R, h = P->p.h, W = 2 + 2 * d + 2;
+  const size_t T = (size_t)M * R;
+  const size_t nx = (size_t)d * R, nrn = (size_t)M * (d + 1) * (h + 1), nxs = (size_t)d * P->p.nstarts;
+  const size_t ndual = (size_t)d * std::max(h, 1) * T;
+  const double sample_size = o->sample_size > 0 ? o->sample_size : (double)M;
+  // device state: x0 (d×R), the launch outputs, the ETO rows, the stop flags, Adam's moments, the checks
+  double* dx0 = host ? (double*)solve_slot(P, 0, sizeof(double) * nx) : x0s;
+  const double* drn = host ? (const double*)solve_slot(P, 1, sizeof(double) * nrn) : rnstream;
+  const double* dxs = host ? (const double*)solve_slot(P, 2, sizeof(double) * nxs) : xstarts;
+  const double* ddual = (host && dual_y_dx) ? (const double*)solve_slot(P, 3, sizeof(double) * ndual) : dual_y_dx;
+  double* deto = (host || !eto) ? (double*)solve_slot(P, 4, sizeof(double) * R * W) : eto;
+  int32_t* dact = (host || !active) ? (int32_t*)solve_slot(P, 5, sizeof(int32_t) * R) : active;
+  double* dvals = (double*)solve_slot(P, 6, sizeof(double) * T);
+  double* dgx = (double*)solve_slot(P, 7, sizeof(double) * d * T);
+  double* dgt = (double*)solve_slot(P, 8, sizeof(double) * T);
+  int32_t* dst = (int32_t*)solve_slot(P, 9, sizeof(int32_t) * T);
+  double* dm = o->optimizer == MRBO_OPT_ADAM ? (double*)solve_slot(P, 10, sizeof(double) * nx) : nullptr;
+  double* dv = o->optimizer == MRBO_OPT_ADAM ? (double*)solve_slot(P, 11, sizeof(double) * nx) : nullptr;
+  int32_t* dchk = (int32_t*)solve_slot(P, 12, sizeof(int32_t) * 2 * mrbo_plan::NCHK);
+  if (!dx0 || !drn || !dxs || (dual_y_dx && !ddual) || !deto || !dact || !dvals || !dgx || !dgt || !dst || !dchk ||
+      (o->optimizer == MRBO_OPT_ADAM && (!dm || !dv)))
+    return fail(MRBO_ERR_NOMEM, "outer-ascent buffers");
+  if (!P->hchk && hipHostMalloc(&P->hchk, sizeof(int32_t) * 2 * mrbo_plan::NCHK) != hipSuccess) {
+    P->hchk = nullptr;
+    return fail(MRBO_ERR_NOMEM, "pinned check ring");
+  }
+  for (auto& e : P->chk_ev)
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (host) {
+    HIP_TRY(hipMemcpyAsync(dx0, x0s, sizeof(double) * nx, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync((void*)drn, rnstream, sizeof(double) * nrn, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync((void*)dxs, xstarts, sizeof(double) * nxs, hipMemcpyHostToDevice, st));
+    if (dual_y_dx) HIP_TRY(hipMemcpyAsync((void*)ddual, dual_y_dx, sizeof(double) * ndual, hipMemcpyHostToDevice, st));
+  }
+  // every restart starts active (stochastic_solve's loop runs until its eswavs break); Adam's
+  // moment estimates start at zero
+  hipLaunchKernelGGL(fill_int_kernel, dim3((R + 63) / 64), dim3(64), 0, st, (int*)dact, R, 1);
+  if (dm) {
+    HIP_TRY(hipMemsetAsync(dm, 0, sizeof(double) * nx, st));
+    HIP_TRY(hipMemsetAsync(dv, 0, sizeof(double) * nx, st));
+  }
+  // The iterations follow each other on the stream without a host round trip.  Behind them the
+  // host reads iteration j's check (status bits, restarts still active) LAG iterations later: once
+  // every restart has stopped, the launches already queued find x0 unchanged and reproduce the
+  // same trajectories and ETO rows bit for bit, so stopping a few iterations late changes no output.
+  constexpr int LAG = 2;
+  int it = 0, stopped_at = 0, bits = 0;
+  auto read_check = [&](int j) -> int {   // iteration j ≥ 1 (its slot not yet reused)
+    const int k = (j - 1) % mrbo_plan::NCHK;
+    if (hipEventSynchronize(P->chk_ev[k]) != hipSuccess) return -1;
+    bits |= P->hchk[2 * k];
+    if (P->hchk[2 * k + 1] == 0 && !stopped_at) stopped_at = j;
+    return 0;
+  };
+  int rc = MRBO_OK;
+  while (it < o->iterations && !stopped_at && !bits) {
+    ++it;
+    rc = mrbo_simulate_mc(P, dx0, drn, dxs, ddual, nullptr, dvals, dgx, dgt, dst, nullptr, nullptr, nullptr, 0, st);
+    if (rc != MRBO_OK) return rc;
+    rc = mrbo_eto_reduce(P, dvals, dgx, dgt, deto, 0, st);
+    if (rc != MRBO_OK) return rc;
+    if (o->optimizer == MRBO_OPT_SGA)
+      rc = mrbo_sga_step(P, deto, dx0, dact, sample_size, o->eta, 0, st);
+    else
+      rc = mrbo_adam_step(P, deto, dx0, dact, dm, dv, it, sample_size, o->eta, o->beta1, o->beta2, o->eps, 0, st);
+    if (rc != MRBO_OK) return rc;
+    const int k = (it - 1) % mrbo_plan::NCHK;
+    hipLaunchKernelGGL(solve_check_kernel, dim3(1), dim3(256), 0, st, (const int*)dst, (long long)T, (const int*)dact, R,
+                       (int*)dchk + 2 * k);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(P->hchk + 2 * k, dchk + 2 * k, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventRecord(P->chk_ev[k], st));
+    if (it > LAG && read_check(it - LAG)) return fail(MRBO_ERR_HIP, "hipEventSynchronize");
+  }
+  for (int j = std::max(1, it - LAG + 1); j <= it; ++j)   // the checks still in flight
+    if (read_check(j)) return fail(MRBO_ERR_HIP, "hipEventSynchronize");
+  if (host) {
+    HIP_TRY(hipMemcpyAsync(x0s, dx0, sizeof(double) * nx, hipMemcpyDeviceToHost, st));
+    if (eto) HIP_TRY(hipMemcpyAsync(eto, deto, sizeof(double) * R * W, hipMemcpyDeviceToHost, st));
+    if (active) HIP_TRY(hipMemcpyAsync(active, dact, sizeof(int32_t) * R, hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  result[0] = it;                              // iterations launched
+  result[1] = stopped_at ? stopped_at : it;    // the iteration after which no restart was active
+  result[2] = bits;                            // OR of every launch's trajectory status bits
   return MRBO_OK;
 }
 
@@ -1145,8 +1312,8 @@ int mrbo_plan_set_order(mrbo_plan_t* P, const int32_t* order, int64_t n) {
 
 int mrbo_plan_info(const mrbo_plan_t* P, int32_t* info, int32_t n) {
   if (!P || !info || n < 0) return fail(MRBO_ERR_ARG, "bad arguments");
-  const int32_t v[6] = {P->RPL, P->blocks, P->wpg, P->batch, P->spec, (int32_t)P->smem};
-  for (int i = 0; i < n && i < 6; ++i) info[i] = v[i];
+  const int32_t v[7] = {P->RPL, P->blocks, P->wpg, P->batch, P->spec, (int32_t)P->smem, P->fx ? 4 : 6};
+  for (int i = 0; i < n && i < 7; ++i) info[i] = v[i];
   return MRBO_OK;
 }
 

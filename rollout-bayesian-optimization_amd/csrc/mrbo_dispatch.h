@@ -41,7 +41,8 @@ struct KernelSet {
   MRBO_UNIT bool kset_d##DD(int rpl, KernelSet& ks);                                            \
   MRBO_UNIT void launch_rollout_d##DD(int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp); \
   MRBO_UNIT void launch_evalb_d##DD(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp); \
-  MRBO_UNIT void launch_tables_d##DD(int rpl, int nstarts, hipStream_t st, const KParams& kp);
+  MRBO_UNIT void launch_tables_d##DD(int rpl, int nstarts, hipStream_t st, const KParams& kp); \
+  MRBO_UNIT void launch_ytab_d##DD(int spec, dim3 b, size_t sm, hipStream_t st, const KParams& kp);
 MRBO_DECLARE_D(1) MRBO_DECLARE_D(2) MRBO_DECLARE_D(3) MRBO_DECLARE_D(4)
 MRBO_DECLARE_D(5) MRBO_DECLARE_D(6) MRBO_DECLARE_D(7) MRBO_DECLARE_D(8)
 MRBO_DECLARE_D(9) MRBO_DECLARE_D(10) MRBO_DECLARE_D(11) MRBO_DECLARE_D(12)
@@ -53,7 +54,8 @@ MRBO_DECLARE_D(13) MRBO_DECLARE_D(14) MRBO_DECLARE_D(15) MRBO_DECLARE_D(16)
   MRBO_UNIT bool kset_d##DD##_f4(int rpl, KernelSet& ks);                                       \
   MRBO_UNIT void launch_rollout_d##DD##_f4(int rpl, int spec, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp); \
   MRBO_UNIT void launch_evalb_d##DD##_f4(int rpl, dim3 g, dim3 b, size_t sm, hipStream_t st, const KParams& kp); \
-  MRBO_UNIT void launch_tables_d##DD##_f4(int rpl, int nstarts, hipStream_t st, const KParams& kp);
+  MRBO_UNIT void launch_tables_d##DD##_f4(int rpl, int nstarts, hipStream_t st, const KParams& kp); \
+  MRBO_UNIT void launch_ytab_d##DD##_f4(int spec, dim3 b, size_t sm, hipStream_t st, const KParams& kp);
 MRBO_DECLARE_DF4(1) MRBO_DECLARE_DF4(2) MRBO_DECLARE_DF4(3) MRBO_DECLARE_DF4(4)
 MRBO_DECLARE_DF4(5) MRBO_DECLARE_DF4(6) MRBO_DECLARE_DF4(7) MRBO_DECLARE_DF4(8)
 #undef MRBO_DECLARE_DF4

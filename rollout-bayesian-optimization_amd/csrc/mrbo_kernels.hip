@@ -143,6 +143,32 @@ void MRBO_SFX(launch_rollout_d)(int rpl, int spec, dim3 g, dim3 b, size_t sm, hi
   else launch_rollout_spec<0>(rpl, g, b, sm, st, kp);
 }
 
+// The Y0 table of a square-layout launch (rows per lane 1) with batched starts: ONE workgroup of
+// the rollout launch's shape (b, sm) and kernel variant (spec as launch_rollout_d) writes it just
+// before the rollout kernel, on the same stream
+void MRBO_SFX(launch_ytab_d)(int spec, dim3 b, size_t sm, hipStream_t st, const KParams& kp) {
+#if MRBO_HAS_HALF
+  if (spec == 2) {
+    hipLaunchKernelGGL((ytab_kernel<MRBO_D, 1, 1, 2>), dim3(1), b, sm, st, kp);
+    return;
+  }
+#endif
+#if defined(MRBO_AB_MIN) && (defined(MRBO_AB_COST) || MRBO_AB_RPL != 1)
+  (void)spec; (void)b; (void)sm; (void)st; (void)kp;
+#elif defined(MRBO_AB_MIN) && defined(MRBO_AB_GENERIC)
+  hipLaunchKernelGGL((ytab_kernel<MRBO_D, 1, 0>), dim3(1), b, sm, st, kp);
+#elif defined(MRBO_AB_MIN)
+  if constexpr (has_spec(MRBO_D, 1)) hipLaunchKernelGGL((ytab_kernel<MRBO_D, 1, 1>), dim3(1), b, sm, st, kp);
+#else
+  if constexpr (has_spec(MRBO_D, 1))
+    if (spec == 1) {
+      hipLaunchKernelGGL((ytab_kernel<MRBO_D, 1, 1>), dim3(1), b, sm, st, kp);
+      return;
+    }
+  hipLaunchKernelGGL((ytab_kernel<MRBO_D, 1, 0>), dim3(1), b, sm, st, kp);
+#endif
+}
+
 template <int RPL>
 static void launch_tables_one(int nstarts, hipStream_t st, const KParams& kp) {
   if constexpr (has_rpl(MRBO_D, RPL))

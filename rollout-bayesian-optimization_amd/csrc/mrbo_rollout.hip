@@ -1982,10 +1982,10 @@ __device__ __forceinline__ double newton(WaveCtx<D, RPL, HW>& W, const KParams& 
 // Workgroup prologue (kp.batch): base kernel rows of the clamped start points and the squared
 // norms of their forward products -- constants of the launch shared by every multistart.
 //   kxb[i][k] = ψ(|x_k − X_i|) (0 on padded rows);  per start, Y = L0⁻¹[kx, ∇kx](x_k):
-//   Y0 → this workgroup's global slice kp.ytab, base Gram YᵀY → gtab (LDS)
+//   base Gram YᵀY → gtab (LDS); with store_y (ytab_kernel only) Y0 → the launch's table kp.ytab
 // The per-wave areas (not yet initialised) serve as scratch for the squares.
 template <int D, int RPL, int HW>
-__device__ __forceinline__ void stage_start_tables(const KParams& kp, double* smem) {
+__device__ __forceinline__ void stage_start_tables(const KParams& kp, double* smem, bool store_y) {
   using Ly = Lay<D, RPL, HW>;
   constexpr int NR = Ly::NR;
   const WgTables<D, RPL, HW> tb(kp);
@@ -2012,19 +2012,15 @@ __device__ __forceinline__ void stage_start_tables(const KParams& kp, double* sm
     kxb[q] = v;
   }
   __syncthreads();
-  // per start (waves in turn): Y = L0⁻¹[kx, ∇kx](x_k) by the register-broadcast product, Y0 to
-  // this workgroup's global slice, the base Gram YᵀY (upper triangle) to gtab
+  // per start (waves in turn): Y = L0⁻¹[kx, ∇kx](x_k) by the register-broadcast product, the base
+  // Gram YᵀY (upper triangle) to gtab, and (store_y) Y0 to the launch's table
   const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
   double* red = smem + tb.end + (long long)wv * Ly::WAVE_LDS;   // wave-area scratch
-  // One table for the launch: every workgroup computes bit-identical Y0 rows (same inputs, same
-  // code), so they all write the same values to the same slice -- a race between identical values,
-  // which any reader resolves to the same bits.  The per-workgroup slices (MRBO_YTAB_PER_WG) wrote
-  // 2.4 MB per C3 launch to HBM; the shared slice ends as one dirty copy per XCD L2.
-#ifdef MRBO_YTAB_PER_WG
-  double* ytab = kp.ytab + (long long)blockIdx.x * ns * NR;
-#else
+  // One Y0 table for the launch, written once by ytab_kernel (one workgroup, launched before the
+  // rollout kernel on the same stream, running this same code) and only read by the rollout
+  // workgroups.  Round 5 had every rollout workgroup write the same bits to the shared slice (a
+  // benign but formal race); per-workgroup slices had cost 2.4 MB of HBM writes per C3 launch.
   double* ytab = kp.ytab;
-#endif
   for (int k = wv; k < ns; k += nw) {
     double bv[Ly::D1], acc[Ly::D1];
     double rho2 = 0.0, r[D];
@@ -2042,7 +2038,7 @@ __device__ __forceinline__ void stage_start_tables(const KParams& kp, double* sm
 #pragma unroll
     for (int c = 0; c < Ly::D1; ++c) acc[c] = 0.0;
     bcast_product<Ly::D1, Ly::LD>(acc, bv, smem + lane, kp.N);
-    ytab[(long long)k * NR + lane] = acc[0];
+    if (store_y) ytab[(long long)k * NR + lane] = acc[0];
 #pragma unroll
     for (int ch = 0; ch < (Ly::NG + 15) / 16; ++ch) {
       double gv[16];
@@ -2813,11 +2809,7 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL, HW>& W, const KParams
   W.XS = kp.xs_lds ? smem + tb.xs : kp.xstarts;
   W.KXB = Ly::SQ ? smem + tb.kxb : kp.kxb_g;
   W.GTAB = Ly::SQ ? smem + tb.gtab : kp.gtab_g;
-#ifdef MRBO_YTAB_PER_WG
-  W.YTAB = kp.ytab + (long long)blockIdx.x * kp.nstarts * Ly::NR;
-#else
-  W.YTAB = kp.ytab;   // the launch's shared table (stage_start_tables)
-#endif
+  W.YTAB = kp.ytab;   // the launch's table (ytab_kernel)
   W.B = wbase;
   W.red = wbase + Ly::BROWS * Ly::BS;
   W.U = W.red + Ly::REDN;
@@ -2876,9 +2868,8 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL, HW>& W, const KParams
 // (every configuration of BASELINE.json).  The other kernels' and rules' code paths fold away,
 // which frees registers in the whole trajectory (VGPR spills 94 -> 33 at d = 6).  SPEC = 0
 // reads both from the launch parameters.
-template <int D, int RPL, int SPEC, int HW = 1>
-__global__ void __launch_bounds__((KBounds<D, RPL, HW>::threads), (KBounds<D, RPL, HW>::waves_per_simd)) rollout_kernel(KParams kp_in) {
-  KParams kp = kp_in;   // a local copy: the fixed fields below propagate as constants
+template <int SPEC>
+__device__ __forceinline__ void spec_params(KParams& kp) {
   if constexpr (SPEC == 1) {
     kp.kernel = KERNEL_MATERN52;
     kp.rule = RULE_EI;
@@ -2888,15 +2879,43 @@ __global__ void __launch_bounds__((KBounds<D, RPL, HW>::threads), (KBounds<D, RP
     kp.rule = RULE_EI;
     kp.cost = COST_QUADRATIC;
   }
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  // stage L0⁻¹ (and the inner-solve start points) once per workgroup (the only block barrier)
+}
+
+// stage L0⁻¹ (and the inner-solve start points) once per workgroup (the only block barrier)
+template <int D, int RPL, int HW>
+__device__ __forceinline__ void stage_linv(const KParams& kp, double* smem) {
   using Ly = Lay<D, RPL, HW>;
   for (int q = threadIdx.x; q < (int)Ly::LINV_DOUBLES; q += blockDim.x) smem[q] = kp.Linv[Ly::LINV_LDS_SRC + q];
   if (kp.xs_lds)
     for (int q = threadIdx.x; q < kp.nstarts * D; q += blockDim.x) smem[Ly::LINV_DOUBLES + q] = kp.xstarts[q];
   __syncthreads();
+}
+
+// The Y0(x_start) table of the square layouts (kp.batch), written ONCE per launch: one workgroup of
+// the rollout launch's shape and LDS size, launched just before rollout_kernel on the same stream,
+// runs the rollout prologue's own code with store_y (so its rows are the bits the rollout
+// workgroups' own Gram tables come from).
+template <int D, int RPL, int SPEC, int HW = 1>
+__global__ void __launch_bounds__((KBounds<D, RPL, HW>::threads), (KBounds<D, RPL, HW>::waves_per_simd)) ytab_kernel(KParams kp_in) {
+  KParams kp = kp_in;
+  spec_params<SPEC>(kp);
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  using Ly = Lay<D, RPL, HW>;
   if constexpr (Ly::SQ) {
-    if (kp.batch) stage_start_tables<D, RPL, HW>(kp, smem);
+    stage_linv<D, RPL, HW>(kp, smem);
+    stage_start_tables<D, RPL, HW>(kp, smem, true);
+  }
+}
+
+template <int D, int RPL, int SPEC, int HW = 1>
+__global__ void __launch_bounds__((KBounds<D, RPL, HW>::threads), (KBounds<D, RPL, HW>::waves_per_simd)) rollout_kernel(KParams kp_in) {
+  KParams kp = kp_in;   // a local copy: the fixed fields below propagate as constants
+  spec_params<SPEC>(kp);
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  using Ly = Lay<D, RPL, HW>;
+  stage_linv<D, RPL, HW>(kp, smem);
+  if constexpr (Ly::SQ) {
+    if (kp.batch) stage_start_tables<D, RPL, HW>(kp, smem, false);   // Y0 itself: ytab_kernel
   }
   WaveCtx<D, RPL, HW> W;
   wave_setup<D, RPL, HW>(W, kp, smem, threadIdx.x / WAVE);

@@ -24,9 +24,10 @@
 module MRBO
 
 # the reference's generic functions this module adds methods to (must be `import`ed to extend)
-import Main: simulate_trajectory_mc, simulate_trajectory_ghq
+import Main: simulate_trajectory_mc, simulate_trajectory_ghq, stochastic_solve
 # the reference's types, constructors and accessors used below (Main-level bindings)
 using Main: Surrogate, Trajectory, TrajectoryParameters, ExpectedTrajectoryOutput,
+            StochasticGradientAscent, StandardSGA, Adam, ExperimentSetup, get_starts,
             Matern52, Matern32, Matern12, SquaredExponential, Periodic,
             get_observed, get_active_covariates, get_active_cholesky, get_active_coefficients,
             get_active_observations, get_observations, get_kernel, get_decision_rule, get_name,
@@ -79,6 +80,20 @@ struct MrboParamsC
     cost_c0::Float64
     cost_w::Ptr{Float64}
 end
+
+# mirrors mrbo_solve_opts_t (the outer ascent of mrbo_stochastic_solve)
+struct MrboSolveOptsC
+    optimizer::Int32     # 0 StandardSGA, 1 Adam
+    iterations::Int32
+    eta::Float64
+    beta1::Float64
+    beta2::Float64
+    eps::Float64
+    sample_size::Float64 # eswavs sample size (0 → the plan's M = tp.mc_iters)
+end
+
+mrbo_solve_opts(o::StandardSGA, iterations::Int) = MrboSolveOptsC(Int32(0), Int32(iterations), o.η, 0.9, 0.999, 1e-8, 0.0)
+mrbo_solve_opts(o::Adam, iterations::Int) = MrboSolveOptsC(Int32(1), Int32(iterations), o.η, o.β1, o.β2, o.ε, 0.0)
 
 struct MrboBackend
     device::Int
@@ -267,6 +282,40 @@ with_grad_container(c, with_gradient, a, M, R) =
     !with_gradient ? Array{Float64, 3}(undef, 0, 0, 0) :
     isnothing(c) ? Array{Float64, 3}(undef, a, M, R) :
     size(c) == (a, M, R) ? c : throw(DimensionMismatch("gradient container must be $a×$M×$R"))
+
+# The reference's outer loop on the GPU: stochastic_solve(; optimizer, surrogate, tp, es, start)
+# (utils.jl:235-265) for every column of `starts` (d×R, e.g. generate_batch's points, utils.jl:97-106)
+# in ONE mrbo_stochastic_solve call on one cached plan: up to `iterations` × [the rollout launch of
+# all restarts, their ETO rows, eswavs (utils.jl:114-123) + update! (optimizers.jl)] on the device,
+# each restart stopping for good at its eswavs break, with no host round trip per iteration (the
+# R = 1 method above, called 50 times per restart by the reference's loop, pays one per call).
+# Returns the final points (get_starting_point(tpc) of every restart, d×R) and every restart's ETO
+# at its last launch.  θ = tp.θ.  The optimizer's fields are read, never mutated (Adam's moments
+# live on the device for the call).
+function stochastic_solve(backend::MrboBackend; optimizer::StochasticGradientAscent, surrogate::Surrogate,
+                          tp::TrajectoryParameters, es::ExperimentSetup, starts::AbstractMatrix{<:Real},
+                          iterations::Int = 50)
+    X = Matrix{Float64}(starts)
+    d, R = size(X)
+    xs = Matrix{Float64}(get_starts(es))
+    plan = mrbo_cached_plan(surrogate, tp, tp.θ, size(xs, 2); device = backend.device, R = R)
+    rns = tp.rnstream_sequence
+    W = 2 + 2d + 2
+    eto = Matrix{Float64}(undef, W, R)   # C's R×W rows = the columns here
+    active = zeros(Int32, R)
+    res = zeros(Int32, 3)
+    opts = Ref(mrbo_solve_opts(optimizer, iterations))
+    GC.@preserve X rns xs eto active res opts begin
+        mrbo_check(ccall((:mrbo_stochastic_solve, libmrbo), Cint,
+                         (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{MrboSolveOptsC},
+                          Ptr{Float64}, Ptr{Int32}, Ptr{Int32}, UInt32, Ptr{Cvoid}),
+                         plan.handle, X, rns, xs, C_NULL, opts, eto, active, res, MRBO_FLAG_HOST_POINTERS, C_NULL))
+    end
+    res[3] != 0 && throw(ErrorException("rollout failed during the ascent (status bits $(res[3]))"))
+    etos = [ExpectedTrajectoryOutput(μxθ=eto[1, r], σ_μxθ=eto[2, r], ∇μx=eto[3:2+d, r], σ_∇μx=eto[3+d:2+2d, r],
+                                     ∇μθ=eto[3+2d:3+2d, r], σ_∇μθ=eto[4+2d:4+2d, r]) for r in 1:R]
+    return X, etos
+end
 
 # The GPU method of simulate_trajectory_ghq (rollout.jl:409-467): node vectors nodes[indices[m]]
 # and weights[indices[m]] as M×(h+1) matrices for mrbo_simulate_ghq.

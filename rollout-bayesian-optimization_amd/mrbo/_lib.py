@@ -35,8 +35,10 @@ EXPORTS = [
     "mrbo_simulate_mc", "mrbo_simulate_ghq", "mrbo_eto_reduce", "mrbo_partial_moments", "mrbo_eval_base", "mrbo_rnstream",
     "mrbo_initial_guesses", "mrbo_dual_uniform", "mrbo_last_kernel_ms", "mrbo_gp_fit", "mrbo_gp_fit_theta",
     "mrbo_plan_info", "mrbo_last_gp_fit_ms", "mrbo_plan_set_order", "mrbo_base_solve", "mrbo_sga_step",
-    "mrbo_kernel_times", "mrbo_merge_moments", "mrbo_adam_step",
+    "mrbo_kernel_times", "mrbo_merge_moments", "mrbo_adam_step", "mrbo_stochastic_solve",
 ]
+
+MRBO_OPT_SGA, MRBO_OPT_ADAM = 0, 1
 
 
 class SurrogateDesc(ctypes.Structure):
@@ -53,6 +55,13 @@ class ParamsDesc(ctypes.Structure):
                 ("sigma_tol", ctypes.c_double), ("seed", ctypes.c_uint64),
                 ("sample_offset", ctypes.c_int32), ("samples_total", ctypes.c_int32),
                 ("cost", ctypes.c_int32), ("cost_c0", ctypes.c_double), ("cost_w", _dp)]
+
+
+class SolveOpts(ctypes.Structure):
+    """mrbo_solve_opts_t (include/mrbo.h)."""
+    _fields_ = [("optimizer", ctypes.c_int32), ("iterations", ctypes.c_int32), ("eta", ctypes.c_double),
+                ("beta1", ctypes.c_double), ("beta2", ctypes.c_double), ("eps", ctypes.c_double),
+                ("sample_size", ctypes.c_double)]
 
 
 _lib = None
@@ -91,6 +100,8 @@ def load():
     L.mrbo_sga_step.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_uint32, _vp]
     L.mrbo_adam_step.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int32] + [ctypes.c_double] * 5 + [
         ctypes.c_uint32, _vp]
+    L.mrbo_stochastic_solve.argtypes = [_vp, _vp, _vp, _vp, _vp, ctypes.POINTER(SolveOpts), _vp, _vp,
+                                        ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32, _vp]
     L.mrbo_base_solve.argtypes = [_vp, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]
     L.mrbo_rnstream.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _dp]
     L.mrbo_initial_guesses.argtypes = [ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp]

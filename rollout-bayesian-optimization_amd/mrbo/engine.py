@@ -181,6 +181,24 @@ class RolloutPlan:
                                            float(sample_size), float(eta), float(beta1), float(beta2), float(eps), 0,
                                            ctypes.c_void_p(st.cuda_stream)))
 
+    def stochastic_solve(self, x0s, rnstream, xstarts, optimizer="sga", iterations=50, eta=None, beta1=0.9,
+                         beta2=0.999, eps=1e-8, sample_size=0, eto=None, active=None, dual_y_dx=None, stream=None):
+        """mrbo_stochastic_solve on device tensors: the whole outer ascent (utils.jl:235-265) for the
+        plan's R restarts in one call; x0s (d·R, column-major) is updated in place, eto (W·R) and
+        active (R, int32) receive the final rows and stop flags when given.  Returns (iterations
+        launched, iteration after which no restart was active, OR of the status bits)."""
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        p = lambda t_: None if t_ is None else ctypes.c_void_p(t_.data_ptr())
+        opt = _lib.MRBO_OPT_SGA if optimizer == "sga" else _lib.MRBO_OPT_ADAM
+        eta = (0.01 if opt == _lib.MRBO_OPT_SGA else 0.001) if eta is None else eta
+        o = _lib.SolveOpts(opt, int(iterations), float(eta), float(beta1), float(beta2), float(eps), float(sample_size))
+        res = (ctypes.c_int32 * 3)()
+        _lib.check(self.lib.mrbo_stochastic_solve(self.handle, p(x0s), p(rnstream), p(xstarts), p(dual_y_dx),
+                                                  ctypes.byref(o), p(eto), p(active), res, 0,
+                                                  ctypes.c_void_p(st.cuda_stream)))
+        return int(res[0]), int(res[1]), int(res[2])
+
     def eval_base(self, xs):
         """eval(s, x, θ) at the columns of xs (d×P); returns (3+4d+d²)×P numpy."""
         torch = _torch()
@@ -242,10 +260,10 @@ class RolloutPlan:
 
     def info(self):
         """Launch geometry: rows per lane, workgroups, waves per workgroup, batched start values,
-        specialised kernel, LDS bytes per workgroup."""
-        v = (ctypes.c_int32 * 6)()
-        _lib.check(self.lib.mrbo_plan_info(self.handle, v, 6))
-        keys = ("rpl", "blocks", "waves_per_group", "batch", "spec", "lds_bytes")
+        specialised kernel, LDS bytes per workgroup, fantasy capacity of the kernel unit (FMAX)."""
+        v = (ctypes.c_int32 * 7)()
+        _lib.check(self.lib.mrbo_plan_info(self.handle, v, 7))
+        keys = ("rpl", "blocks", "waves_per_group", "batch", "spec", "lds_bytes", "fmax")
         return dict(zip(keys, (int(x) for x in v)))
 
 

@@ -11,10 +11,13 @@ measure and check what the Julia shim does:
     reference's rollout.jl:328-339);
   * simulate_trajectory_mc_batch: the batched method, the columns of X0 in one launch;
   * stochastic_solve: utils.jl:235-265 (50 iterations, eswavs, StandardSGA update!) driving the
-    R = 1 method, i.e. the reference's own outer loop on the drop-in.
+    R = 1 method, i.e. the reference's own outer loop on the drop-in;
+  * stochastic_solve_batch: MRBO.jl's device-resident method of that loop -- the whole ascent of
+    a restart batch in ONE mrbo_stochastic_solve call on one cached plan.
 There is no CPU path: every call goes through libmrbo.so on the GPU.
 """
 import ctypes
+import hashlib
 
 import numpy as np
 
@@ -34,9 +37,19 @@ def release_plans():
     _PLAN_CACHE.clear()
 
 
+def _digest(a):
+    """hash(x) of MRBO.jl's key: the bytes of the array's active part."""
+    return hashlib.blake2b(np.ascontiguousarray(a, dtype=np.float64).tobytes(), digest_size=16).hexdigest()
+
+
 def _key(s, tp, theta, nstarts, device, M, R):
+    """mrbo_plan_key (MRBO.jl): the surrogate's identity AND the hashes of its active covariates,
+    observations and Cholesky factor and of every observation (fmini, Q3), so that a surrogate
+    freed and replaced by another at the same id() -- CPython reuses ids -- never meets a stale plan."""
     lbs, ubs = tp.get_spatial_bounds()
-    return (id(s), s.version, s.observed, tp.horizon, tuple(np.asarray(lbs).ravel()), tuple(np.asarray(ubs).ravel()),
+    n = s.observed
+    return (id(s), s.version, n, _digest(s.X[:, :n]), _digest(s.y[:n]), _digest(s.L[:n, :n]), _digest(s.y),
+            float(s.σn2), tp.horizon, tuple(np.asarray(lbs).ravel()), tuple(np.asarray(ubs).ravel()),
             float(theta), int(nstarts), int(M), int(R), int(device), s.get_decision_rule().rule_id,
             float(s.ψ.lengthscale), float(s.ψ.period))
 
@@ -161,3 +174,32 @@ def stochastic_solve(T, tp, xstarts, start, eta=0.01, iterations=50, device=0, t
             break
         x = x + eta * eto.gradient()
     return x
+
+
+def stochastic_solve_batch(T, tp, xstarts, starts, optimizer="sga", eta=None, iterations=50, device=0):
+    """MRBO.jl stochastic_solve(backend::MrboBackend; optimizer, surrogate, tp, es, starts): the
+    reference's outer loop (utils.jl:235-265) for every column of `starts` (d×R, e.g. the
+    generate_batch points) in ONE C-ABI call -- up to `iterations` × (launch, ETO, eswavs +
+    update!) on the device on one cached plan, host arrays staged once.  Returns (X d×R: every
+    restart's get_starting_point(tpc), eto R×W: its final ETO rows (mrbo_eto_reduce's layout),
+    active R: 1 where eswavs never stopped it, result: [iterations launched, iteration after which
+    no restart was active, status bits])."""
+    X = np.array(starts, dtype=np.float64, order="F")
+    d, R = X.shape
+    xs = np.asfortranarray(xstarts, dtype=np.float64)
+    plan = cached_plan(T.s, tp, T.θ[0], xs.shape[1], device=device, R=R)
+    rn = np.asfortranarray(tp.rnstream_sequence, dtype=np.float64)
+    W = 2 + 2 * d + 2
+    eto = np.zeros((R, W))
+    active = np.zeros(R, dtype=np.int32)
+    opt = _lib.MRBO_OPT_SGA if optimizer == "sga" else _lib.MRBO_OPT_ADAM
+    eta = (0.01 if opt == _lib.MRBO_OPT_SGA else 0.001) if eta is None else eta
+    o = _lib.SolveOpts(opt, int(iterations), float(eta), 0.9, 0.999, 1e-8, 0.0)
+    res = (ctypes.c_int32 * 3)()
+    pv = lambda a: ctypes.c_void_p(a.ctypes.data)
+    _lib.check(plan.lib.mrbo_stochastic_solve(plan.handle, pv(X), pv(rn), pv(xs), None, ctypes.byref(o), pv(eto),
+                                              pv(active), res, _lib.MRBO_FLAG_HOST_POINTERS, None))
+    stats["launches"] += int(res[0])
+    if res[2]:
+        raise RuntimeError(f"rollout failed during the ascent (status bits {int(res[2])})")
+    return X, eto, active, [int(v) for v in res]

@@ -206,10 +206,13 @@ def tight_value_stats(dv, v, vmax):
     return dict(over_tight=int((dv > tt).sum()), tight_margin_max=float((dv / tt).max()), tight_tol_min=float(tt.min()))
 
 
-def _compare(key, g, r, o, o_replay, M, kind="full", work_exact=True):
+def _compare(key, g, r, o, o_replay, M, kind="full", work_exact=True, work_agree=None):
     """The T2 / T3 assertions above and the non-vacuity guard; records the measured statistics
     under `key`.  work_exact: assert per-trajectory Newton work equality on the identical paths
-    (all cases but C4's, module docstring)."""
+    (all cases but C4's, module docstring).  work_agree (per trajectory, flat): the trajectories on
+    which the oracle's two builds agree on the path and on every work counter -- where rounding
+    alone does not decide the line-search work, the GPU's per-trajectory work must equal the
+    oracle's (C4, whose identical paths are otherwise held to the totals only)."""
     assert kind in ("full", "forward")
     assert (r["status"] == 0).all() and (o["status"] == 0).all() and (o_replay["status"] == 0).all()
     dx = np.abs(r["policy_x"] - o["policy_x"]) / (1 + np.abs(o["policy_x"]))
@@ -271,6 +274,12 @@ def _compare(key, g, r, o, o_replay, M, kind="full", work_exact=True):
     assert stats["identical_grad"]["over_tol"] == 0, stats
     if work_exact:
         assert stats["work_unequal_identical"] == 0, stats
+    if work_agree is not None:
+        m = exact & work_agree
+        stats["work_agree"] = dict(identical=int(exact.sum()), oracle_builds_agree=int(m.sum()),
+                                   unequal=int((evals_r[:, m] != evals_o[:, m]).any(axis=0).sum()))
+        assert m.sum() >= 0.25 * exact.sum(), stats   # not vacuous
+        assert stats["work_agree"]["unequal"] == 0, stats
     tg, to = np.asarray(stats["work_totals"]["gpu"], float), np.asarray(stats["work_totals"]["oracle"], float)
     assert np.all(np.abs(tg - to) <= 0.01 * np.maximum(to, 1.0)), stats
     if not flip.any():
@@ -304,11 +313,17 @@ def _replay_t2(g, r, o, ok=None):
     return float(vm.max()), float(ratio.max())
 
 
+ORACLE_FAST = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "build",
+                           "librbo_oracle_fast.so")
+
+
 def _end_to_end(oracle, key, g, M, cost=None, plan_opts=None, kind="full", htol=1e-4, rule="EI", theta=0.0,
                 ghq=None, work_exact=True):
     """GPU launch, the oracle on the same inputs, the oracle's replay of the GPU's policy points, then
     _compare.  rule / theta: the base decision rule (EI, POI, LCB); ghq = (nodes, weights): the
-    Gauss–Hermite estimator instead of Monte-Carlo draws (M = the number of node vectors)."""
+    Gauss–Hermite estimator instead of Monte-Carlo draws (M = the number of node vectors).
+    work_exact = "agree": the oracle's second build (-O3 -march=native, oracle/Makefile) runs the
+    same inputs too, and per-trajectory work equality is asserted where its two builds agree."""
     opts = dict(plan_opts or {})
     if htol != 1e-4:
         opts["htol"] = htol
@@ -325,6 +340,18 @@ def _end_to_end(oracle, key, g, M, cost=None, plan_opts=None, kind="full", htol=
     rp = np.asfortranarray(r["policy_x"][:, 1:])
     o2 = oracle.simulate_mc(_osur(oracle, g), g["x0s"], rn, g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
                             replay_x=rp, want_policy=False, want_kappa=True, **kw)
-    return _compare(key, g, r, o, o2, M, kind=kind, work_exact=work_exact)
+    agree = None
+    if work_exact == "agree":
+        assert os.path.exists(ORACLE_FAST), "the oracle's timing build (make -C oracle) is needed"
+        try:
+            oracle.use_library(ORACLE_FAST)
+            of = oracle.simulate_mc(_osur(oracle, g), g["x0s"], rn, g["xstarts"], g["lbs"], g["ubs"], int(g["h"]), **kw)
+        finally:
+            oracle.use_library(None)
+        dxo = (np.abs(of["policy_x"] - o["policy_x"]) / (1 + np.abs(o["policy_x"]))).max(axis=(0, 1)).ravel(order="F")
+        agree = (dxo <= 1e-12) & (of["evals"].reshape(3, -1, order="F") ==
+                                  o["evals"].reshape(3, -1, order="F")).all(axis=0)
+        work_exact = False
+    return _compare(key, g, r, o, o2, M, kind=kind, work_exact=work_exact, work_agree=agree)
 
 

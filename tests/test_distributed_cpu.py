@@ -1,4 +1,4 @@
-"""World-size-2/3 gloo tests of the multi-GPU path's exchange (no GPU): each rank rolls out its
+"""World-size-2/3/8 gloo tests of the multi-GPU path's exchange (no GPU): each rank rolls out its
 contiguous MC shard (the CPU oracle stands in for the device here -- test infrastructure),
 reduces its per-restart moments (Σ, M2), one all_gather, Chan merge, and every rank derives the
 same ETO as a single-process run over all samples."""
@@ -19,6 +19,17 @@ def _free_port():
     return p
 
 
+def _case(world):
+    """golden c2near (6 MC × 2 restarts) for 2 and 3 ranks; 8 ranks -- the 8-GPU node's world --
+    on C2's base data at 24 MC × 2 restarts (3 samples per rank)"""
+    if world <= 3:
+        return load_golden("c2near")
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "rollout-bayesian-optimization_amd"), os.path.join(ROOT, "tests")]
+    from parity import _problem_arrays
+    return _problem_arrays("C2", 24, 2)
+
+
 def _worker(rank, world, port, out_q):
     import sys
     sys.path[:0] = [os.path.join(ROOT, "rollout-bayesian-optimization_amd"), ROOT]
@@ -28,7 +39,7 @@ def _worker(rank, world, port, out_q):
     from oracle import oracle as O
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    g = load_golden("c2near")
+    g = _case(world)
     h, M = int(g["h"]), g["rnstream"].shape[0]
     d, R = g["x0s"].shape
     lo, hi = shard(M, world, rank)
@@ -47,9 +58,9 @@ def _worker(rank, world, port, out_q):
 import pytest
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gloo_eto_matches_single_process(oracle, world):
-    g = load_golden("c2near")
+    g = _case(world)
     h = int(g["h"])
     s = oracle.OracleSurrogate(g["X"], g["L"], g["c"], g["y"], fmini=float(g["fmini"]))
     full = oracle.simulate_mc(s, g["x0s"], g["rnstream"], g["xstarts"], g["lbs"], g["ubs"], h, nthreads=1)

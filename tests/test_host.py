@@ -329,3 +329,35 @@ def test_tight_value_check_has_teeth():
     worse = 1000 * err
     assert value_bound_stats(worse, vb)["over_bound"] == 0      # the bound alone misses it
     assert tight_value_stats(worse, v, v.max())["over_tight"] > 0
+
+
+def test_shim_plan_key_tracks_the_surrogate_data():
+    """mrbo.shim's plan cache key mirrors MRBO.jl's mrbo_plan_key: besides the surrogate's identity
+    it hashes the active covariates, observations and Cholesky factor (CPython reuses id() once a
+    surrogate is freed, so identity + version alone could hand a new surrogate a stale plan)."""
+    from mrbo import configs, shim
+    pb = configs.problem("C2", M=8, R=2)
+    s, tp = pb.surrogate, pb.tp
+    k0 = shim._key(s, tp, 0.0, 18, 0, 8, 2)
+    assert shim._key(s, tp, 0.0, 18, 0, 8, 2) == k0
+    n = s.observed
+    for arr, idx in ((s.X, (0, n - 1)), (s.y, (n - 1,)), (s.L, (n - 1, n - 1))):
+        old = arr[idx]
+        arr[idx] = old + 1e-3        # same id, version and observation count: other data
+        assert shim._key(s, tp, 0.0, 18, 0, 8, 2) != k0
+        arr[idx] = old
+    assert shim._key(s, tp, 0.0, 18, 0, 8, 2) == k0
+
+
+def test_bench_kernel_label_names_the_profiled_kernel():
+    """bench.py's roofline.kernel is the rollout kernel's name as rocprofv3 prints it, per plan spec
+    (0 generic, 1 Matérn-5/2 + EI, 2 the half-wave kernel, 3 the cost kernel) and kernel unit."""
+    import bench
+    assert bench.kernel_label(6, dict(rpl=1, spec=1, fmax=4)) == "mrbo::fmax4::rollout_kernel<6, 1, 1, 1>"
+    assert bench.kernel_label(2, dict(rpl=1, spec=2, fmax=4)) == "mrbo::fmax4::rollout_kernel<2, 1, 1, 2>"
+    assert bench.kernel_label(8, dict(rpl=4, spec=3, fmax=6)) == "mrbo::fmax6::rollout_kernel<8, 4, 2, 1>"
+    assert bench.kernel_label(6, dict(rpl=2, spec=0, fmax=6)) == "mrbo::fmax6::rollout_kernel<6, 2, 0, 1>"
+    # the committed rocprof summary of the headline names that kernel
+    import csv
+    rows = list(csv.DictReader(open(os.path.join(ROOT, "profiles", "r05", "kernel_stats_c3_r5l.csv"))))
+    assert any(bench.kernel_label(6, dict(rpl=1, spec=1, fmax=4)) in r["Name"] for r in rows)

@@ -30,7 +30,8 @@ HEADER = os.path.join(ROOT, "include", "mrbo.h")
 NAMES = os.path.join(ROOT, "tests", "golden", "julia_ref_names.json")
 IDENT = r"[A-Za-z_¡-￿][A-Za-z0-9_!¡-￿]*"
 
-STRUCT_MAP = {"MrboSurrogateC": "mrbo_surrogate_t", "MrboParamsC": "mrbo_params_t"}
+STRUCT_MAP = {"MrboSurrogateC": "mrbo_surrogate_t", "MrboParamsC": "mrbo_params_t",
+              "MrboSolveOptsC": "mrbo_solve_opts_t"}
 SCALAR = {"Int32": "int32_t", "Cint": "int32_t", "UInt32": "uint32_t", "UInt64": "uint64_t", "Int64": "int64_t",
           "Float64": "double", "Cdouble": "double", "Cvoid": "void"}
 SIZE_ALIGN = {"int32_t": 4, "uint32_t": 4, "int64_t": 8, "uint64_t": 8, "double": 8, "ptr": 8}

@@ -4,6 +4,8 @@ mrbo.shim (the Python mirror of julia/MRBO.jl's C-ABI calls, host pointers):
   per_call_plan  R = 1, a new plan per call and destroyed after it (the round-4 shim)
   cached_r1      R = 1 on the cached plan (MRBO.jl simulate_trajectory_mc(T, tp, ::MrboBackend))
   batched        the R restarts of the config in ONE launch (MRBO.jl's batched method)
+  stochastic_solve_r1_loop / _device   the reference's outer loop over the R restarts: through the
+                 R = 1 method, and as ONE mrbo_stochastic_solve call (MRBO.jl's device-resident method)
 Each row: trajectories per second over whole calls (host staging, launch, copies back, host
 ETO), and the per-call time.  Not the bench metric (bench.py's value is the device-resident rate).
 
@@ -77,6 +79,32 @@ def main():
         s = timed(fn, n)
         rows[name] = {"trajectories_per_call": per, "ms_per_call": s * 1e3, "trajectories_per_s": per / s}
         shim.release_plans()
+    # the reference's outer loop (stochastic_solve, utils.jl:235-265) over the R restarts: through the
+    # R = 1 method (MRBO.jl simulate_trajectory_mc, one call per restart and iteration), and as ONE
+    # mrbo_stochastic_solve call (MRBO.jl's device-resident method).  Both do the same rollout work:
+    # the R = 1 loop's calls are the useful trajectories, the rate of either row counts those alone.
+    steps = []
+    t0 = time.perf_counter()
+    for r in range(R):
+        trace = []
+        shim.stochastic_solve(T, tp, xs, pb.x0s[:, r], eta=0.01, trace=trace)
+        steps.append(len(trace))
+    s_loop = time.perf_counter() - t0
+    useful = int(sum(steps)) * M
+    rows["stochastic_solve_r1_loop"] = {"calls": int(sum(steps)), "s_per_ascent": s_loop,
+                                        "trajectories": useful, "trajectories_per_s": useful / s_loop}
+    shim.release_plans()
+    shim.stochastic_solve_batch(T, tp, xs, pb.x0s, eta=0.01)          # warm-up (the cached plan)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    X, _, _, res = shim.stochastic_solve_batch(T, tp, xs, pb.x0s, eta=0.01)
+    s_dev = time.perf_counter() - t0
+    rows["stochastic_solve_device"] = {"iterations_launched": res[0], "all_stopped_after": res[1],
+                                       "trajectories_launched": res[0] * M * R, "s_per_ascent": s_dev,
+                                       "useful_trajectories": useful, "trajectories_per_s": useful / s_dev,
+                                       "launched_trajectories_per_s": res[0] * M * R / s_dev,
+                                       "steps_per_restart": steps}
+    shim.release_plans()
     print(json.dumps({"config": a.config, "M": M, "R": R, "rows": rows,
                       "note": "whole calls through the C ABI with host pointers (mrbo.shim = MRBO.jl's sequence)"}),
           flush=True)
