@@ -152,6 +152,47 @@ __device__ __forceinline__ double djoin(int lo, int hi) {
   return __builtin_bit_cast(double, (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
+// A fresh register pair holding v's bits: ONE v_mov_b64.  v_permlane16/32_swap overwrite both of
+// their operands, so a swap of a double with itself needs two copies of it while it stays live; the
+// compiler made them per dword (two v_mov_b32 per operand, four per double).  TAG makes the two
+// copies distinct asm statements, so that they are not merged into one.  MRBO_NO_DCOPY: the
+// compiler's copies (A/B).
+template <int TAG>
+__device__ __forceinline__ double dcopy(double v) {
+  double r;
+  if constexpr (TAG == 0) asm("v_mov_b64 %0, %1" : "=v"(r) : "v"(v));
+  else asm("v_mov_b64 %0, %1 ; copy %2" : "=v"(r) : "v"(v), "i"(TAG));
+  return r;
+}
+
+// v_permlane16_swap (M = 16) / v_permlane32_swap (M = 32) of a double with itself, per dword:
+// first = [r0 r0 r2 r2] / [lo lo], second = [r1 r1 r3 r3] / [hi hi] (16-lane rows / 32-lane
+// halves).  KEEP: v stays live after the swap (two copies); else v itself is one operand.
+template <int M, bool KEEP>
+__device__ __forceinline__ void self_swap(double v, double& first, double& second) {
+#ifdef MRBO_NO_DCOPY
+  const double c0 = v, c1 = v;
+#else
+  const double c0 = KEEP ? dcopy<0>(v) : v;
+  const double c1 = dcopy<1>(v);
+#endif
+  int al, ah, bl, bh;
+  dsplit(c0, al, ah);
+  dsplit(c1, bl, bh);
+  if constexpr (M == 16) {
+    const auto l = __builtin_amdgcn_permlane16_swap(al, bl, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(ah, bh, false, false);
+    first = djoin(l[0], h[0]);
+    second = djoin(l[1], h[1]);
+  } else {
+    static_assert(M == 32, "self_swap: M is 16 or 32");
+    const auto l = __builtin_amdgcn_permlane32_swap(al, bl, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(ah, bh, false, false);
+    first = djoin(l[0], h[0]);
+    second = djoin(l[1], h[1]);
+  }
+}
+
 // M = 32 / 16: lanes with bit M clear get a(l) + a(l^M), lanes with it set get b(l^M) + b(l).
 // gfx950's v_permlane32_swap / v_permlane16_swap exchange exactly these cross halves of the
 // register pair in place: two swaps per double and one add -- no select, no LDS round trip.
@@ -177,32 +218,18 @@ __device__ __forceinline__ double swap_fold(double a, double b) {
 // row 16b + n in every lane.
 template <int P>
 __device__ __forceinline__ void row_blocks(double v, double& blk_p, double& blk_p2) {
-  int lo, hi;
-  dsplit(v, lo, hi);
-  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // [r0 r0 r2 r2], [r1 r1 r3 r3]
-  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  const int tlo = P ? a[1] : a[0], thi = P ? b[1] : b[0];
-  const auto c = __builtin_amdgcn_permlane32_swap(tlo, tlo, false, false); // [rP ×4], [rP+2 ×4]
-  const auto d = __builtin_amdgcn_permlane32_swap(thi, thi, false, false);
-  blk_p = djoin(c[0], d[0]);
-  blk_p2 = djoin(c[1], d[1]);
+  double a0, a1;
+  self_swap<16, true>(v, a0, a1);                  // [r0 r0 r2 r2], [r1 r1 r3 r3]
+  self_swap<32, false>(P ? a1 : a0, blk_p, blk_p2); // [rP ×4], [rP+2 ×4]
 }
 
 // All four blocks at once: one v_permlane16_swap and two v_permlane32_swap per dword (blocks 0, 2
 // from the first pl16 half, 1, 3 from the second) instead of a pl16 + pl32 pair per block pair.
 __device__ __forceinline__ void row_blocks4(double v, double& b0, double& b1, double& b2, double& b3) {
-  int lo, hi;
-  dsplit(v, lo, hi);
-  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // [r0 r0 r2 r2], [r1 r1 r3 r3]
-  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  const auto c0 = __builtin_amdgcn_permlane32_swap(a[0], a[0], false, false);   // [r0 ×4], [r2 ×4]
-  const auto d0 = __builtin_amdgcn_permlane32_swap(b[0], b[0], false, false);
-  const auto c1 = __builtin_amdgcn_permlane32_swap(a[1], a[1], false, false);   // [r1 ×4], [r3 ×4]
-  const auto d1 = __builtin_amdgcn_permlane32_swap(b[1], b[1], false, false);
-  b0 = djoin(c0[0], d0[0]);
-  b2 = djoin(c0[1], d0[1]);
-  b1 = djoin(c1[0], d1[0]);
-  b3 = djoin(c1[1], d1[1]);
+  double a0, a1;
+  self_swap<16, true>(v, a0, a1);    // [r0 r0 r2 r2], [r1 r1 r3 r3]
+  self_swap<32, false>(a0, b0, b2);  // [r0 ×4], [r2 ×4]
+  self_swap<32, false>(a1, b1, b3);  // [r1 ×4], [r3 ×4]
 }
 
 // The three broadcast operands of a folded product (bcast_fold_fwd / _bwd) in 3 swaps and 2 copies
@@ -214,12 +241,13 @@ __device__ __forceinline__ void row_blocks4(double v, double& b0, double& b1, do
 //   backward: X is the folded operand (rows 0, 1: block 1, row 2: block 0, row 3 idle) and the
 //             self-swap of Y gives blocks 3 and 2.
 __device__ __forceinline__ void fold_blocks(double v, bool fwd, double& p0, double& p1, double& m) {
-  int lo, hi;
-  dsplit(v, lo, hi);
-  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);   // [r0 r0 r2 r2], [r1 r1 r3 r3]
-  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  const auto xl = __builtin_amdgcn_permlane32_swap(a[1], a[0], false, false);   // X, Y (low dwords)
-  const auto xh = __builtin_amdgcn_permlane32_swap(b[1], b[0], false, false);
+  double a0, a1;
+  self_swap<16, true>(v, a0, a1);   // [r0 r0 r2 r2], [r1 r1 r3 r3]
+  int a0l, a0h, a1l, a1h;
+  dsplit(a0, a0l, a0h);
+  dsplit(a1, a1l, a1h);
+  const auto xl = __builtin_amdgcn_permlane32_swap(a1l, a0l, false, false);   // X, Y (low dwords)
+  const auto xh = __builtin_amdgcn_permlane32_swap(a1h, a0h, false, false);
   const int sl = fwd ? xl[0] : xl[1], sh = fwd ? xh[0] : xh[1];   // the pair to self-swap
   const auto cl = __builtin_amdgcn_permlane32_swap(sl, sl, false, false);
   const auto ch = __builtin_amdgcn_permlane32_swap(sh, sh, false, false);
@@ -232,11 +260,9 @@ __device__ __forceinline__ void fold_blocks(double v, bool fwd, double& p0, doub
 // register with itself leaves the lower half's values in both halves of the first result and the
 // upper half's in both halves of the second (H a compile-time constant after unrolling).
 __device__ __forceinline__ double half_value(double v, int H) {
-  int lo, hi;
-  dsplit(v, lo, hi);
-  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-  return H ? djoin(a[1], b[1]) : djoin(a[0], b[0]);
+  double lo, hi;
+  self_swap<32, true>(v, lo, hi);
+  return H ? hi : lo;
 }
 
 // M = 8, 4, 2, 1: v from a partner lane that differs in bit M and agrees on all higher bits
@@ -273,8 +299,13 @@ __device__ __forceinline__ void fold_step(double* v, int lane, int& idx) {
 }
 template <int M>
 __device__ __forceinline__ double fold_all(double v) {
-  if constexpr (M >= 16) return swap_fold<M>(v, v);
-  else return v + dpp_partner<M>(v);
+  if constexpr (M >= 16) {
+    double a, b;   // a(l) + a(l^M) in every lane: the self-swap's two halves summed
+    self_swap<M, false>(v, a, b);
+    return a + b;
+  } else {
+    return v + dpp_partner<M>(v);
+  }
 }
 
 // Transpose-reduce K per-lane values across the 64 lanes: log2(K) transpose steps (pairs
@@ -326,6 +357,24 @@ __device__ __forceinline__ void half_reduce(double (&v)[K], double* red, int lan
   red[idx] = v[0];
 }
 
+// min over the first LANES lanes' values (LANES = 64, or 32 within each half-wave) in every lane, by
+// the butterfly of wave_allreduce1: permlane self-swaps across lane bits 5 / 4, DPP moves below
+// (no ds_bpermute and no per-lane shuffle address).  min is exact, so every lane holds the same bits.
+template <int LANES>
+__device__ __forceinline__ double lanes_min(double v) {
+  double a, b;
+  if constexpr (LANES == 64) {
+    self_swap<32, false>(v, a, b);
+    v = fmin(a, b);
+  }
+  self_swap<16, false>(v, a, b);
+  v = fmin(a, b);
+  v = fmin(v, dpp_partner<8>(v));
+  v = fmin(v, dpp_partner<4>(v));
+  v = fmin(v, dpp_partner<2>(v));
+  return fmin(v, dpp_partner<1>(v));
+}
+
 // Sum over the 64 lanes in EVERY lane, no LDS round trip: the butterfly of wave_reduce<1>
 // (each step adds the partner's value; a + b == b + a, so all lanes hold the same bits, those
 // wave_reduce<1> stores for lane 0).
@@ -353,17 +402,24 @@ __device__ __forceinline__ double sconst() {
   return djoin(lo, hi);
 }
 
-// a·b + c with c a lane-uniform constant held in an SGPR pair (sconst): one VOP3 v_fma_f64 with the
-// SGPR operand.  A plain fma() with an SGPR addend is shrunk by the compiler to v_fmac_f64, whose
-// addend is also its destination, so every Horner step copied its coefficient into a VGPR pair
-// first (two v_mov_b32 per step, three VALU instructions per polynomial term).  Not volatile: the
+// A quiet NaN materialised at its use (two SALU moves): the compiler hoisted the NAN literal of the
+// failure outputs into a VGPR pair held across the persistent loop, and spilled it.
+__device__ __forceinline__ double qnan() { return sconst<0u, 0x7ff80000u>(); }
+
+// a·b + C with C = the compile-time double of bits (HI, LO), materialised in an SGPR pair (sconst):
+// one VOP3 v_fma_f64 with the SGPR operand.  A plain fma() with an SGPR addend is shrunk by the
+// compiler to v_fmac_f64, whose addend is also its destination, so every Horner step copied its
+// coefficient into a VGPR pair first (two v_mov_b32 per step, three VALU instructions per
+// polynomial term).  The addend is a template constant, so only a lane-uniform value can reach the
+// "s" operand (a per-lane value there would be silently read from lane 0).  Not volatile: the
 // scheduler moves it like any arithmetic.  MRBO_NO_FMA_SC: plain fma (A/B).
-__device__ __forceinline__ double fma_sc(double a, double b, double c) {
+template <unsigned LO, unsigned HI>
+__device__ __forceinline__ double fma_sc(double a, double b) {
 #ifdef MRBO_NO_FMA_SC
-  return fma(a, b, c);
+  return fma(a, b, sconst<LO, HI>());
 #else
   double d;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(sconst<LO, HI>()));
   return d;
 #endif
 }
@@ -384,10 +440,10 @@ __device__ __forceinline__ double fexp(double x) {
   double c10e = sconst<0xfca7ab0cu, 0x3e928af3u>();
   asm volatile("" : "+v"(c10e));
   const double b5 = fma(sconst<0x6a5dcb37u, 0x3e5ade15u>(), r, c10e);                 // c10 + c11 r
-  const double b4 = fma_sc(r, sconst<0x623fde64u, 0x3ec71deeu>(), sconst<0x7c89e6b0u, 0x3efa0199u>());   // c8 + c9 r
-  const double b3 = fma_sc(r, sconst<0x14761f6eu, 0x3f2a01a0u>(), sconst<0x1852b7b0u, 0x3f56c16cu>());
-  const double b2 = fma_sc(r, sconst<0x11122322u, 0x3f811111u>(), sconst<0x555502a1u, 0x3fa55555u>());
-  const double b1 = fma_sc(r, sconst<0x55555511u, 0x3fc55555u>(), sconst<0x0000000bu, 0x3fe00000u>());
+  const double b4 = fma_sc<0x7c89e6b0u, 0x3efa0199u>(r, sconst<0x623fde64u, 0x3ec71deeu>());   // c8 + c9 r
+  const double b3 = fma_sc<0x1852b7b0u, 0x3f56c16cu>(r, sconst<0x14761f6eu, 0x3f2a01a0u>());
+  const double b2 = fma_sc<0x555502a1u, 0x3fa55555u>(r, sconst<0x11122322u, 0x3f811111u>());
+  const double b1 = fma_sc<0x0000000bu, 0x3fe00000u>(r, sconst<0x55555511u, 0x3fc55555u>());
   const double b0 = r + 1.0;
   const double q2 = fma(b5, r2, b4), q1 = fma(b3, r2, b2), q0 = fma(b1, r2, b0);
   const double p = fma(fma(q2, r4, q1), r4, q0);
@@ -396,14 +452,14 @@ __device__ __forceinline__ double fexp(double x) {
   double c10 = sconst<0xfca7ab0cu, 0x3e928af3u>();
   asm volatile("" : "+v"(c10));   // one of the first step's two constants must live in VGPRs
   double p = fma(sconst<0x6a5dcb37u, 0x3e5ade15u>(), r, c10);
-  p = fma_sc(r, p, sconst<0x623fde64u, 0x3ec71deeu>());
-  p = fma_sc(r, p, sconst<0x7c89e6b0u, 0x3efa0199u>());
-  p = fma_sc(r, p, sconst<0x14761f6eu, 0x3f2a01a0u>());
-  p = fma_sc(r, p, sconst<0x1852b7b0u, 0x3f56c16cu>());
-  p = fma_sc(r, p, sconst<0x11122322u, 0x3f811111u>());
-  p = fma_sc(r, p, sconst<0x555502a1u, 0x3fa55555u>());
-  p = fma_sc(r, p, sconst<0x55555511u, 0x3fc55555u>());
-  p = fma_sc(r, p, sconst<0x0000000bu, 0x3fe00000u>());
+  p = fma_sc<0x623fde64u, 0x3ec71deeu>(r, p);
+  p = fma_sc<0x7c89e6b0u, 0x3efa0199u>(r, p);
+  p = fma_sc<0x14761f6eu, 0x3f2a01a0u>(r, p);
+  p = fma_sc<0x1852b7b0u, 0x3f56c16cu>(r, p);
+  p = fma_sc<0x11122322u, 0x3f811111u>(r, p);
+  p = fma_sc<0x555502a1u, 0x3fa55555u>(r, p);
+  p = fma_sc<0x55555511u, 0x3fc55555u>(r, p);
+  p = fma_sc<0x0000000bu, 0x3fe00000u>(r, p);
   p = fma(r, p, 1.0);
   p = fma(r, p, 1.0);
   double e = __builtin_ldexp(p, (int)k);
@@ -591,34 +647,34 @@ __device__ __forceinline__ PhiPair ei_phi_Phi(double z) {
   {
     double pe_h = sconst<0xf1ab7ccbu, 0x3dd09a8bu>();
     asm volatile("" : "+v"(pe_h));
-    pe_h = fma_sc(t2, pe_h, sconst<0x73fda30du, 0x3e06db11u>());
-    pe_h = fma_sc(t2, pe_h, sconst<0xf4266242u, 0xbe427e42u>());
-    pe_h = fma_sc(t2, pe_h, sconst<0x1ed381c5u, 0xbe672292u>());
-    pe_h = fma_sc(t2, pe_h, sconst<0xb901a919u, 0x3ec385e7u>());
-    pe_h = fma_sc(t2, pe_h, sconst<0x645605dcu, 0xbf066e11u>());
+    pe_h = fma_sc<0x73fda30du, 0x3e06db11u>(t2, pe_h);
+    pe_h = fma_sc<0xf4266242u, 0xbe427e42u>(t2, pe_h);
+    pe_h = fma_sc<0x1ed381c5u, 0xbe672292u>(t2, pe_h);
+    pe_h = fma_sc<0xb901a919u, 0x3ec385e7u>(t2, pe_h);
+    pe_h = fma_sc<0x645605dcu, 0xbf066e11u>(t2, pe_h);
     double pe_l = sconst<0xfbfa9e67u, 0x3f427e65u>();
     asm volatile("" : "+v"(pe_l));
-    pe_l = fma_sc(t2, pe_l, sconst<0xc891e642u, 0xbf7143c4u>());
-    pe_l = fma_sc(t2, pe_l, sconst<0xf77381b3u, 0xbfa8ff5eu>());
-    pe_l = fma_sc(t2, pe_l, sconst<0x0c35056au, 0xbfbd7683u>());
-    pe_l = fma_sc(t2, pe_l, sconst<0x284b1971u, 0xbf859e2cu>());
-    pe_l = fma_sc(t2, pe_l, sconst<0x9a0ee914u, 0x3ff3e0a9u>());
+    pe_l = fma_sc<0xc891e642u, 0xbf7143c4u>(t2, pe_l);
+    pe_l = fma_sc<0xf77381b3u, 0xbfa8ff5eu>(t2, pe_l);
+    pe_l = fma_sc<0x0c35056au, 0xbfbd7683u>(t2, pe_l);
+    pe_l = fma_sc<0x284b1971u, 0xbf859e2cu>(t2, pe_l);
+    pe_l = fma_sc<0x9a0ee914u, 0x3ff3e0a9u>(t2, pe_l);
     const double pe_ = fma(u6, pe_h, pe_l);
     pe = pe_;
     double po_h = sconst<0x617fb329u, 0xbe1406aau>();
     asm volatile("" : "+v"(po_h));
-    po_h = fma_sc(t2, po_h, sconst<0xdb5ecc9au, 0x3e4d421du>());
-    po_h = fma_sc(t2, po_h, sconst<0x3786431fu, 0xbe79e096u>());
-    po_h = fma_sc(t2, po_h, sconst<0xc09ddffau, 0x3ea42eb1u>());
-    po_h = fma_sc(t2, po_h, sconst<0x97b263b0u, 0xbecffe87u>());
-    po_h = fma_sc(t2, po_h, sconst<0x306b92a0u, 0x3ef97053u>());
+    po_h = fma_sc<0xdb5ecc9au, 0x3e4d421du>(t2, po_h);
+    po_h = fma_sc<0x3786431fu, 0xbe79e096u>(t2, po_h);
+    po_h = fma_sc<0xc09ddffau, 0x3ea42eb1u>(t2, po_h);
+    po_h = fma_sc<0x97b263b0u, 0xbecffe87u>(t2, po_h);
+    po_h = fma_sc<0x306b92a0u, 0x3ef97053u>(t2, po_h);
     double po_l = sconst<0x5777da87u, 0xbf1fda8au>();
     asm volatile("" : "+v"(po_l));
-    po_l = fma_sc(t2, po_l, sconst<0xf98105c2u, 0xbf33cf36u>());
-    po_l = fma_sc(t2, po_l, sconst<0x67477473u, 0x3f938ec6u>());
-    po_l = fma_sc(t2, po_l, sconst<0x6045eed1u, 0x3fb68610u>());
-    po_l = fma_sc(t2, po_l, sconst<0xec6b3bb9u, 0x3fb8f702u>());
-    po_l = fma_sc(t2, po_l, sconst<0x20ea5946u, 0xbfc1ebd2u>());
+    po_l = fma_sc<0xf98105c2u, 0xbf33cf36u>(t2, po_l);
+    po_l = fma_sc<0x67477473u, 0x3f938ec6u>(t2, po_l);
+    po_l = fma_sc<0x6045eed1u, 0x3fb68610u>(t2, po_l);
+    po_l = fma_sc<0xec6b3bb9u, 0x3fb8f702u>(t2, po_l);
+    po_l = fma_sc<0x20ea5946u, 0xbfc1ebd2u>(t2, po_l);
     const double po_ = fma(u6, po_h, po_l);
     po = po_;
   }
@@ -627,31 +683,31 @@ __device__ __forceinline__ PhiPair ei_phi_Phi(double z) {
   {
     double pe_ = sconst<0xf1ab7ccbu, 0x3dd09a8bu>();
     asm volatile("" : "+v"(pe_));
-    pe_ = fma_sc(t2, pe_, sconst<0x73fda30du, 0x3e06db11u>());
-    pe_ = fma_sc(t2, pe_, sconst<0xf4266242u, 0xbe427e42u>());
-    pe_ = fma_sc(t2, pe_, sconst<0x1ed381c5u, 0xbe672292u>());
-    pe_ = fma_sc(t2, pe_, sconst<0xb901a919u, 0x3ec385e7u>());
-    pe_ = fma_sc(t2, pe_, sconst<0x645605dcu, 0xbf066e11u>());
-    pe_ = fma_sc(t2, pe_, sconst<0xfbfa9e67u, 0x3f427e65u>());
-    pe_ = fma_sc(t2, pe_, sconst<0xc891e642u, 0xbf7143c4u>());
-    pe_ = fma_sc(t2, pe_, sconst<0xf77381b3u, 0xbfa8ff5eu>());
-    pe_ = fma_sc(t2, pe_, sconst<0x0c35056au, 0xbfbd7683u>());
-    pe_ = fma_sc(t2, pe_, sconst<0x284b1971u, 0xbf859e2cu>());
-    pe_ = fma_sc(t2, pe_, sconst<0x9a0ee914u, 0x3ff3e0a9u>());
+    pe_ = fma_sc<0x73fda30du, 0x3e06db11u>(t2, pe_);
+    pe_ = fma_sc<0xf4266242u, 0xbe427e42u>(t2, pe_);
+    pe_ = fma_sc<0x1ed381c5u, 0xbe672292u>(t2, pe_);
+    pe_ = fma_sc<0xb901a919u, 0x3ec385e7u>(t2, pe_);
+    pe_ = fma_sc<0x645605dcu, 0xbf066e11u>(t2, pe_);
+    pe_ = fma_sc<0xfbfa9e67u, 0x3f427e65u>(t2, pe_);
+    pe_ = fma_sc<0xc891e642u, 0xbf7143c4u>(t2, pe_);
+    pe_ = fma_sc<0xf77381b3u, 0xbfa8ff5eu>(t2, pe_);
+    pe_ = fma_sc<0x0c35056au, 0xbfbd7683u>(t2, pe_);
+    pe_ = fma_sc<0x284b1971u, 0xbf859e2cu>(t2, pe_);
+    pe_ = fma_sc<0x9a0ee914u, 0x3ff3e0a9u>(t2, pe_);
     pe = pe_;
     double po_ = sconst<0x617fb329u, 0xbe1406aau>();
     asm volatile("" : "+v"(po_));
-    po_ = fma_sc(t2, po_, sconst<0xdb5ecc9au, 0x3e4d421du>());
-    po_ = fma_sc(t2, po_, sconst<0x3786431fu, 0xbe79e096u>());
-    po_ = fma_sc(t2, po_, sconst<0xc09ddffau, 0x3ea42eb1u>());
-    po_ = fma_sc(t2, po_, sconst<0x97b263b0u, 0xbecffe87u>());
-    po_ = fma_sc(t2, po_, sconst<0x306b92a0u, 0x3ef97053u>());
-    po_ = fma_sc(t2, po_, sconst<0x5777da87u, 0xbf1fda8au>());
-    po_ = fma_sc(t2, po_, sconst<0xf98105c2u, 0xbf33cf36u>());
-    po_ = fma_sc(t2, po_, sconst<0x67477473u, 0x3f938ec6u>());
-    po_ = fma_sc(t2, po_, sconst<0x6045eed1u, 0x3fb68610u>());
-    po_ = fma_sc(t2, po_, sconst<0xec6b3bb9u, 0x3fb8f702u>());
-    po_ = fma_sc(t2, po_, sconst<0x20ea5946u, 0xbfc1ebd2u>());
+    po_ = fma_sc<0xdb5ecc9au, 0x3e4d421du>(t2, po_);
+    po_ = fma_sc<0x3786431fu, 0xbe79e096u>(t2, po_);
+    po_ = fma_sc<0xc09ddffau, 0x3ea42eb1u>(t2, po_);
+    po_ = fma_sc<0x97b263b0u, 0xbecffe87u>(t2, po_);
+    po_ = fma_sc<0x306b92a0u, 0x3ef97053u>(t2, po_);
+    po_ = fma_sc<0x5777da87u, 0xbf1fda8au>(t2, po_);
+    po_ = fma_sc<0xf98105c2u, 0xbf33cf36u>(t2, po_);
+    po_ = fma_sc<0x67477473u, 0x3f938ec6u>(t2, po_);
+    po_ = fma_sc<0x6045eed1u, 0x3fb68610u>(t2, po_);
+    po_ = fma_sc<0xec6b3bb9u, 0x3fb8f702u>(t2, po_);
+    po_ = fma_sc<0x20ea5946u, 0xbfc1ebd2u>(t2, po_);
     po = po_;
   }
 #endif
@@ -778,11 +834,17 @@ __host__ __device__ __forceinline__ unsigned long long splitmix64(unsigned long 
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
   return z ^ (z >> 31);
 }
-__host__ __device__ __forceinline__ double dual_uniform(unsigned long long seed, long long traj, int j, int k) {
-  unsigned long long key = splitmix64(seed ^ 0x5851F42D4C957F2DULL);
-  key = splitmix64(key ^ (unsigned long long)traj);
+__host__ __device__ __forceinline__ unsigned long long dual_key0(unsigned long long seed) {
+  return splitmix64(seed ^ 0x5851F42D4C957F2DULL);
+}
+// the same from the seed's first key (dual_key0), which the kernel keeps in LDS
+__host__ __device__ __forceinline__ double dual_uniform_k(unsigned long long key0, long long traj, int j, int k) {
+  unsigned long long key = splitmix64(key0 ^ (unsigned long long)traj);
   key = splitmix64(key ^ (((unsigned long long)(unsigned)j << 32) | (unsigned)k));
   return (double)(key >> 11) * (1.0 / 9007199254740992.0);
+}
+__host__ __device__ __forceinline__ double dual_uniform(unsigned long long seed, long long traj, int j, int k) {
+  return dual_uniform_k(dual_key0(seed), traj, j, k);
 }
 
 // value of a double in lane k (wave-uniform k)

@@ -105,7 +105,7 @@ struct Lay {
   static constexpr int U_HF = U_UB + D;                  // fantasy rows: [x - X_r (D), g1, g2]  FMAX×(D+2)
   static constexpr int U_STAMP = U_HF + FMAX * (D + 2);   // cycle accumulators (MRBO_STAMPS)
   static constexpr int U_KC = U_STAMP + NSTAMP_SLOTS;             // launch constants (KC_*), see wave_setup
-  static constexpr int U_SIZE = ((U_KC + 13) + 1) & ~1;
+  static constexpr int U_SIZE = ((U_KC + 15) + 1) & ~1;
   static constexpr int G12 = 3 * NRL;                    // per-lane [g1, g2, Y0] of the base rows
   static constexpr int EC = SQ ? (2 * FMAX + 1) * NRL : 0;  // E (FMAX×NRL) + C ((FMAX+1)×NRL) in LDS
   static constexpr int WAVE_LDS = BROWS * BS + REDN + U_SIZE + G12 + EC;
@@ -149,7 +149,9 @@ enum { SC_MU = 0, SC_SIG = 1, SC_ALPHA = 2, SC_G00 = 3, SC_VAR = 4, SC_GMU = 5, 
 // (a v_readlane per reload, on the VALU).  Branch conditions keep the kernel-argument copy.
 enum { KC_PSI0 = 0, KC_D2PSI0 = 1, KC_THETA = 2, KC_SIGTOL = 3, KC_GTOL = 4, KC_GCMU = 5, KC_GCSIG = 6,
        KC_GCD2 = 7, KC_XTOL = 8, KC_FTOL = 9, KC_HTOL = 10, KC_SN2 = 11,
-       KC_BOX = 12 };   // max_a (ub_a − lb_a): the Newton step's length cap
+       KC_BOX = 12,     // max_a (ub_a − lb_a): the Newton step's length cap
+       KC_FMINB = 13,   // fmin of the base surrogate (each trajectory's surface −1)
+       KC_DXKEY = 14 }; // splitmix64(seed ^ C): the δx counter RNG's first key (bits of a double)
 #define KCV(F) (W.U[Lay<D, RPL, HW>::U_KC + KC_##F])
 
 // ∂_lane c(x) by unrolled select (lane < D; a runtime index would put gc in scratch)
@@ -382,11 +384,9 @@ __device__ __forceinline__ void bcast_product_k(double (&acc)[K], const double (
       double bp[K];
 #pragma unroll
       for (int c = 0; c < K; ++c) {
-        int lo, hi;
-        dsplit(v[c], lo, hi);
-        const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-        const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-        bp[c] = p == 0 ? djoin(a[0], b[0]) : djoin(a[1], b[1]);
+        double b0, b1;
+        self_swap<16, true>(v[c], b0, b1);
+        bp[c] = p == 0 ? b0 : b1;
       }
       bcast_run<K, 8 * JSTRIDE>(acc, bp, a0 + 8u * 16u * p * JSTRIDE);
     }
@@ -2194,12 +2194,7 @@ __device__ __forceinline__ void batch_start_values(WaveCtx<D, RPL, HW>& W, const
         double g1, g2;
         rad_eval(W.rad, rho2, v, g1, g2);
       }
-      int lo, hi;
-      dsplit(v, lo, hi);
-      const auto l2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-      const auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-      pf[2 * e] = djoin(l2[0], h2[0]);       // lower half's value (q = 2e)
-      pf[2 * e + 1] = djoin(l2[1], h2[1]);   // upper half's value (q = 2e + 1)
+      self_swap<32, false>(v, pf[2 * e], pf[2 * e + 1]);   // lower half's value (q = 2e), upper half's (2e + 1)
     }
 #pragma unroll
     for (int q = 0; q < FMAX; ++q) pf[q] = (q < nf) ? pf[q] : 0.0;
@@ -2334,9 +2329,7 @@ __device__ __forceinline__ int multistart(WaveCtx<D, RPL, HW>& W, const KParams&
       const int kn = __builtin_ctzll(nanm);
       if (!best_nan || kn < best) { win = kn; win_nan = true; }
     } else if (!best_nan) {
-      double m = mine ? f_lane : INFINITY;
-#pragma unroll
-      for (int o = Lay<D, RPL, HW>::LANES / 2; o >= 1; o >>= 1) m = fmin(m, __shfl_xor(m, o, WAVE));
+      const double m = lanes_min<Lay<D, RPL, HW>::LANES>(mine ? f_lane : INFINITY);
       const unsigned long long eq = hw_ballot<HW>(mine && f_lane == m, W.half);
       if (eq) {
         const int km = __builtin_ctzll(eq);
@@ -2600,7 +2593,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL, HW>& W, const KParams
   // surface -1 = the base surrogate; C[0] = c0
 #pragma unroll
   for (int s = 0; s < RPL; ++s) W.C[lane + WAVE * s] = kp.c0[lane + WAVE * s];
-  if (lane == 0) U[Ly::U_FMIN] = kp.fmin_base;
+  if (lane == 0) U[Ly::U_FMIN] = U[Ly::U_KC + KC_FMINB];
   // kp.base_solve: this item is start tr of a base_solve launch (one multistart call site: the
   // loop below runs its solve step once, on surface -1, for start tr alone)
   const bool bsolve = kp.base_solve != 0;
@@ -2666,7 +2659,7 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL, HW>& W, const KParams
   }
   wave_sync();
   const long long oidx = (long long)m + (long long)M * r;
-  if (kp.obs && lane <= h) kp.obs[oidx * (h + 1) + lane] = st ? NAN : U[Ly::U_YF + lane];
+  if (kp.obs && lane <= h) kp.obs[oidx * (h + 1) + lane] = st ? qnan() : U[Ly::U_YF + lane];
   if (kp.evals && lane == 0) {
     kp.evals[NCOUNT * oidx + 0] = nevals.grad;
     kp.evals[NCOUNT * oidx + 1] = nevals.value;
@@ -2675,8 +2668,8 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL, HW>& W, const KParams
     kp.evals[NCOUNT * oidx + 4] = 0;
   }
   if (st) {
-    if (lane == 0) { kp.values[oidx] = NAN; kp.status[oidx] = st; if (kp.grad_theta) kp.grad_theta[oidx] = NAN; }
-    if (kp.grad_x && lane < D) kp.grad_x[oidx * D + lane] = NAN;
+    if (lane == 0) { kp.values[oidx] = qnan(); kp.status[oidx] = st; if (kp.grad_theta) kp.grad_theta[oidx] = qnan(); }
+    if (kp.grad_x && lane < D) kp.grad_x[oidx * D + lane] = qnan();
     return;
   }
   STAMP(W, 11);
@@ -2711,7 +2704,8 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL, HW>& W, const KParams
         if (lane < D) {
           U[Ly::U_DX + lane] = kp.dual_y
               ? kp.dual_y[(long long)lane + D * ((j - 1) + (long long)h * (m + (long long)M * r))]
-              : dual_uniform(kp.seed, (long long)(kp.sample_offset + m), j, lane);   // keyed by the global sample alone
+              : dual_uniform_k(__builtin_bit_cast(unsigned long long, U[Ly::U_KC + KC_DXKEY]),
+                               (long long)(kp.sample_offset + m), j, lane);   // keyed by the global sample alone
         }
         wave_sync();
         // i == j: solve_dual_x(j) (rollout.jl:150-191) then pair (j, j-1);
@@ -2768,15 +2762,15 @@ __device__ __forceinline__ void trajectory(WaveCtx<D, RPL, HW>& W, const KParams
   if (lane == 0) {
     kp.values[base] = value;
     kp.status[base] = st;
-    if (kp.grad_theta) kp.grad_theta[base] = (grad_zero || st) ? (st ? NAN : 0.0) : -gth;
+    if (kp.grad_theta) kp.grad_theta[base] = (grad_zero || st) ? (st ? qnan() : 0.0) : -gth;
   }
   if (kp.grad_x && lane < D) {
     double gx = 0.0;
     if (!grad_zero) gx = -(U[Ly::U_GMU0 + lane] * U[Ly::U_YBAR] + U[Ly::U_ACC + lane]);
-    if (st) gx = NAN;
+    if (st) gx = qnan();
     kp.grad_x[base * D + lane] = gx;
   }
-  if (st && lane == 0) kp.values[base] = NAN;
+  if (st && lane == 0) kp.values[base] = qnan();
   if (kp.evals && lane == 0) {
     kp.evals[NCOUNT * base + 3] = nevals.rich;
     kp.evals[NCOUNT * base + 4] = nevals.pairs;
@@ -2861,6 +2855,10 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL, HW>& W, const KParams
     double box = 0.0;
     for (int a = 0; a < D; ++a) box = fmax(box, kp.ubs[a] - kp.lbs[a]);
     kc[KC_BOX] = box;
+    // read back per trajectory from LDS: held in registers across the persistent loop, these two
+    // 64-bit values were VGPR spills (8 B of scratch per lane each)
+    kc[KC_FMINB] = kp.fmin_base;
+    kc[KC_DXKEY] = __builtin_bit_cast(double, dual_key0(kp.seed));
   }
 }
 

@@ -39,11 +39,15 @@ Per trajectory t, with normwise relative errors
      policy points' own rounding difference Δx on the adjoint (‖∂x̄_j/∂x_j‖ ≤ κ·‖∂H/∂x‖/‖H‖, and
      ‖∂H/∂x‖/‖H‖ ≤ 10 is the kernel's derivative ratio ≈ √5/ℓ at ℓ ≥ 0.5); Newton work per counter
      (gradient, value, Hessian) summed over them within 1 % of the oracle's, and equal per
-     trajectory (work_exact, every case but C4's): on flat acquisition surfaces the line search of
-     a start that does not win the multistart is rounding-sensitive -- two builds of the ORACLE
-     itself (-ffp-contract=off vs -O3 -march=native) disagree on 56 of 122 identical-path C4
-     trajectories at ℓ = 0.5 (totals within 0.2 %) and on none at C3 (tests/test_oracle.py), so
-     C4 asserts the totals only
+     trajectory (work_exact, every case but the rounding-sensitive surfaces): on flat acquisition
+     surfaces the Newton decisions of a start that does not win the multistart are
+     rounding-sensitive -- two builds of the ORACLE itself (-ffp-contract=off vs -O3 -march=native)
+     disagree on 460 of 989 identical-path C4 trajectories at ℓ = 0.5 by up to (3, 40, 3) and on
+     none at C3 (tests/test_oracle.py) -- so C4 at ℓ = 0.5 and C5 + NonUniformCost hold every
+     identical path to within 3 Newton steps per trajectory (work_exact="steps"), with the two
+     oracle builds' own disagreement measured beside it (envelope); flips there are bounded by
+     max(0.1 %, twice the oracle builds' flip fraction on the same inputs) (C5 + cost at ℓ = 1:
+     the builds flip on 4 of 128)
      ETO: no flips → normwise 1e-9 relative per block (mean value, std value, mean ∇x);
      flips → each mean within 3·σ/√M of the oracle's (σ the oracle's std)
   Non-vacuity (every case; a case that only exercises the forward rollout says so with
@@ -206,13 +210,19 @@ def tight_value_stats(dv, v, vmax):
     return dict(over_tight=int((dv > tt).sum()), tight_margin_max=float((dv / tt).max()), tight_tol_min=float(tt.min()))
 
 
-def _compare(key, g, r, o, o_replay, M, kind="full", work_exact=True, work_agree=None):
+MAX_LS = 20          # backtracking trials per Newton step (the plans' max_ls)
+WORK_STEPS = 3       # "steps" rule: per-trajectory work within this many Newton steps
+
+
+def _compare(key, g, r, o, o_replay, M, kind="full", work_exact=True, builds=None):
     """The T2 / T3 assertions above and the non-vacuity guard; records the measured statistics
-    under `key`.  work_exact: assert per-trajectory Newton work equality on the identical paths
-    (all cases but C4's, module docstring).  work_agree (per trajectory, flat): the trajectories on
-    which the oracle's two builds agree on the path and on every work counter -- where rounding
-    alone does not decide the line-search work, the GPU's per-trajectory work must equal the
-    oracle's (C4, whose identical paths are otherwise held to the totals only)."""
+    under `key`.  work_exact: True asserts per-trajectory Newton work equality on the identical
+    paths; "steps" asserts it per trajectory to within WORK_STEPS Newton steps (≤ 3 gradient and
+    Hessian evaluations, ≤ 3·(max_ls + 1) value evaluations) -- the rounding envelope of the
+    rounding-sensitive surfaces (C4 at ℓ = 0.5, C5 + NonUniformCost), where the oracle's own two
+    builds differ by up to (3, 40, 3) on 460 of 989 identical C4 paths; False: totals only.
+    builds: the oracle's two builds compared on the same inputs (_end_to_end envelope): their flip
+    fraction widens the flip bar to max(FLIP_MAX, 2 × theirs), and their statistics are recorded."""
     assert kind in ("full", "forward")
     assert (r["status"] == 0).all() and (o["status"] == 0).all() and (o_replay["status"] == 0).all()
     dx = np.abs(r["policy_x"] - o["policy_x"]) / (1 + np.abs(o["policy_x"]))
@@ -258,6 +268,17 @@ def _compare(key, g, r, o, o_replay, M, kind="full", work_exact=True, work_agree
     sd_o = np.concatenate([e_o[1:2], e_o[2 + d:2 + 2 * d]])
     dev = np.abs(np.concatenate([e_r[0:1], e_r[2:2 + d]]) - np.concatenate([e_o[0:1], e_o[2:2 + d]]))
     stats["eto_mean_max_in_se"] = float(np.max(dev / np.maximum(sd_o / np.sqrt(M), 1e-300)))
+    flip_max = FLIP_MAX
+    if builds is not None:
+        stats["oracle_builds"] = builds
+        flip_max = max(FLIP_MAX, 2.0 * builds["flip_fraction"])
+    if work_exact == "steps":
+        dw = np.abs(evals_r[:, exact] - evals_o[:, exact])
+        lim = np.array([WORK_STEPS, WORK_STEPS * (MAX_LS + 1), WORK_STEPS])[:, None]
+        stats["work_steps"] = dict(identical=int(exact.sum()), unequal=int((dw > 0).any(axis=0).sum()),
+                                   max_diff=dw.max(axis=1).tolist() if dw.size else [0, 0, 0],
+                                   over=int((dw > lim).any(axis=0).sum()))
+    stats["flip_max"] = flip_max
     _REPORT[key] = stats
     # non-vacuity
     assert cov["gpu_grad_evals"] > 0, stats
@@ -268,18 +289,14 @@ def _compare(key, g, r, o, o_replay, M, kind="full", work_exact=True, work_agree
     assert stats["replay_value_tight"]["over_tight"] == 0, stats
     assert stats["replay_grad"]["over_tol"] == 0, stats
     # T3
-    assert stats["flip_fraction"] <= FLIP_MAX, stats
+    assert stats["flip_fraction"] <= flip_max, stats
     assert stats["identical_value_bound"]["over_bound"] == 0, stats
     assert stats["identical_value_tight"]["over_tight"] == 0, stats
     assert stats["identical_grad"]["over_tol"] == 0, stats
-    if work_exact:
+    if work_exact is True:
         assert stats["work_unequal_identical"] == 0, stats
-    if work_agree is not None:
-        m = exact & work_agree
-        stats["work_agree"] = dict(identical=int(exact.sum()), oracle_builds_agree=int(m.sum()),
-                                   unequal=int((evals_r[:, m] != evals_o[:, m]).any(axis=0).sum()))
-        assert m.sum() >= 0.25 * exact.sum(), stats   # not vacuous
-        assert stats["work_agree"]["unequal"] == 0, stats
+    elif work_exact == "steps":
+        assert stats["work_steps"]["over"] == 0, stats
     tg, to = np.asarray(stats["work_totals"]["gpu"], float), np.asarray(stats["work_totals"]["oracle"], float)
     assert np.all(np.abs(tg - to) <= 0.01 * np.maximum(to, 1.0)), stats
     if not flip.any():
@@ -318,12 +335,14 @@ ORACLE_FAST = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__fil
 
 
 def _end_to_end(oracle, key, g, M, cost=None, plan_opts=None, kind="full", htol=1e-4, rule="EI", theta=0.0,
-                ghq=None, work_exact=True):
+                ghq=None, work_exact=True, envelope=False):
     """GPU launch, the oracle on the same inputs, the oracle's replay of the GPU's policy points, then
     _compare.  rule / theta: the base decision rule (EI, POI, LCB); ghq = (nodes, weights): the
     Gauss–Hermite estimator instead of Monte-Carlo draws (M = the number of node vectors).
-    work_exact = "agree": the oracle's second build (-O3 -march=native, oracle/Makefile) runs the
-    same inputs too, and per-trajectory work equality is asserted where its two builds agree."""
+    envelope: the oracle's second build (-O3 -march=native, oracle/Makefile: the same algorithm
+    under different rounding) runs the same inputs too, and its disagreement with the checker --
+    flips, per-trajectory work on identical paths -- is the measured rounding envelope of the
+    surface (_compare's `builds`)."""
     opts = dict(plan_opts or {})
     if htol != 1e-4:
         opts["htol"] = htol
@@ -340,8 +359,8 @@ def _end_to_end(oracle, key, g, M, cost=None, plan_opts=None, kind="full", htol=
     rp = np.asfortranarray(r["policy_x"][:, 1:])
     o2 = oracle.simulate_mc(_osur(oracle, g), g["x0s"], rn, g["xstarts"], g["lbs"], g["ubs"], int(g["h"]),
                             replay_x=rp, want_policy=False, want_kappa=True, **kw)
-    agree = None
-    if work_exact == "agree":
+    builds = None
+    if envelope:
         assert os.path.exists(ORACLE_FAST), "the oracle's timing build (make -C oracle) is needed"
         try:
             oracle.use_library(ORACLE_FAST)
@@ -349,9 +368,11 @@ def _end_to_end(oracle, key, g, M, cost=None, plan_opts=None, kind="full", htol=
         finally:
             oracle.use_library(None)
         dxo = (np.abs(of["policy_x"] - o["policy_x"]) / (1 + np.abs(o["policy_x"]))).max(axis=(0, 1)).ravel(order="F")
-        agree = (dxo <= 1e-12) & (of["evals"].reshape(3, -1, order="F") ==
-                                  o["evals"].reshape(3, -1, order="F")).all(axis=0)
-        work_exact = False
-    return _compare(key, g, r, o, o2, M, kind=kind, work_exact=work_exact, work_agree=agree)
+        ido = dxo <= 1e-12
+        dwo = np.abs(of["evals"].reshape(3, -1, order="F") - o["evals"].reshape(3, -1, order="F"))[:, ido]
+        builds = dict(flips=int((dxo > 1e-6).sum()), flip_fraction=float((dxo > 1e-6).mean()),
+                      identical=int(ido.sum()), work_unequal_identical=int((dwo > 0).any(axis=0).sum()),
+                      work_max_diff=dwo.max(axis=1).tolist() if dwo.size else [0, 0, 0])
+    return _compare(key, g, r, o, o2, M, kind=kind, work_exact=work_exact, builds=builds)
 
 

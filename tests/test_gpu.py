@@ -53,7 +53,7 @@ def test_end_to_end_vs_oracle(gpu, oracle, name, M, R, ell, kind):
     with a lengthscale at the design spacing (dense K; at ℓ = 1 its K is nearly the identity)."""
     g = _problem_arrays(name, M, R, ell=ell)
     _end_to_end(oracle, f"{name} small ({M} x {R}, l={ell or 1.0:.4g}, {kind})", g, M, kind=kind,
-                work_exact="agree" if name == "C4" else True)
+                work_exact="steps" if name == "C4" else True, envelope=name == "C4")
 
 
 @pytest.mark.parametrize("rule,rid,theta", [("POI", 1, 0.0), ("POI", 1, 0.05), ("LCB", 2, 2.0)])
