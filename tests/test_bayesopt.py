@@ -178,28 +178,37 @@ def test_myopic_loop_end_to_end(gpu, tmp_path):
         assert res[b]["ell_start"] == res[a]["ell_end"]
 
 
-@pytest.mark.gpu
-def test_bo_comparison_with_reference_runs(gpu):
-    """tools/bo_compare.py at 20 trials against the reference's recorded gap curves
-    (tests/golden/bo_ref_gaps.json), at the final budget label of each case: no evidence that the
-    build closes LESS of the gap than the reference's recorded runs (one-sided Mann–Whitney
-    p ≥ 0.05), for
-      rollout rows: the archived non-myopic runs, against the build-defined rollout solver
-        (mrbo/bayesopt.py rollout_solve, with its incumbent restart); it closes more of the gap than
-        the archived runs on Branin, so the test is one-sided, as for
-      myopic rows: multistart_base_solve! of analytic EI from 64 + 2 starts
-        (experiments/myopic_bayesopt.jl); on Hartmann-6 the build's projected Newton closes more of
-        it than the reference's recorded IPNewton runs (Optim.jl, absent and unpinned).
-    A test of NO DETECTED deficit at these sample sizes, not of equivalence; the 95 % interval of
-    the difference of mean gaps is recorded beside them (profiles/r03/bo_compare_*.jsonl)."""
+def _bo_compare():
     import sys
     from conftest import ROOT
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bo_compare as B
+    return B
+
+
+def test_bo_comparison_exceptions_are_the_measured_ones():
+    """The BO comparison asserts every recorded case but the four with a measured deficit, each
+    documented with its cause (six-hump POI tagged UNEXPLAINED)."""
+    B = _bo_compare()
+    assert set(B.EXCEPTIONS) == {"myopic_sixhump_poi", "myopic_sixhump_lcb", "myopic_hartmann6d_poi",
+                                 "rollout_h0_rosenbrock"}
+    assert B.EXCEPTIONS["myopic_sixhump_poi"].startswith("UNEXPLAINED")
+    assert set(B.ASSERTED) | set(B.EXCEPTIONS) == set(B.SETTINGS) and len(B.ASSERTED) == len(B.SETTINGS) - 4
     ref = B.load_reference()
-    rows = {}
-    for key in B.ASSERTED:
-        row = B.run_case(key, ref[key], 20, 1906, lambda m: None)
-        rows[key] = row["gaps"][B.SETTINGS[key]["labels"][-1]]
-    bad = {k: v for k, v in rows.items() if not v["mannwhitney_p_worse"] >= 0.05}
-    assert not bad, bad
+    assert set(B.SETTINGS) <= set(ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", _bo_compare().ASSERTED)
+def test_bo_case_with_reference_runs(gpu, key):
+    """tools/bo_compare.py at 20 trials, one recorded case of the reference (tests/golden/
+    bo_ref_gaps.json) at its final budget label: no evidence that the build closes LESS of the gap
+    than the reference's recorded runs (one-sided Mann–Whitney p ≥ 0.05).  Every case is asserted
+    except bo_compare.EXCEPTIONS (measured deficits with their causes)."""
+    B = _bo_compare()
+    ref = B.load_reference()
+    row = B.run_case(key, ref[key], 20, 1906, lambda m: None)
+    g = row["gaps"][B.SETTINGS[key]["labels"][-1]]
+    assert g["mannwhitney_p_worse"] >= 0.05, (key, g)
+
+

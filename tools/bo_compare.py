@@ -47,9 +47,24 @@ SETTINGS = {f"myopic_{fn}_{rule}": dict(fn=fn, rule=rule, horizon=0, budget=30, 
 SETTINGS.update({f"rollout_h{h}_{fn}": dict(fn=fn, rule="ei", horizon=h, budget=20, initial=1, starts=8, batch=8,
                                             labels=["5", "10", "20"])
                  for fn in ROLLOUT_FNS for h in (0, 1)})
-# the cases the GPU test asserts (tests/test_bayesopt.py): the round-2 set
-ASSERTED = ["myopic_braninhoo_ei", "myopic_hartmann6d_ei", "rollout_h0_braninhoo", "rollout_h1_braninhoo",
-            "rollout_h0_gramacylee", "rollout_h1_gramacylee"]
+# The cases with a MEASURED deficit against the reference's recorded runs, each
+# with what is known of its cause.  The GPU test (tests/test_bayesopt.py) asserts every other case.
+EXCEPTIONS = {
+    "myopic_sixhump_poi": "UNEXPLAINED: ours closes less (-0.08 at 30, 3 of 4 seeds); not the faces (3 % of "
+                          "observations, solve margins leave it), not repeats (no-repeat pick leaves it); what "
+                          "remains is which interior KKT point of POI the solver returns or the MLE lengthscale "
+                          "path -- IPNewton / Optim.jl, absent here (profiles/r05/bo_myopic/)",
+    "myopic_sixhump_lcb": "borderline: one-sided p = 0.04 at 60 trials, no two-sided difference "
+                          "(profiles/r04/bo_compare_myopic_all_reuse_60trials_r4e.jsonl); same solver question as POI",
+    "myopic_hartmann6d_poi": "the faces: projected Newton stops on a face where IPNewton's barrier keeps its iterate "
+                             "inside; the deficit shrinks with the solve margin (-0.091 -> -0.085 -> -0.034 at "
+                             "margins 0, 0.01, 0.05; profiles/r05/bo_myopic/)",
+    "rollout_h0_rosenbrock": "EI underflow regime: |fmini - mu| >> sigma on the whole batch of Rosenbrock's "
+                             "10^2-10^3 scale, EI = 0 and zero gradients; 90 % of trials repeat a point "
+                             "(DESIGN.md §10; profiles/r03/bo_trace/)",
+}
+# the cases the GPU test asserts: every recorded case without a measured deficit
+ASSERTED = [k for k in SETTINGS if k not in EXCEPTIONS]
 
 
 def load_reference(path=FIXTURE):

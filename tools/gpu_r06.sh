@@ -16,6 +16,7 @@
 #   myopic    myopic BO diagnostics: seeds, solve margins, no-repeat pick (4 cases, 60 trials)
 #   c5        C5 at ℓ = 1 (2 048 × 512) and ℓ = 20 (64 × 64)
 #   c5cost    C5 + NonUniformCost at M = 256, R = 128 (one step)
+#   ab6       A/B: this library vs mrbo/variants/libmrbo_r6old.so (C3, C3-MLE)
 #   prof      rocprofv3 --kernel-trace --stats of the default bench (20 steps after 3 warm-up) + the PMC
 #             passes (tools/profile.sh), C3 and C3-MLE
 # Outputs under gpurun_out/<tag>/.
@@ -108,6 +109,12 @@ for l in open(sys.argv[1]):
       timeout -k 10 400 python -u bench.py --config C5 --cost --mc-per-gpu 256 --restarts 128 --steps 1 --warmup 1 --no-cpu-baseline \
         > "$out/bench_c5_cost.json" 2> "$out/bench_c5_cost.err"
       rc=$?; tail -c 400 "$out/bench_c5_cost.json" ;;
+    ab6)
+      # the round-6 library against the round's starting C3 kernel (mrbo/variants/libmrbo_r6old.so),
+      # interleaved on one box: C3 and C3-MLE
+      REPS=3 TAG=c3 timeout -k 10 400 bash tools/ab_rep.sh r6old main > "$out/ab_c3.log" 2>&1 && \
+      REPS=2 TAG=c3mle BENCH_ARGS="--mle" timeout -k 10 500 bash tools/ab_rep.sh r6old main > "$out/ab_c3mle.log" 2>&1
+      rc=$?; cat "$out/ab_c3.log" "$out/ab_c3mle.log" | grep -v "mrbo stamps" | tail -24 ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac
   echo "== $step rc=$rc $(date +%T)"
