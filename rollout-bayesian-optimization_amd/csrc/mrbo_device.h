@@ -168,13 +168,15 @@ __device__ __forceinline__ double dcopy(double v) {
 // v_permlane16_swap (M = 16) / v_permlane32_swap (M = 32) of a double with itself, per dword:
 // first = [r0 r0 r2 r2] / [lo lo], second = [r1 r1 r3 r3] / [hi hi] (16-lane rows / 32-lane
 // halves).  KEEP: v stays live after the swap (two copies); else v itself is one operand.
-template <int M, bool KEEP>
+// COPY = false: the compiler's own copies (the L2-fed and GP-fit kernels at 512 registers, where
+// the explicit copies' fixed live ranges cost spills: C5 + cost scratch 352 → 896 B per lane).
+template <int M, bool KEEP, bool COPY = true>
 __device__ __forceinline__ void self_swap(double v, double& first, double& second) {
 #ifdef MRBO_NO_DCOPY
   const double c0 = v, c1 = v;
 #else
-  const double c0 = KEEP ? dcopy<0>(v) : v;
-  const double c1 = dcopy<1>(v);
+  const double c0 = (KEEP && COPY) ? dcopy<0>(v) : v;
+  const double c1 = COPY ? dcopy<1>(v) : v;
 #endif
   int al, ah, bl, bh;
   dsplit(c0, al, ah);
@@ -196,11 +198,25 @@ __device__ __forceinline__ void self_swap(double v, double& first, double& secon
 // M = 32 / 16: lanes with bit M clear get a(l) + a(l^M), lanes with it set get b(l^M) + b(l).
 // gfx950's v_permlane32_swap / v_permlane16_swap exchange exactly these cross halves of the
 // register pair in place: two swaps per double and one add -- no select, no LDS round trip.
+// A zero padding operand (a reduction slot past the values' count, known at compile time after
+// unrolling) is made by one v_mov_b64 instead of the compiler's two v_mov_b32: the swap overwrites
+// it, so it cannot stay an inline constant.
+__device__ __forceinline__ double swap_operand(double v) {
+#ifndef MRBO_NO_DCOPY
+  if (__builtin_constant_p(v) && v == 0.0) {
+    double z;
+    asm("v_mov_b64 %0, 0" : "=v"(z));
+    return z;
+  }
+#endif
+  return v;
+}
+
 template <int M>
 __device__ __forceinline__ double swap_fold(double a, double b) {
   int alo, ahi, blo, bhi;
-  dsplit(a, alo, ahi);
-  dsplit(b, blo, bhi);
+  dsplit(swap_operand(a), alo, ahi);
+  dsplit(swap_operand(b), blo, bhi);
   if constexpr (M == 32) {
     const auto lo = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
     const auto hi = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
@@ -216,20 +232,21 @@ __device__ __forceinline__ double swap_fold(double a, double b) {
 // Register broadcast (rollout products, GP-fit Cholesky): blocks p and p+2 of v (lane j holds
 // row j), each replicated into all four 16-lane rows, so that DPP row_newbcast:n then reads
 // row 16b + n in every lane.
-template <int P>
+template <int P, bool COPY = false>
 __device__ __forceinline__ void row_blocks(double v, double& blk_p, double& blk_p2) {
   double a0, a1;
-  self_swap<16, true>(v, a0, a1);                  // [r0 r0 r2 r2], [r1 r1 r3 r3]
-  self_swap<32, false>(P ? a1 : a0, blk_p, blk_p2); // [rP ×4], [rP+2 ×4]
+  self_swap<16, true, COPY>(v, a0, a1);                  // [r0 r0 r2 r2], [r1 r1 r3 r3]
+  self_swap<32, false, COPY>(P ? a1 : a0, blk_p, blk_p2); // [rP ×4], [rP+2 ×4]
 }
 
 // All four blocks at once: one v_permlane16_swap and two v_permlane32_swap per dword (blocks 0, 2
 // from the first pl16 half, 1, 3 from the second) instead of a pl16 + pl32 pair per block pair.
+template <bool COPY = false>
 __device__ __forceinline__ void row_blocks4(double v, double& b0, double& b1, double& b2, double& b3) {
   double a0, a1;
-  self_swap<16, true>(v, a0, a1);    // [r0 r0 r2 r2], [r1 r1 r3 r3]
-  self_swap<32, false>(a0, b0, b2);  // [r0 ×4], [r2 ×4]
-  self_swap<32, false>(a1, b1, b3);  // [r1 ×4], [r3 ×4]
+  self_swap<16, true, COPY>(v, a0, a1);    // [r0 r0 r2 r2], [r1 r1 r3 r3]
+  self_swap<32, false, COPY>(a0, b0, b2);  // [r0 ×4], [r2 ×4]
+  self_swap<32, false, COPY>(a1, b1, b3);  // [r1 ×4], [r3 ×4]
 }
 
 // The three broadcast operands of a folded product (bcast_fold_fwd / _bwd) in 3 swaps and 2 copies

@@ -201,6 +201,7 @@ struct WaveCtx {
   double* E;            // LDS (SQ) or global: FMAX × NR  inverse-factor fantasy rows (base columns)
   double* C;            // LDS (SQ) or global: (FMAX+1) × NR  base part of c for surfaces -1..h
   double* SUMS;         // packed layouts: global [64][8] per-start sums of the batched start pass
+  double* STASH;        // L2-fed layouts (GL): global [RPL][D][64] gradient columns of the last value pass
   double X0[RPL][D];    // own base rows
   bool valid[RPL];
   int N, Npad;
@@ -371,7 +372,9 @@ __device__ __forceinline__ void bcast_run(double (&acc)[K], const double (&bq)[K
   BcastAsm<K, STRIDE>::run(acc, bq, addr);
 }
 
-template <int K, int JSTRIDE, int HW = 1>
+// COPY: the row replication's operand copies as v_mov_b64 (self_swap); false for the 512-register
+// L2-fed kernels' LDS-resident blocks (gl_block), where they cost spills
+template <int K, int JSTRIDE, int HW = 1, bool COPY = true>
 __device__ __forceinline__ void bcast_product_k(double (&acc)[K], const double (&v)[K], const double* lbase, int nrows) {
   const unsigned a0 = lds_addr(lbase);
   if constexpr (HW == 2) {
@@ -398,21 +401,21 @@ __device__ __forceinline__ void bcast_product_k(double (&acc)[K], const double (
     double bp[K], bp2[K];
 #pragma unroll
     for (int c = 0; c < K; ++c) {
-      if (p == 0) row_blocks<0>(v[c], bp[c], bp2[c]);
-      else row_blocks<1>(v[c], bp[c], bp2[c]);
+      if (p == 0) row_blocks<0, COPY>(v[c], bp[c], bp2[c]);
+      else row_blocks<1, COPY>(v[c], bp[c], bp2[c]);
     }
     bcast_run<K, 8 * JSTRIDE>(acc, bp, a0 + 8u * 16u * p * JSTRIDE);
     if (16 * (p + 2) < nrows) bcast_run<K, 8 * JSTRIDE>(acc, bp2, a0 + 8u * 16u * (p + 2) * JSTRIDE);
   }
 }
 
-template <int K, int JSTRIDE, int HW = 1>
+template <int K, int JSTRIDE, int HW = 1, bool COPY = true>
 __device__ __forceinline__ void bcast_product(double (&acc)[K], const double (&v)[K], const double* lbase, int nrows) {
   if constexpr (K > 9) {
-    bcast_product<8, JSTRIDE, HW>(head8(acc), head8(v), lbase, nrows);
-    bcast_product<K - 8, JSTRIDE, HW>(tail8(acc), tail8(v), lbase, nrows);
+    bcast_product<8, JSTRIDE, HW, COPY>(head8(acc), head8(v), lbase, nrows);
+    bcast_product<K - 8, JSTRIDE, HW, COPY>(tail8(acc), tail8(v), lbase, nrows);
   } else {
-    bcast_product_k<K, JSTRIDE, HW>(acc, v, lbase, nrows);
+    bcast_product_k<K, JSTRIDE, HW, COPY>(acc, v, lbase, nrows);
   }
 }
 
@@ -456,7 +459,7 @@ __device__ __forceinline__ void bcast_fold_fwd_k(double (&acc)[K], const double 
   for (int c = 0; c < K; ++c) {
 #ifdef MRBO_FOLD_SELECT   // round-5 first form: all four blocks, then a per-row select
     double b2, b3;
-    row_blocks4(v[c], b0[c], b1[c], b2, b3);
+    row_blocks4<true>(v[c], b0[c], b1[c], b2, b3);
     m[c] = (q == 1) ? b3 : b2;
 #else
     fold_blocks(v[c], true, b0[c], b1[c], m[c]);
@@ -489,7 +492,7 @@ __device__ __forceinline__ void bcast_fold_bwd_k(double (&acc)[K], const double 
   for (int c = 0; c < K; ++c) {
 #ifdef MRBO_FOLD_SELECT
     double b0, b1;
-    row_blocks4(v[c], b0, b1, b2[c], b3[c]);
+    row_blocks4<true>(v[c], b0, b1, b2[c], b3[c]);
     m[c] = (q == 2) ? b0 : b1;
 #else
     fold_blocks(v[c], false, b2[c], b3[c], m[c]);
@@ -755,9 +758,9 @@ __device__ __forceinline__ void gl_block(double (&acc)[K], const double (&v)[K],
       if (fwd) bcast_fold_fwd<K>(acc, v, sq, lane);
       else bcast_fold_bwd<K>(acc, v, sq, lane);
     } else if (fwd) {
-      bcast_product<K, LD>(acc, v, sq + lane, nrows);
+      bcast_product<K, LD, 1, false>(acc, v, sq + lane, nrows);
     } else {
-      bcast_product<K, 1>(acc, v, sq + lane * LD, nrows);
+      bcast_product<K, 1, 1, false>(acc, v, sq + lane * LD, nrows);
     }
   } else {
     gl_bcast_product<K>(acc, v, Lg + (long long)b * WAVE * WAVE + lane, nrows);
@@ -994,7 +997,36 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
       }
     }
 #else
-    if (mode == EV_VALUE) {
+    // NonUniformCost (α/c has a gradient wherever c varies, so the certificates rarely stop a
+    // start and ≈ 54 % of C5 + cost's value passes are followed by a gradient pass at the same x):
+    // the value pass runs all D1 columns -- its L2-fed walk is bound by the L0⁻¹ stream, not by
+    // the FMAs, so 9 columns cost little more than 1 -- and stashes columns 1..d in the wave's
+    // global slot, where the GRADC pass that follows reads them instead of streaming L0⁻¹ again.
+    // Same blocks, same rows in the same order per column: bit-identical sums.  MRBO_NO_GL_EAGER:
+    // the lazy K = 1 value pass (A/B).
+#ifdef MRBO_NO_GL_EAGER
+    const bool eager = false;
+#else
+    const bool eager = kp.cost != COST_NONE;
+#endif
+    if (mode == EV_VALUE && eager) {
+#pragma unroll
+      for (int s = 0; s < RPL; ++s)
+#pragma unroll
+        for (int t = 0; t <= s; ++t)
+          gl_block<D1, Ly::LD, Ly::NLB>(acc[s], Bown[t], W.Linv, W.LinvL, Ly::blk(s, t), true, lane, nrows(t));
+#pragma unroll
+      for (int s = 0; s < RPL; ++s)
+#pragma unroll
+        for (int a = 0; a < D; ++a) W.STASH[(long long)(s * D + a) * WAVE + lane] = acc[s][1 + a];
+    } else if (mode == EV_GRADC && eager) {
+#pragma unroll
+      for (int s = 0; s < RPL; ++s) {
+#pragma unroll
+        for (int a = 0; a < D; ++a) acc[s][1 + a] = W.STASH[(long long)(s * D + a) * WAVE + lane];
+        acc[s][0] = W.G12[3 * (lane + WAVE * s) + 2];
+      }
+    } else if (mode == EV_VALUE) {
 #ifdef MRBO_K1_STREAM
       double v1[RPL], o1[RPL];
 #pragma unroll
@@ -2816,6 +2848,7 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL, HW>& W, const KParams
   else W.E = kp.work + slot * kp.work_stride;
   W.C = W.E + (long long)FMAX * Ly::NRL;
   W.SUMS = W.E + (long long)(2 * FMAX + 1) * Ly::NR;   // packed layouts only (work_stride covers it)
+  W.STASH = W.SUMS + 64 * 8;                           // GL layouts (work_stride covers it)
   W.N = kp.N;
   W.Npad = kp.Npad;
   W.rad.kind = kp.kernel;
