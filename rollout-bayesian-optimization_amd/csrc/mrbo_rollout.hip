@@ -40,6 +40,12 @@ inline namespace MRBO_FNS {
 
 constexpr double PAD_FAR = 1e100;   // coordinate of padded data rows (WaveCtx::rowv)
 
+#ifdef MRBO_NO_SQ_EAGER
+constexpr bool SQ_EAGER_ON = false;
+#else
+constexpr bool SQ_EAGER_ON = true;
+#endif
+
 template <int D, int RPL, int HW = 1>
 struct Lay {
   static constexpr int D1 = D + 1;
@@ -108,7 +114,11 @@ struct Lay {
   static constexpr int U_SIZE = ((U_KC + 15) + 1) & ~1;
   static constexpr int G12 = 3 * NRL;                    // per-lane [g1, g2, Y0] of the base rows
   static constexpr int EC = SQ ? (2 * FMAX + 1) * NRL : 0;  // E (FMAX×NRL) + C ((FMAX+1)×NRL) in LDS
-  static constexpr int WAVE_LDS = BROWS * BS + REDN + U_SIZE + G12 + EC;
+  // SQ_EAGER (the square layout of the FMAX = 4 units, full-wave): the value pass runs all D1
+  // columns of the forward product and stashes columns 1..d here for the GRADC pass that follows
+  static constexpr bool SQ_EAGER = SQ_EAGER_ON && SQ && HW == 1 && FMAX <= 4;
+  static constexpr int STASH = SQ_EAGER ? D * NRL : 0;
+  static constexpr int WAVE_LDS = BROWS * BS + REDN + U_SIZE + G12 + EC + STASH;
   // L0⁻¹ in LDS, shared by the waves of a workgroup.  BC: dense zero-padded 64×64 blocks,
   // column-major with odd leading dimension LD = 65, so the column walk (forward product,
   // lane i reads [i][j]) and the row walk (backward product, lane i reads [k][i]) are both
@@ -902,7 +912,21 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
 #else
     constexpr bool DFOLD = false;
 #endif
-    if (mode == EV_VALUE) {
+    if (Ly::SQ_EAGER && mode == EV_VALUE) {
+      // The K = 1 value product is bound by LDS reads (one ds_read_b64 per FMA, eight waves on
+      // one LDS); ≈ 95 % of C3's non-batched value passes are followed by a GRADC pass at the same
+      // x.  So the value pass runs all D1 columns (seven FMAs per read) and stashes columns 1..d
+      // in the wave's LDS, where the GRADC pass reads them instead of its K = d product.  Same
+      // fold, same steps per column: bit-identical sums.  MRBO_NO_SQ_EAGER: the lazy pass (A/B).
+      if (fold) bcast_fold_fwd<D1>(acc[0], Bown[0], W.Linv, lane);
+      else bcast_product<D1, Ly::LD, HW>(acc[0], Bown[0], W.Linv + lane, nrows(0));
+#pragma unroll
+      for (int a = 0; a < D; ++a) W.STASH[a * WAVE + lane] = acc[0][1 + a];
+    } else if (Ly::SQ_EAGER && mode == EV_GRADC) {
+#pragma unroll
+      for (int a = 0; a < D; ++a) acc[0][1 + a] = W.STASH[a * WAVE + lane];
+      acc[0][0] = W.G12[3 * lane + 2];
+    } else if (mode == EV_VALUE) {
 #pragma unroll
       for (int s = 0; s < RPL; ++s) {
         double a1[1] = {0.0};
@@ -2848,7 +2872,8 @@ __device__ __forceinline__ void wave_setup(WaveCtx<D, RPL, HW>& W, const KParams
   else W.E = kp.work + slot * kp.work_stride;
   W.C = W.E + (long long)FMAX * Ly::NRL;
   W.SUMS = W.E + (long long)(2 * FMAX + 1) * Ly::NR;   // packed layouts only (work_stride covers it)
-  W.STASH = W.SUMS + 64 * 8;                           // GL layouts (work_stride covers it)
+  if constexpr (Ly::SQ) W.STASH = W.G12 + Ly::G12 + Ly::EC;   // SQ_EAGER: wave LDS
+  else W.STASH = W.SUMS + 64 * 8;                              // GL layouts (work_stride covers it)
   W.N = kp.N;
   W.Npad = kp.Npad;
   W.rad.kind = kp.kernel;

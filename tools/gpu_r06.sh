@@ -17,6 +17,7 @@
 #   c5        C5 at ℓ = 1 (2 048 × 512) and ℓ = 20 (64 × 64)
 #   c5cost    C5 + NonUniformCost at M = 256, R = 128 (one step)
 #   ab6       A/B: this library vs mrbo/variants/libmrbo_r6old.so (C3, C3-MLE)
+#   ab6c5     the same for C5 + NonUniformCost (256 × 128)
 #   prof      rocprofv3 --kernel-trace --stats of the default bench (20 steps after 3 warm-up) + the PMC
 #             passes (tools/profile.sh), C3 and C3-MLE
 # Outputs under gpurun_out/<tag>/.
@@ -115,6 +116,11 @@ for l in open(sys.argv[1]):
       REPS=3 TAG=c3 timeout -k 10 400 bash tools/ab_rep.sh r6old main > "$out/ab_c3.log" 2>&1 && \
       REPS=2 TAG=c3mle BENCH_ARGS="--mle" timeout -k 10 500 bash tools/ab_rep.sh r6old main > "$out/ab_c3mle.log" 2>&1
       rc=$?; cat "$out/ab_c3.log" "$out/ab_c3mle.log" | grep -v "mrbo stamps" | tail -24 ;;
+    ab6c5)
+      # C5 + NonUniformCost (the bench row's shape, 256 × 128 per launch): this library vs r6old
+      REPS=2 STEPS=1 TAG=c5cost BENCH_ARGS="--config C5 --cost --mc-per-gpu 256 --restarts 128" \
+        timeout -k 10 600 bash tools/ab_rep.sh r6old main > "$out/ab_c5cost.log" 2>&1
+      rc=$?; grep -v "mrbo stamps" "$out/ab_c5cost.log" | tail -8 ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac
   echo "== $step rc=$rc $(date +%T)"
