@@ -741,7 +741,8 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   const int slots = std::max(P->blocks * P->wpg, P->eblocks * P->ewpg);
   // per wave slot: E (FMAX × NR) and C ((FMAX+1) × NR), then the batched start pass's per-start
   // sums (64 × 8) for the packed layouts
-  // and, for the L2-fed layouts, the value pass's stashed gradient columns (RPL × d × 64)
+  // and, for the L2-fed layouts, room for the value pass's stashed gradient columns (RPL × d × 64,
+  // MRBO_GL_EAGER builds)
   P->work_stride = (long long)(2 * FMAX + 1) * P->NR + 64 * 8 + (ks.gl ? (long long)P->NR * d : 0);
   bool ok = hipMalloc(&P->dX0, sizeof(double) * X0.size()) == hipSuccess &&
             hipMalloc(&P->dc0, sizeof(double) * c0.size()) == hipSuccess &&

@@ -1021,17 +1021,16 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
       }
     }
 #else
-    // NonUniformCost (α/c has a gradient wherever c varies, so the certificates rarely stop a
-    // start and ≈ 54 % of C5 + cost's value passes are followed by a gradient pass at the same x):
-    // the value pass runs all D1 columns -- its L2-fed walk is bound by the L0⁻¹ stream, not by
-    // the FMAs, so 9 columns cost little more than 1 -- and stashes columns 1..d in the wave's
-    // global slot, where the GRADC pass that follows reads them instead of streaming L0⁻¹ again.
-    // Same blocks, same rows in the same order per column: bit-identical sums.  MRBO_NO_GL_EAGER:
-    // the lazy K = 1 value pass (A/B).
-#ifdef MRBO_NO_GL_EAGER
-    const bool eager = false;
-#else
+    // MRBO_GL_EAGER (A/B, not the default): with NonUniformCost ≈ 54 % of C5 + cost's value
+    // passes are followed by a gradient pass at the same x, so the value pass could run all D1
+    // columns and stash columns 1..d in the wave's global slot for that GRADC pass (same blocks,
+    // same rows in the same order per column: bit-identical sums).  Measured (round 6, C5 + cost
+    // 256 × 128, same box): 1 278 → 1 386 ms, +8.5 % -- at one wave per SIMD the nine-column
+    // walk costs far more than the L0⁻¹ stream it saves.
+#ifdef MRBO_GL_EAGER
     const bool eager = kp.cost != COST_NONE;
+#else
+    const bool eager = false;
 #endif
     if (mode == EV_VALUE && eager) {
 #pragma unroll

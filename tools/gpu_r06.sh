@@ -113,13 +113,13 @@ for l in open(sys.argv[1]):
     ab6)
       # the round-6 library against the round's starting C3 kernel (mrbo/variants/libmrbo_r6old.so),
       # interleaved on one box: C3 and C3-MLE
-      REPS=3 TAG=c3 timeout -k 10 400 bash tools/ab_rep.sh r6old main > "$out/ab_c3.log" 2>&1 && \
-      REPS=2 TAG=c3mle BENCH_ARGS="--mle" timeout -k 10 500 bash tools/ab_rep.sh r6old main > "$out/ab_c3mle.log" 2>&1
+      REPS=3 TAG=c3 timeout -k 10 400 bash tools/ab_rep.sh r6old ${AB6_VARIANTS:-} main > "$out/ab_c3.log" 2>&1 && \
+      REPS=2 TAG=c3mle BENCH_ARGS="--mle" timeout -k 10 500 bash tools/ab_rep.sh r6old ${AB6_VARIANTS:-} main > "$out/ab_c3mle.log" 2>&1
       rc=$?; cat "$out/ab_c3.log" "$out/ab_c3mle.log" | grep -v "mrbo stamps" | tail -24 ;;
     ab6c5)
       # C5 + NonUniformCost (the bench row's shape, 256 × 128 per launch): this library vs r6old
       REPS=2 STEPS=1 TAG=c5cost BENCH_ARGS="--config C5 --cost --mc-per-gpu 256 --restarts 128" \
-        timeout -k 10 600 bash tools/ab_rep.sh r6old main > "$out/ab_c5cost.log" 2>&1
+        timeout -k 10 600 bash tools/ab_rep.sh ${AB6C5_VARIANTS:-r6old main} > "$out/ab_c5cost.log" 2>&1
       rc=$?; grep -v "mrbo stamps" "$out/ab_c5cost.log" | tail -8 ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac
