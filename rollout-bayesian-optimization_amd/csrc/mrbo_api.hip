@@ -65,6 +65,7 @@ struct mrbo_plan {
   long long work_stride = 0;
   int* dqueue = nullptr;    // work-queue heads: one per XCD, 64 B apart (rollout_kernel)
   const int32_t* order = nullptr;   // mrbo_plan_set_order: caller-owned device permutation of M×R
+  const int32_t* skip_active = nullptr;   // set by mrbo_stochastic_solve for its launches only
   int wpg = 4, blocks = 0;
   size_t smem = 0;
   int spec = 0;             // 1: rollout_kernel<D, RPL, 1> (Matérn-5/2 + EI fixed); 2: its half-wave form <D, 1, 1, 2>;
@@ -841,6 +842,7 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
   kp.values = dvalues; kp.grad_x = with_grad ? dgx : nullptr; kp.grad_theta = with_grad ? dgt : nullptr;
   kp.status = (int*)dstatus; kp.policy = dpol; kp.obs = dobs; kp.evals = (long long*)devals;
   kp.order = P->order;
+  kp.skip_active = P->skip_active;
   HIP_TRY(hipMemsetAsync(P->dqueue, 0, sizeof(int) * MRBO_QUEUE_INTS, st));
 #ifdef MRBO_STAMPS
   static unsigned long long* dstamps = nullptr;
@@ -1066,6 +1068,13 @@ int mrbo_stochastic_solve(mrbo_plan_t* P, double* x0s, const double* rnstream, c
     if (P->hchk[2 * k + 1] == 0 && !stopped_at) stopped_at = j;
     return 0;
   };
+  // A restart that eswavs has stopped keeps its x0, so its trajectories would reproduce the
+  // outputs of its last launch bit for bit: the later launches skip them (kp.skip_active)
+  struct SkipGuard {
+    mrbo_plan_t* P;
+    ~SkipGuard() { P->skip_active = nullptr; }
+  } guard{P};
+  P->skip_active = dact;
   int rc = MRBO_OK;
   while (it < o->iterations && !stopped_at && !bits) {
     ++it;

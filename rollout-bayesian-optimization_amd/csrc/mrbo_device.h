@@ -112,6 +112,9 @@ struct KParams {
   const double* ghq_w;
   int* queue;           // work-queue heads, one per XCD at queue[16·x] (zeroed before every launch)
   const int* order;     // optional: queue position -> trajectory (mrbo_plan_set_order), else identity
+  const int* skip_active;  // mrbo_stochastic_solve: a restart r with skip_active[r] == 0 has stopped
+                           // (eswavs); its trajectories are not re-run (x0 unchanged: the outputs
+                           // the previous launch left are the ones they would reproduce).  Else null
   long long T;          // trajectories (or points for eval_base)
   const double* pts;    // eval_base: d×P
   double* pts_out;      // eval_base output

@@ -3011,6 +3011,7 @@ __global__ void __launch_bounds__((KBounds<D, RPL, HW>::threads), (KBounds<D, RP
       const long long id = kp.order[tr];
       tr = (id >= 0 && id < kp.T) ? id : tr;
     }
+    if (kp.skip_active && kp.skip_active[tr / kp.M] == 0) continue;   // a stopped restart (outer ascent)
     trajectory<D, RPL, HW>(W, kp, tr);
   }
 #ifdef MRBO_STAMPS

@@ -59,7 +59,7 @@ for step in "$@"; do
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1].split('/')[-1], d['value'], d['ms_per_step'], d['roofline']['kernel_ms'])" "$f"
       done ;;
     prof)
-      bash tools/profile.sh "${tag}_c3" --steps 20 --warmup 3 --no-cpu-baseline && bash tools/profile.sh "${tag}_c3mle" --steps 5 --warmup 2 --no-cpu-baseline --mle
+      bash tools/profile.sh "${tag}_c3" --steps 40 --warmup 5 --no-cpu-baseline && bash tools/profile.sh "${tag}_c3mle" --steps 5 --warmup 2 --no-cpu-baseline --mle
       rc=$? ;;
     ab)
       AB_TAG="" timeout -k 10 400 bash tools/ab_run.sh ${AB_VARIANTS:-old new oldst newst} > "$out/ab.log" 2>&1
