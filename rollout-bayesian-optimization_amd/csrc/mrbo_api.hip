@@ -665,6 +665,11 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
     delete P;
     return fail(MRBO_ERR_UNSUPPORTED, "d=%d (rows per lane %d) not compiled into this library", d, P->RPL);
   }
+  if (ks.kparams_bytes != sizeof(KParams)) {
+    delete P;
+    return fail(MRBO_ERR_UNSUPPORTED, "kernel unit d=%d (FMAX %d) was compiled against another KParams layout "
+                "(%zu vs %zu bytes): rebuild the library", d, P->fx ? 4 : 6, ks.kparams_bytes, sizeof(KParams));
+  }
   // the kernel's image of L0⁻¹ (zero above the diagonal and on padded rows); the global
   // variant appends a row-packed copy (row k: columns 0..k) for the backward product
   std::vector<double> packed((size_t)ks.linv_dev, 0.0);

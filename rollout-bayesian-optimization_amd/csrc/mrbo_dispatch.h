@@ -26,6 +26,9 @@ struct KernelSet {
   size_t wave_bytes_half = 0;
   // Matérn-5/2 + EI + quadratic NonUniformCost at compile time (rollout_kernel<D, RPL, 2>), or null
   const void* rollout_cost = nullptr;
+  // sizeof(KParams) in the unit that filled this set: the host API refuses a unit compiled against
+  // another KParams layout (a stale object would read every launch parameter at a shifted offset)
+  size_t kparams_bytes = 0;
 };
 
 // The host API sees every unit's entry points as weak references (MRBO_API_TU): a library

@@ -77,6 +77,7 @@ static KernelSet kset() {
 #if MRBO_HAS_COST
   if constexpr (has_cost(D, RPL)) ks.rollout_cost = (const void*)&rollout_kernel<D, RPL, 2>;
 #endif
+  ks.kparams_bytes = sizeof(KParams);
   return ks;
 }
 
