@@ -361,3 +361,21 @@ def test_bench_kernel_label_names_the_profiled_kernel():
     import csv
     rows = list(csv.DictReader(open(os.path.join(ROOT, "profiles", "r05", "kernel_stats_c3_r5l.csv"))))
     assert any(bench.kernel_label(6, dict(rpl=1, spec=1, fmax=4)) in r["Name"] for r in rows)
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc needed")
+def test_every_kernel_unit_matches_the_kparams_layout(tmp_path):
+    """Each kernel unit's KernelSet carries sizeof(KParams) from its own compile; mrbo_plan_create
+    refuses a mismatch at run time (a unit left stale by an edit during a long build once read every
+    launch parameter at a shifted offset).  This checks every unit of the built library on the CPU."""
+    import subprocess
+    src = os.path.join(ROOT, "tests", "kparams_layout_check.cpp")
+    csrc = os.path.join(ROOT, "rollout-bayesian-optimization_amd", "csrc")
+    libdir = os.path.join(ROOT, "rollout-bayesian-optimization_amd", "mrbo")
+    obj, exe = str(tmp_path / "k.o"), str(tmp_path / "k")
+    hipcc = "/opt/rocm/bin/hipcc"
+    subprocess.check_call([hipcc, "--offload-arch=gfx950", "-std=c++17", f"-I{csrc}", "-c", src, "-o", obj])
+    subprocess.check_call([hipcc, "--offload-arch=gfx950", obj, "-o", exe, f"-L{libdir}", "-l:libmrbo.so",
+                           f"-Wl,-rpath,{libdir}"])
+    out = subprocess.run([exe], capture_output=True, text=True)
+    assert out.returncode == 0 and " 0 mismatched" in out.stdout, out.stdout + out.stderr
