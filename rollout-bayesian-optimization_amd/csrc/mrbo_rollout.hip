@@ -40,10 +40,15 @@ inline namespace MRBO_FNS {
 
 constexpr double PAD_FAR = 1e100;   // coordinate of padded data rows (WaveCtx::rowv)
 
-#ifdef MRBO_NO_SQ_EAGER
-constexpr bool SQ_EAGER_ON = false;
-#else
+// MRBO_SQ_EAGER (A/B, not the default): the eager all-column value pass of the square layout
+// (Lay::SQ_EAGER).  Measured neutral (C3 −0.3 %, C3-MLE +0.2 %, within the spread) while it issues
+// 4 % more VALU per wave: about half of C3's non-batched value passes are NOT followed by a GRADC
+// pass (the iteration converges on x_tol / f_tol after an accepted trial), and their extra columns
+// are wasted work.
+#ifdef MRBO_SQ_EAGER
 constexpr bool SQ_EAGER_ON = true;
+#else
+constexpr bool SQ_EAGER_ON = false;
 #endif
 
 template <int D, int RPL, int HW = 1>
@@ -917,7 +922,7 @@ __device__ __forceinline__ int evaluate(WaveCtx<D, RPL, HW>& W, const KParams& k
       // one LDS); ≈ 95 % of C3's non-batched value passes are followed by a GRADC pass at the same
       // x.  So the value pass runs all D1 columns (seven FMAs per read) and stashes columns 1..d
       // in the wave's LDS, where the GRADC pass reads them instead of its K = d product.  Same
-      // fold, same steps per column: bit-identical sums.  MRBO_NO_SQ_EAGER: the lazy pass (A/B).
+      // fold, same steps per column: bit-identical sums.  Off by default (SQ_EAGER_ON above).
       if (fold) bcast_fold_fwd<D1>(acc[0], Bown[0], W.Linv, lane);
       else bcast_product<D1, Ly::LD, HW>(acc[0], Bown[0], W.Linv + lane, nrows(0));
 #pragma unroll
