@@ -855,6 +855,18 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
   HIP_TRY(hipMemsetAsync(dstamps, 0, sizeof(unsigned long long) * NSTAMP_SLOTS, st));
   kp.stamps = dstamps;
 #endif
+#ifdef MRBO_TAIL   // per-wave (start, end, trajectories) of the rollout launch: the tail of the persistent grid
+  static unsigned long long* dtail = nullptr;
+  static int ntail = 0;
+  const int nwaves = P->blocks * P->wpg;
+  if (nwaves > ntail) {
+    if (dtail) HIP_TRY(hipFree(dtail));
+    HIP_TRY(hipMalloc(&dtail, sizeof(unsigned long long) * 3 * nwaves));
+    ntail = nwaves;
+  }
+  HIP_TRY(hipMemsetAsync(dtail, 0, sizeof(unsigned long long) * 3 * nwaves, st));
+  kp.stamps = dtail;
+#endif
   kp.xs_lds = P->xs_lds;
   kp.batch = P->batch;
   if (P->batch && P->RPL > 1) {   // packed layouts: global start tables for this launch's xstarts
@@ -877,6 +889,40 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(P->ev[2 * slot + 1], st));
   ++P->nlaunch;
+#ifdef MRBO_TAIL
+  {
+    std::vector<unsigned long long> h(3 * (size_t)nwaves);
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipMemcpy(h.data(), dtail, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+    unsigned long long t0 = ~0ull, t1 = 0;
+    long long ntr = 0;
+    int nmin = 1 << 30, nmax = 0, nw = 0;
+    for (int w = 0; w < nwaves; ++w) {
+      if (!h[3 * w + 1]) continue;
+      ++nw;
+      t0 = std::min(t0, h[3 * w]);
+      t1 = std::max(t1, h[3 * w + 1]);
+      ntr += (long long)h[3 * w + 2];
+      nmin = std::min(nmin, (int)h[3 * w + 2]);
+      nmax = std::max(nmax, (int)h[3 * w + 2]);
+    }
+    std::vector<double> ends;
+    double busy = 0, headv = 0;
+    for (int w = 0; w < nwaves; ++w) {
+      if (!h[3 * w + 1]) continue;
+      ends.push_back((double)(h[3 * w + 1] - t0));
+      busy += (double)(h[3 * w + 1] - h[3 * w]);
+      headv += (double)(h[3 * w] - t0);
+    }
+    std::sort(ends.begin(), ends.end());
+    const double span = (double)(t1 - t0);
+    auto pct = [&](double q) { return ends[std::min(ends.size() - 1, (size_t)(q * ends.size()))] / span; };
+    fprintf(stderr, "[mrbo tail] waves %d span %.1f us  busy %.4f  start skew %.4f  idle tail %.4f  "
+            "ends p0 %.4f p10 %.4f p50 %.4f p90 %.4f  traj/wave %d..%d  us/traj/wave %.2f\n",
+            nw, span / 100.0, busy / (nw * span), headv / (nw * span), 1.0 - (busy + headv) / (nw * span),
+            pct(0.0), pct(0.1), pct(0.5), pct(0.9), nmin, nmax, busy / 100.0 / (double)std::max(ntr, 1ll));
+  }
+#endif
 #ifdef MRBO_STAMPS
   {
     // region names follow the STAMP(W, k) sites in mrbo_rollout.hip

@@ -2983,6 +2983,10 @@ __global__ void __launch_bounds__((KBounds<D, RPL, HW>::threads), (KBounds<D, RP
 #ifdef MRBO_STAMPS
   W.tlast = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef MRBO_TAIL   // per-wave start / end (100 MHz REFCLK, one clock for all XCDs) and trajectory count
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  int n_taken = 0;
+#endif
 #ifndef MRBO_QUEUE_SINGLE
   // One queue per XCD over a contiguous eighth of the trajectories (chunk x = [x·T/8, (x+1)·T/8),
   // its head at kp.queue[16·x], one 64-B line each): the waves of an XCD first drain the chunk of
@@ -3018,7 +3022,19 @@ __global__ void __launch_bounds__((KBounds<D, RPL, HW>::threads), (KBounds<D, RP
     }
     if (kp.skip_active && kp.skip_active[tr / kp.M] == 0) continue;   // a stopped restart (outer ascent)
     trajectory<D, RPL, HW>(W, kp, tr);
+#ifdef MRBO_TAIL
+    ++n_taken;
+#endif
   }
+#ifdef MRBO_TAIL
+  if (kp.stamps && W.lane == 0 && W.half == 0) {
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+    const long long g = (long long)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+    kp.stamps[3 * g] = t_start;
+    kp.stamps[3 * g + 1] = t_end;
+    kp.stamps[3 * g + 2] = (unsigned long long)n_taken;
+  }
+#endif
 #ifdef MRBO_STAMPS
   if (kp.stamps && W.lane == 0)
     for (int k = 0; k < NSTAMP_SLOTS; ++k)

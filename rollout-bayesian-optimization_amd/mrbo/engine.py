@@ -252,11 +252,21 @@ class RolloutPlan:
         """Schedule the next launches longest-first by the per-trajectory work counters of the
         launch that filled `out` (on the device, no host round trip).  Consecutive SGA steps move
         x0 a little and reuse the MC streams, so a trajectory's work repeats closely and the
-        longest ones no longer start last (the launch's tail)."""
+        longest ones no longer start last (the launch's tail).
+
+        The kernel's waves drain one queue per XCD over a contiguous eighth of the queue positions
+        first (mrbo_rollout.hip rollout_kernel), so the ranking is dealt round-robin over the eight
+        chunks: the r-th longest trajectory goes to position r // 8 of chunk r % 8.  Every chunk is
+        then longest-first and carries an eighth of the work; a plain global sort would hand XCD 0
+        the longest eighth and leave the shortest ones of chunk 0 for the end of the launch."""
         torch = _torch()
         ev = out["evals"].view(-1, _lib.NCOUNTERS).to(torch.float64)
         w = torch.tensor(self.ORDER_WEIGHTS, dtype=torch.float64, device=ev.device)
-        self.set_order(torch.argsort(ev @ w, descending=True).to(torch.int32))
+        ranks = torch.argsort(ev @ w, descending=True)
+        pos = xcd_round_robin(ranks.numel(), ranks.device)
+        order = torch.empty_like(ranks)
+        order[pos] = ranks
+        self.set_order(order.to(torch.int32))
 
     def info(self):
         """Launch geometry: rows per lane, workgroups, waves per workgroup, batched start values,
@@ -265,6 +275,22 @@ class RolloutPlan:
         _lib.check(self.lib.mrbo_plan_info(self.handle, v, 7))
         keys = ("rpl", "blocks", "waves_per_group", "batch", "spec", "lds_bytes", "fmax")
         return dict(zip(keys, (int(x) for x in v)))
+
+
+XCD_QUEUES = 8   # work-queue heads of the rollout kernel (MRBO_QUEUE_INTS / 16)
+
+
+def xcd_round_robin(T, device=None):
+    """Queue positions 0..T-1 in the order (position within its chunk, chunk), for the kernel's
+    per-XCD chunks [x·T/8, (x+1)·T/8) (integer division, as rollout_kernel computes them): entry r
+    is the position that the r-th item of a ranking takes when the ranking is dealt round-robin
+    over the chunks.  Pure index arithmetic (CPU-testable): no GPU needed."""
+    import torch
+    p = torch.arange(T, dtype=torch.int64, device=device)
+    lo = torch.tensor([x * T // XCD_QUEUES for x in range(XCD_QUEUES)], dtype=torch.int64, device=device)
+    chunk = torch.bucketize(p, lo[1:], right=True)
+    key = (p - lo[chunk]) * XCD_QUEUES + chunk
+    return torch.argsort(key)
 
 
 def rnstream(M, d, H):
