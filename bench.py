@@ -66,11 +66,14 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--schedule", choices=("auto", "index", "longest-first"), default="auto",
                     help="order in which the persistent waves take the trajectories: index order, or "
-                         "longest first by the first step's work counters; auto (default) = longest first "
-                         "when the launch is at most two rounds of the resident waves deep, index order "
-                         "otherwise (C2: kernel 0.544 -> 0.518 ms, 7.34 -> 7.71 M traj/s; at C3's 32 rounds "
-                         "longest first measured 1 %% slower, so C3 stays in index order; DESIGN.md §9)")
+                         "longest first by the first step's work counters, dealt round-robin over the "
+                         "kernel's eight per-XCD queue chunks (mrbo.engine.xcd_round_robin); auto (default) "
+                         "= longest first (C3: idle tail of the persistent grid 7.0 -> 1.2 %%, kernel "
+                         "9.28 -> 8.75 ms; C3-MLE 46.1 -> 45.0 ms; DESIGN.md §2)")
     ap.add_argument("--longest-first", action="store_true", help="same as --schedule longest-first")
+    ap.add_argument("--resort", type=int, default=0,
+                    help="longest-first schedule: re-rank from every K-th step's work counters "
+                         "(0, default: from the first step's only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--solver", choices=("sga", "adam"), default="sga",
                     help="outer update!: StandardSGA (default) or Adam (optimizers.jl:25-74), both on the device")
@@ -245,8 +248,7 @@ def main():
     plan = _plan_for(T.s, h, hi - lo, R, pb.es.get_starts().shape[1], pb.lbs, pb.ubs, T.θ[0], local,
                      dict(sample_offset=lo, samples_total=M_total, **pb.plan_opts()))
     geo = plan.info()   # resident persistent waves: workgroups x waves per workgroup
-    longest_first = args.longest_first or args.schedule == "longest-first" or (
-        args.schedule == "auto" and (hi - lo) * R <= 2 * geo["blocks"] * geo["waves_per_group"])
+    longest_first = args.longest_first or args.schedule in ("auto", "longest-first")
     dev = f"cuda:{local}"
     drn = to_device(np.asfortranarray(pb.tp.rnstream_sequence[lo:hi]), dev)   # resident in HBM
     dxs = to_device(pb.es.get_starts(), dev)
@@ -271,10 +273,12 @@ def main():
             # the device (mrbo_merge_moments): the same host profile as the one-GPU step
             e = parallel.sharded_eto_device(plan, plan.partial_moments(out, hi - lo), shard_sizes)
         evals_acc.add_(out["evals"])        # also in warmup: no first-use op inside the timed region
-        if longest_first and "ordered" not in last:
+        last["n"] = last.get("n", 0) + 1
+        if longest_first and ("ordered" not in last or (args.resort and last["n"] % args.resort == 0)):
             # the schedule of every later step, from this (first) step's work counters: an SGA step
-            # moves x0 a little and the MC streams repeat, so a trajectory's work repeats closely;
-            # re-sorting every step costs more (≈ 0.09 ms at C2) than it gains
+            # moves x0 a little and the MC streams repeat, so a trajectory's work repeats closely
+            # (--resort K: again from every K-th step's counters).  On the device, no host sync
+            # (mrbo_plan_order_longest_first)
             plan.order_longest_first(out)
             last["ordered"] = True
         # eswavs + update! of every active restart on the device (mrbo_sga_step / mrbo_adam_step):
@@ -354,7 +358,7 @@ def main():
                                   if args.solver == "sga" else
                                   f"eswavs + Adam η={eta:g} β=(0.9, 0.999) ε=1e-8 (utils.jl:114-123, "
                                   f"optimizers.jl:49-74)"),
-                   "schedule": "longest first (first step's work counters)" if longest_first else "index order"},
+                   "schedule": "longest first (first step's work counters, round-robin over the per-XCD queue chunks)" if longest_first else "index order"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": kernel_label(d, info), "kernel_ms": kms, "flops_per_launch": fl,

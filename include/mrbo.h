@@ -331,6 +331,19 @@ int mrbo_plan_info(const mrbo_plan_t* plan, int32_t* info, int32_t n);
  * runs -- its outputs are left undefined.  The Python mirror (RolloutPlan.set_order) checks. */
 int mrbo_plan_set_order(mrbo_plan_t* plan, const int32_t* order, int64_t n);
 
+/* The same, with the order computed on the device by the library (no reference counterpart;
+ * scheduling only): `evals` is a DEVICE array of M×R×5 work counters as a previous
+ * mrbo_simulate_mc on this plan wrote them.  The trajectories are ranked by their weighted work
+ * (grad 2.5, value 1, Hessian 3, adjoint rich evaluation 5, adjoint pair 3, in value-evaluation
+ * units; a stable descending radix sort), and the ranking is dealt round-robin over the rollout
+ * kernel's eight per-XCD queue chunks, so that each chunk is longest first and carries an eighth
+ * of the work.  The plan owns the order (grown on demand, freed with the plan); it is used by the
+ * plan's later launches until mrbo_plan_set_order replaces it (NULL: identity).  Stream-ordered:
+ * no host round trip.  `order_out` (DEVICE, M×R int32, or NULL) receives a copy of the order.
+ * mrbo_stochastic_solve does this after its first launch when the caller has set no order.
+ * M×R ≥ 2^31: MRBO_ERR_ARG.                                                                    */
+int mrbo_plan_order_longest_first(mrbo_plan_t* plan, const int64_t* evals, int32_t* order_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

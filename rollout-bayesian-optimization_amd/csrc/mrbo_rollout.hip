@@ -1718,18 +1718,20 @@ __device__ __forceinline__ bool newton_pg_ok(WaveCtx<D, RPL, HW>& W, const KPara
 // shifted matrix; the shift is formed by every lane from A0 alone), and p comes from lane 0 when
 // A0 factored, else from lane 32: the same values as the sequential retry, in the time of one
 // factorisation (the retry is taken at ~80-90 % of C3's directions).
-template <int D, int RPL, int HW>
-__device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL, HW>& W, const KParams& kp) {
+// ALL_FREE: every coordinate is free (the common interior case; a wave-uniform branch in
+// newton_direction): the masks below are compile-time true and their selects fold away -- the
+// same values as the masked form, whose selects then pick the unmasked operand.
+template <int D, int RPL, int HW, bool ALL_FREE>
+__device__ __forceinline__ bool newton_direction_fm(WaveCtx<D, RPL, HW>& W, const KParams& kp, int fm) {
   using Ly = Lay<D, RPL, HW>;
   constexpr int NH = D * (D + 1) / 2;
   double* U = W.U;
   const int lane = W.ln();
-  const int fm = (int)U[Ly::U_SC + SC_FREE];
   bool fr[D];
   double gs[D];
 #pragma unroll
   for (int a = 0; a < D; ++a) {
-    fr[a] = (fm >> a) & 1;
+    fr[a] = ALL_FREE || ((fm >> a) & 1);
     gs[a] = U[Ly::U_NG + a];
   }
   // masked reduced Hessian of f = -α, packed lower; H read unconditionally (a load under a
@@ -1811,6 +1813,19 @@ __device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL, HW>& W, const K
   wave_sync();
   STAMP(W, 18);
   return true;
+}
+
+template <int D, int RPL, int HW>
+__device__ __forceinline__ bool newton_direction(WaveCtx<D, RPL, HW>& W, const KParams& kp) {
+  using Ly = Lay<D, RPL, HW>;
+  // the free set of this lane's trajectory (U is per trajectory: in half-wave mode the two halves
+  // hold different sets, so the mask stays per lane there); written by the trajectory's lane 0
+  int fm = (int)W.U[Ly::U_SC + SC_FREE];
+  if constexpr (HW == 1) fm = __builtin_amdgcn_readfirstlane(fm);
+#ifndef MRBO_NO_ALLFREE
+  if (__builtin_amdgcn_ballot_w64(fm != (1 << D) - 1) == 0ull) return newton_direction_fm<D, RPL, HW, true>(W, kp, fm);
+#endif
+  return newton_direction_fm<D, RPL, HW, false>(W, kp, fm);
 }
 
 // x_t = clamp(x + t p) -> U_X ; returns gᵀ(x_t - x).  Lane a < D computes coordinate a (its own

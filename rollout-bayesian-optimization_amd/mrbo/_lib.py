@@ -36,6 +36,7 @@ EXPORTS = [
     "mrbo_initial_guesses", "mrbo_dual_uniform", "mrbo_last_kernel_ms", "mrbo_gp_fit", "mrbo_gp_fit_theta",
     "mrbo_plan_info", "mrbo_last_gp_fit_ms", "mrbo_plan_set_order", "mrbo_base_solve", "mrbo_sga_step",
     "mrbo_kernel_times", "mrbo_merge_moments", "mrbo_adam_step", "mrbo_stochastic_solve",
+    "mrbo_plan_order_longest_first",
 ]
 
 MRBO_OPT_SGA, MRBO_OPT_ADAM = 0, 1
@@ -118,6 +119,7 @@ def load():
     L.mrbo_merge_moments.argtypes = [_vp, ctypes.c_int32, _vp, ctypes.POINTER(ctypes.c_int64), _vp, ctypes.c_uint32,
                                      _vp]
     L.mrbo_plan_set_order.argtypes = [_vp, _vp, ctypes.c_int64]
+    L.mrbo_plan_order_longest_first.argtypes = [_vp, _vp, _vp, _vp]
     L.mrbo_last_gp_fit_ms.restype = ctypes.c_double
     _lib = L
     return L

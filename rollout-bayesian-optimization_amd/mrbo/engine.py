@@ -248,25 +248,38 @@ class RolloutPlan:
         _lib.check(self.lib.mrbo_plan_set_order(self.handle, ctypes.c_void_p(self._order.data_ptr()),
                                                 self._order.numel()))
 
-    def order_longest_first(self, out):
+    def order_longest_first(self, out, stream=None, order_out=None):
         """Schedule the next launches longest-first by the per-trajectory work counters of the
-        launch that filled `out` (on the device, no host round trip).  Consecutive SGA steps move
-        x0 a little and reuse the MC streams, so a trajectory's work repeats closely and the
-        longest ones no longer start last (the launch's tail).
+        launch that filled `out`: mrbo_plan_order_longest_first, on the device (no host round trip).
+        Consecutive SGA steps move x0 a little and reuse the MC streams, so a trajectory's work
+        repeats closely and the longest ones no longer start last (the launch's tail).
 
         The kernel's waves drain one queue per XCD over a contiguous eighth of the queue positions
-        first (mrbo_rollout.hip rollout_kernel), so the ranking is dealt round-robin over the eight
-        chunks: the r-th longest trajectory goes to position r // 8 of chunk r % 8.  Every chunk is
-        then longest-first and carries an eighth of the work; a plain global sort would hand XCD 0
-        the longest eighth and leave the shortest ones of chunk 0 for the end of the launch."""
+        first (mrbo_rollout.hip rollout_kernel), so the library deals the ranking round-robin over
+        the eight chunks: the r-th longest trajectory goes to position r // 8 of chunk r % 8.  Every
+        chunk is then longest-first and carries an eighth of the work; a plain global sort would hand
+        XCD 0 the longest eighth and leave the shortest ones of chunk 0 for the end of the launch.
+        The plan owns the order; order_out (int32 device tensor of M·R) receives a copy.
+        longest_first_order() is the torch mirror."""
         torch = _torch()
-        ev = out["evals"].view(-1, _lib.NCOUNTERS).to(torch.float64)
-        w = torch.tensor(self.ORDER_WEIGHTS, dtype=torch.float64, device=ev.device)
-        ranks = torch.argsort(ev @ w, descending=True)
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        _lib.check(self.lib.mrbo_plan_order_longest_first(self.handle, p(out["evals"]), p(order_out),
+                                                          ctypes.c_void_p(st.cuda_stream)))
+        self._order = None
+
+    @classmethod
+    def longest_first_order(cls, evals):
+        """Torch mirror of mrbo_plan_order_longest_first: the stable descending ranking of the
+        weighted counters dealt round-robin over the per-XCD chunks (xcd_round_robin)."""
+        import torch
+        ev = evals.view(-1, _lib.NCOUNTERS).to(torch.float64)
+        w = torch.tensor(cls.ORDER_WEIGHTS, dtype=torch.float64, device=ev.device)
+        ranks = torch.sort(ev.clamp(min=0) @ w, descending=True, stable=True).indices
         pos = xcd_round_robin(ranks.numel(), ranks.device)
         order = torch.empty_like(ranks)
         order[pos] = ranks
-        self.set_order(order.to(torch.int32))
+        return order.to(torch.int32)
 
     def info(self):
         """Launch geometry: rows per lane, workgroups, waves per workgroup, batched start values,

@@ -80,3 +80,30 @@ def test_set_order_rejects_wrong_length(gpu):
         plan.set_order(dup)
     rc = plan.lib.mrbo_plan_set_order(plan.handle, ctypes.c_void_p(bad.data_ptr()), bad.numel())
     assert rc == -1   # MRBO_ERR_ARG
+
+
+@pytest.mark.parametrize("name,M,R", [("C2", 256, 16), ("C3", 128, 8), ("C3", 100, 3)])
+def test_library_longest_first_order(gpu, name, M, R):
+    """mrbo_plan_order_longest_first: the device-computed order is a permutation, equals the torch
+    mirror (stable descending ranking of the weighted counters dealt round-robin over the eight
+    per-XCD queue chunks, RolloutPlan.longest_first_order), is what the plan's next launches use,
+    and leaves every output bit-identical.  M·R = 300 checks the ragged chunk sizes."""
+    torch, plan, args = _setup(name, M, R)
+    ref = _launch(torch, plan, args)
+    T = M * R
+    got = torch.full((T,), -7, dtype=torch.int32, device="cuda:0")
+    try:
+        plan.order_longest_first(ref, order_out=got)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.sort(got.to(torch.int64)).values, torch.arange(T, device="cuda:0"))
+        assert torch.equal(got, plan.longest_first_order(ref["evals"]))
+        # queue position 0 of every chunk holds one of the eight longest trajectories
+        ev = ref["evals"].view(T, -1).to(torch.float64) @ torch.tensor(plan.ORDER_WEIGHTS, dtype=torch.float64,
+                                                                       device="cuda:0")
+        heads = got[torch.tensor([x * T // 8 for x in range(8)], device="cuda:0").long()].long()
+        assert ev[heads].min() >= torch.sort(ev, descending=True).values[7]
+        out = _launch(torch, plan, args)     # runs in the library's order
+        for k, v in ref.items():
+            assert torch.equal(out[k], v), f"{name}: output {k} differs under the library's order"
+    finally:
+        plan.set_order(None)

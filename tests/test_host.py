@@ -379,3 +379,25 @@ def test_every_kernel_unit_matches_the_kparams_layout(tmp_path):
                            f"-Wl,-rpath,{libdir}"])
     out = subprocess.run([exe], capture_output=True, text=True)
     assert out.returncode == 0 and " 0 mismatched" in out.stdout, out.stdout + out.stderr
+
+
+@pytest.mark.parametrize("T", [1, 7, 8, 19, 4096, 65536 + 5])
+def test_longest_first_deals_round_robin_over_the_xcd_chunks(T):
+    """order_longest_first deals the work ranking round-robin over the kernel's eight per-XCD queue
+    chunks [x·T/8, (x+1)·T/8): a permutation of the positions, every chunk longest-first, and the
+    chunks' shares of the ranking differ by at most one item per rank round."""
+    import torch
+    from mrbo.engine import XCD_QUEUES, xcd_round_robin
+    pos = xcd_round_robin(T)
+    assert torch.equal(torch.sort(pos).values, torch.arange(T))
+    lo = [x * T // XCD_QUEUES for x in range(XCD_QUEUES + 1)]
+    chunk_of = np.searchsorted(lo[1:], pos.numpy(), side="right")
+    rank_at = np.empty(T, dtype=np.int64)
+    rank_at[pos.numpy()] = np.arange(T)
+    for x in range(XCD_QUEUES):
+        ranks = rank_at[lo[x]:lo[x + 1]]
+        assert (np.diff(ranks) > 0).all()          # the chunk's queue takes its items longest first
+    # the first 8·k ranks spread over the chunks as evenly as their sizes allow
+    k = min(T, 8 * (T // 8))
+    counts = np.bincount(chunk_of[:k], minlength=XCD_QUEUES)
+    assert counts.max() - counts.min() <= 1

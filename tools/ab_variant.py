@@ -36,7 +36,7 @@ def main():
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     vdir = os.path.join(g.PKG, "mrbo", "variants")
     os.makedirs(vdir, exist_ok=True)
-    base = [os.path.join(g.OBJDIR, "api.o"), os.path.join(g.OBJDIR, "gpfit.o")]
+    base = [os.path.join(g.OBJDIR, "api.o"), os.path.join(g.OBJDIR, "gpfit.o"), os.path.join(g.OBJDIR, "order.o")]
     for b in base:
         if not os.path.exists(b):
             raise SystemExit(f"{b} missing: run __graft_entry__.build() first")
