@@ -66,10 +66,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--schedule", choices=("auto", "index", "longest-first"), default="auto",
                     help="order in which the persistent waves take the trajectories: index order, or "
-                         "longest first by the first step's work counters, dealt round-robin over the "
-                         "kernel's eight per-XCD queue chunks (mrbo.engine.xcd_round_robin); auto (default) "
-                         "= longest first (C3: idle tail of the persistent grid 7.0 -> 1.2 %%, kernel "
-                         "9.28 -> 8.75 ms; C3-MLE 46.1 -> 45.0 ms; DESIGN.md §2)")
+                         "longest first by the first step's work counters within each of the kernel's "
+                         "eight per-XCD queue chunks (mrbo_plan_order_longest_first); auto (default) = "
+                         "longest first (C3: idle tail of the persistent grid 6.6 -> 1.1 %%, kernel "
+                         "9.21 -> 8.66 ms; C3-MLE 46.1 -> 45.0 ms; DESIGN.md §2)")
     ap.add_argument("--longest-first", action="store_true", help="same as --schedule longest-first")
     ap.add_argument("--resort", type=int, default=0,
                     help="longest-first schedule: re-rank from every K-th step's work counters "
@@ -358,7 +358,7 @@ def main():
                                   if args.solver == "sga" else
                                   f"eswavs + Adam η={eta:g} β=(0.9, 0.999) ε=1e-8 (utils.jl:114-123, "
                                   f"optimizers.jl:49-74)"),
-                   "schedule": "longest first (first step's work counters, round-robin over the per-XCD queue chunks)" if longest_first else "index order"},
+                   "schedule": "longest first within the per-XCD queue chunks (first step's work counters)" if longest_first else "index order"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": kernel_label(d, info), "kernel_ms": kms, "flops_per_launch": fl,

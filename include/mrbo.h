@@ -333,15 +333,17 @@ int mrbo_plan_set_order(mrbo_plan_t* plan, const int32_t* order, int64_t n);
 
 /* The same, with the order computed on the device by the library (no reference counterpart;
  * scheduling only): `evals` is a DEVICE array of M×R×5 work counters as a previous
- * mrbo_simulate_mc on this plan wrote them.  The trajectories are ranked by their weighted work
- * (grad 2.5, value 1, Hessian 3, adjoint rich evaluation 5, adjoint pair 3, in value-evaluation
- * units; a stable descending radix sort), and the ranking is dealt round-robin over the rollout
- * kernel's eight per-XCD queue chunks, so that each chunk is longest first and carries an eighth
- * of the work.  The plan owns the order (grown on demand, freed with the plan); it is used by the
- * plan's later launches until mrbo_plan_set_order replaces it (NULL: identity).  Stream-ordered:
- * no host round trip.  `order_out` (DEVICE, M×R int32, or NULL) receives a copy of the order.
- * mrbo_stochastic_solve does this after its first launch when the caller has set no order.
- * M×R ≥ 2^31: MRBO_ERR_ARG.                                                                    */
+ * mrbo_simulate_mc on this plan wrote them.  The rollout kernel's waves drain one queue per XCD
+ * over a contiguous eighth of the queue positions, chunk x = [x·T/8, (x+1)·T/8), before the
+ * others; the order keeps every trajectory in its own chunk and puts each chunk's trajectories
+ * longest first by their weighted work (grad 2.5, value 1, Hessian 3, adjoint rich evaluation 5,
+ * adjoint pair 3, in value-evaluation units; one stable descending radix sort, ties in index
+ * order), so the launch no longer ends on its longest trajectories and each XCD still writes one
+ * contiguous range of output rows.  The plan owns the order (grown on demand, freed with the
+ * plan); the plan's later launches use it until mrbo_plan_set_order replaces it (NULL:
+ * identity).  Stream-ordered: no host round trip.  `order_out` (DEVICE, M×R int32, or NULL)
+ * receives a copy of the order.  mrbo_stochastic_solve does this after its first launch when the
+ * caller has set no order.  M×R ≥ 2^31: MRBO_ERR_ARG.                                          */
 int mrbo_plan_order_longest_first(mrbo_plan_t* plan, const int64_t* evals, int32_t* order_out, void* stream);
 
 #ifdef __cplusplus

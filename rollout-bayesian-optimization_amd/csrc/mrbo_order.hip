@@ -6,10 +6,12 @@
 // order the launch ends with whatever trajectories happen to sit last in each chunk; C3's heavy-tailed
 // Newton work (a few trajectories run ~3× the mean) then leaves 7 % of the grid idle at the end.
 // Consecutive SGA steps move x0 a little and reuse the MC streams, so a trajectory's work repeats
-// closely: ranking the trajectories by the previous launch's work counters and dealing the ranking
-// round-robin over the eight chunks makes every chunk longest-first with an eighth of the work
-// (C3: idle tail 7.0 → 1.2 %).  Scheduling only: every output is bit-identical under
-// any order (tests/test_gpu_schedule.py).  The Python mirror is mrbo.engine.xcd_round_robin.
+// closely: each chunk's OWN trajectories (index range [x·T/8, (x+1)·T/8)) are re-ordered longest
+// first by the previous launch's work counters.  A chunk keeps its index range, so each XCD still
+// writes the output rows of one contiguous range (whole cache lines in one L2); an XCD that drains
+// its chunk early takes the short ends of the others.  Scheduling only: every output is
+// bit-identical under any order (tests/test_gpu_schedule.py).  The Python mirror is
+// RolloutPlan.longest_first_order.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -23,6 +25,9 @@ namespace {
 // rich evaluation 5, adjoint pair 3: RolloutPlan.ORDER_WEIGHTS) -- integers, so the key is exact
 constexpr unsigned KW[NCOUNT] = {5u, 2u, 6u, 10u, 6u};
 
+constexpr int Q = MRBO_QUEUE_INTS / 16;   // queue heads: one per XCD
+constexpr unsigned WBITS = 29;             // work key bits below the 3 chunk bits
+
 __global__ void order_keys_kernel(const long long* __restrict__ evals, int T, unsigned* __restrict__ key,
                                   int* __restrict__ idx) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -33,35 +38,12 @@ __global__ void order_keys_kernel(const long long* __restrict__ evals, int T, un
     const long long e = evals[(long long)NCOUNT * t + c];
     k += (unsigned long long)(e > 0 ? e : 0) * KW[c];
   }
-  key[t] = k > 0xFFFFFFFFull ? 0xFFFFFFFFu : (unsigned)k;
+  int x = 0;   // the per-XCD queue chunk that holds t in index order: x·T/8 ≤ t < (x+1)·T/8
+  while (x + 1 < Q && (long long)(x + 1) * T / Q <= t) ++x;
+  const unsigned long long wmax = (1ull << WBITS) - 1;
+  // descending order of (Q − 1 − x, work): chunk 0 first, each chunk longest first
+  key[t] = ((unsigned)(Q - 1 - x) << WBITS) | (unsigned)(k > wmax ? wmax : k);
   idx[t] = t;
-}
-
-// rank r of the (stable, descending) ranking → queue position: chunk x = [x·T/8, (x+1)·T/8)
-// takes ranks x, x + 8, x + 16, ... while every chunk still has room (r < 8·⌊T/8⌋), then the
-// chunks one item longer take the last ranks in chunk order -- the positions in the order
-// (position within its chunk, chunk), as xcd_round_robin enumerates them
-__global__ void order_deal_kernel(const int* __restrict__ ranked, int T, int* __restrict__ order) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= T) return;
-  constexpr int Q = MRBO_QUEUE_INTS / 16;   // queue heads: one per XCD
-  const long long s = T / Q;
-  long long pos;
-  if (r < Q * s) {
-    const int x = r % Q;
-    pos = (long long)x * T / Q + r / Q;
-  } else {
-    int j = r - (int)(Q * s);
-    pos = 0;
-    for (int x = 0; x < Q; ++x) {
-      const long long lo = (long long)x * T / Q, hi = (long long)(x + 1) * T / Q;
-      if (hi - lo == s + 1) {
-        if (j == 0) { pos = lo + s; break; }
-        --j;
-      }
-    }
-  }
-  order[pos] = ranked[r];
 }
 
 size_t sort_tmp_bytes(int T) {
@@ -77,7 +59,7 @@ size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // device bytes order_longest_first needs for T trajectories (the order itself included)
 size_t order_buffer_bytes(int T) {
-  return 5 * align256(sizeof(int) * (size_t)T) + align256(sort_tmp_bytes(T));
+  return 4 * align256(sizeof(int) * (size_t)T) + align256(sort_tmp_bytes(T));
 }
 
 // the schedule from one launch's work counters (evals[NCOUNT·t + k], mrbo_simulate_mc's layout)
@@ -89,18 +71,16 @@ hipError_t order_longest_first(const long long* evals, int T, void* buf, size_t 
   unsigned* key = (unsigned*)p;
   unsigned* key_sorted = (unsigned*)(p + a);
   int* idx = (int*)(p + 2 * a);
-  int* ranked = (int*)(p + 3 * a);
-  int* out = (int*)(p + 4 * a);
-  void* tmp = p + 5 * a;
+  int* out = (int*)(p + 3 * a);
+  void* tmp = p + 4 * a;
   size_t tb = sort_tmp_bytes(T);
   const int tpb = 256, nb = (T + tpb - 1) / tpb;
   hipLaunchKernelGGL(order_keys_kernel, dim3(nb), dim3(tpb), 0, st, evals, T, key, idx);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = hipcub::DeviceRadixSort::SortPairsDescending(tmp, tb, key, key_sorted, idx, ranked, T, 0, 32, st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(order_deal_kernel, dim3(nb), dim3(tpb), 0, st, (const int*)ranked, T, out);
-  e = hipGetLastError();
+  // stable: equal keys keep index order; position r of the result is queue position r, and the
+  // chunk-major key keeps every trajectory inside its own chunk's positions
+  e = hipcub::DeviceRadixSort::SortPairsDescending(tmp, tb, key, key_sorted, idx, out, T, 0, 32, st);
   if (e != hipSuccess) return e;
   *order = out;
   return hipSuccess;

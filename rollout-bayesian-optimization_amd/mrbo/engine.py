@@ -255,12 +255,11 @@ class RolloutPlan:
         repeats closely and the longest ones no longer start last (the launch's tail).
 
         The kernel's waves drain one queue per XCD over a contiguous eighth of the queue positions
-        first (mrbo_rollout.hip rollout_kernel), so the library deals the ranking round-robin over
-        the eight chunks: the r-th longest trajectory goes to position r // 8 of chunk r % 8.  Every
-        chunk is then longest-first and carries an eighth of the work; a plain global sort would hand
-        XCD 0 the longest eighth and leave the shortest ones of chunk 0 for the end of the launch.
-        The plan owns the order; order_out (int32 device tensor of M·R) receives a copy.
-        longest_first_order() is the torch mirror."""
+        first (mrbo_rollout.hip rollout_kernel); the library re-orders each chunk's own trajectories
+        longest first, so every XCD still writes the output rows of one contiguous index range
+        (whole cache lines in one L2), and an XCD that drains its chunk early takes the short ends
+        of the others.  The plan owns the order; order_out (int32 device tensor of M·R) receives a
+        copy.  longest_first_order() is the torch mirror."""
         torch = _torch()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
@@ -270,16 +269,12 @@ class RolloutPlan:
 
     @classmethod
     def longest_first_order(cls, evals):
-        """Torch mirror of mrbo_plan_order_longest_first: the stable descending ranking of the
-        weighted counters dealt round-robin over the per-XCD chunks (xcd_round_robin)."""
+        """Torch mirror of mrbo_plan_order_longest_first (longest_first_within_chunks of the
+        integer work keys 2 × Σ ORDER_WEIGHTS · counters)."""
         import torch
-        ev = evals.view(-1, _lib.NCOUNTERS).to(torch.float64)
-        w = torch.tensor(cls.ORDER_WEIGHTS, dtype=torch.float64, device=ev.device)
-        ranks = torch.sort(ev.clamp(min=0) @ w, descending=True, stable=True).indices
-        pos = xcd_round_robin(ranks.numel(), ranks.device)
-        order = torch.empty_like(ranks)
-        order[pos] = ranks
-        return order.to(torch.int32)
+        ev = evals.view(-1, _lib.NCOUNTERS).clamp(min=0)
+        w2 = torch.tensor([int(round(2 * w)) for w in cls.ORDER_WEIGHTS], dtype=torch.int64, device=ev.device)
+        return longest_first_within_chunks((ev.to(torch.int64) * w2).sum(1))
 
     def info(self):
         """Launch geometry: rows per lane, workgroups, waves per workgroup, batched start values,
@@ -291,19 +286,27 @@ class RolloutPlan:
 
 
 XCD_QUEUES = 8   # work-queue heads of the rollout kernel (MRBO_QUEUE_INTS / 16)
+ORDER_WBITS = 29  # work-key bits of mrbo_plan_order_longest_first (csrc/mrbo_order.hip) below the chunk
 
 
-def xcd_round_robin(T, device=None):
-    """Queue positions 0..T-1 in the order (position within its chunk, chunk), for the kernel's
-    per-XCD chunks [x·T/8, (x+1)·T/8) (integer division, as rollout_kernel computes them): entry r
-    is the position that the r-th item of a ranking takes when the ranking is dealt round-robin
-    over the chunks.  Pure index arithmetic (CPU-testable): no GPU needed."""
+def xcd_chunks(T, device=None):
+    """Per-XCD queue chunk of every queue position 0..T-1: chunk x = [x·T/8, (x+1)·T/8) (integer
+    division, as rollout_kernel computes them).  Pure index arithmetic (CPU-testable)."""
     import torch
     p = torch.arange(T, dtype=torch.int64, device=device)
-    lo = torch.tensor([x * T // XCD_QUEUES for x in range(XCD_QUEUES)], dtype=torch.int64, device=device)
-    chunk = torch.bucketize(p, lo[1:], right=True)
-    key = (p - lo[chunk]) * XCD_QUEUES + chunk
-    return torch.argsort(key)
+    lo = torch.tensor([x * T // XCD_QUEUES for x in range(1, XCD_QUEUES)], dtype=torch.int64, device=device)
+    return torch.bucketize(p, lo, right=True)
+
+
+def longest_first_within_chunks(work, device=None):
+    """The order of mrbo_plan_order_longest_first from integer work keys (2 × the weighted counters):
+    every chunk's own trajectories, longest first, stable in index order on ties -- queue position r
+    takes trajectory order[r] and stays in the chunk it had in index order."""
+    import torch
+    work = torch.as_tensor(work, dtype=torch.int64, device=device).clamp(0, (1 << ORDER_WBITS) - 1)
+    chunk = xcd_chunks(work.numel(), work.device)
+    key = ((XCD_QUEUES - 1 - chunk) << ORDER_WBITS) | work
+    return torch.sort(key, descending=True, stable=True).indices.to(torch.int32)
 
 
 def rnstream(M, d, H):

@@ -382,22 +382,22 @@ def test_every_kernel_unit_matches_the_kparams_layout(tmp_path):
 
 
 @pytest.mark.parametrize("T", [1, 7, 8, 19, 4096, 65536 + 5])
-def test_longest_first_deals_round_robin_over_the_xcd_chunks(T):
-    """order_longest_first deals the work ranking round-robin over the kernel's eight per-XCD queue
-    chunks [x·T/8, (x+1)·T/8): a permutation of the positions, every chunk longest-first, and the
-    chunks' shares of the ranking differ by at most one item per rank round."""
+def test_longest_first_stays_within_the_xcd_chunks(T):
+    """The longest-first order (mrbo_plan_order_longest_first's mirror) re-orders each per-XCD queue
+    chunk [x·T/8, (x+1)·T/8) over its OWN trajectories: a permutation, every chunk's positions hold
+    exactly the trajectories of its index range (so each XCD writes one contiguous range of output
+    rows), longest first, ties in index order."""
     import torch
-    from mrbo.engine import XCD_QUEUES, xcd_round_robin
-    pos = xcd_round_robin(T)
-    assert torch.equal(torch.sort(pos).values, torch.arange(T))
+    from mrbo.engine import XCD_QUEUES, longest_first_within_chunks
+    g = torch.Generator().manual_seed(T)
+    work = torch.randint(0, 50, (T,), generator=g)
+    order = longest_first_within_chunks(work).to(torch.int64)
+    assert torch.equal(torch.sort(order).values, torch.arange(T))
     lo = [x * T // XCD_QUEUES for x in range(XCD_QUEUES + 1)]
-    chunk_of = np.searchsorted(lo[1:], pos.numpy(), side="right")
-    rank_at = np.empty(T, dtype=np.int64)
-    rank_at[pos.numpy()] = np.arange(T)
     for x in range(XCD_QUEUES):
-        ranks = rank_at[lo[x]:lo[x + 1]]
-        assert (np.diff(ranks) > 0).all()          # the chunk's queue takes its items longest first
-    # the first 8·k ranks spread over the chunks as evenly as their sizes allow
-    k = min(T, 8 * (T // 8))
-    counts = np.bincount(chunk_of[:k], minlength=XCD_QUEUES)
-    assert counts.max() - counts.min() <= 1
+        seg = order[lo[x]:lo[x + 1]]
+        assert torch.equal(torch.sort(seg).values, torch.arange(lo[x], lo[x + 1]))
+        w = work[seg]
+        assert (w[:-1] >= w[1:]).all()
+        ties = (w[:-1] == w[1:])
+        assert (seg[:-1][ties] < seg[1:][ties]).all()
