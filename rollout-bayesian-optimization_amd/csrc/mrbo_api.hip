@@ -867,12 +867,13 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
   static unsigned long long* dtail = nullptr;
   static int ntail = 0;
   const int nwaves = P->blocks * P->wpg;
-  if (nwaves > ntail) {
+  const size_t ntailw = 3 * (size_t)nwaves + (size_t)T;   // + one wall time per trajectory
+  if ((long long)ntailw > ntail) {
     if (dtail) HIP_TRY(hipFree(dtail));
-    HIP_TRY(hipMalloc(&dtail, sizeof(unsigned long long) * 3 * nwaves));
-    ntail = nwaves;
+    HIP_TRY(hipMalloc(&dtail, sizeof(unsigned long long) * ntailw));
+    ntail = (int)ntailw;
   }
-  HIP_TRY(hipMemsetAsync(dtail, 0, sizeof(unsigned long long) * 3 * nwaves, st));
+  HIP_TRY(hipMemsetAsync(dtail, 0, sizeof(unsigned long long) * ntailw, st));
   kp.stamps = dtail;
 #endif
   kp.xs_lds = P->xs_lds;
@@ -899,7 +900,7 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
   ++P->nlaunch;
 #ifdef MRBO_TAIL
   {
-    std::vector<unsigned long long> h(3 * (size_t)nwaves);
+    std::vector<unsigned long long> h(3 * (size_t)nwaves + (size_t)T);
     HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipMemcpy(h.data(), dtail, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
     unsigned long long t0 = ~0ull, t1 = 0;
@@ -929,6 +930,22 @@ static int simulate_common(mrbo_plan_t* P, const double* x0s, const double* rnst
             "ends p0 %.4f p10 %.4f p50 %.4f p90 %.4f  traj/wave %d..%d  us/traj/wave %.2f\n",
             nw, span / 100.0, busy / (nw * span), headv / (nw * span), 1.0 - (busy + headv) / (nw * span),
             pct(0.0), pct(0.1), pct(0.5), pct(0.9), nmin, nmax, busy / 100.0 / (double)std::max(ntr, 1ll));
+    // MRBO_TAIL_DUMP=path: append this launch's per-trajectory wall times (int64 REFCLK ticks, T)
+    // and, when the caller asked for them, its work counters (int64, NCOUNT·T) -- calibration data
+    // for the schedule's work weights
+    if (const char* path = getenv("MRBO_TAIL_DUMP")) {
+      if (FILE* f = fopen(path, "ab")) {
+        const long long hdr[2] = {(long long)T, evals ? (long long)NCOUNT : 0ll};
+        fwrite(hdr, sizeof(hdr), 1, f);
+        fwrite(h.data() + 3 * (size_t)nwaves, sizeof(unsigned long long), (size_t)T, f);
+        if (evals) {
+          std::vector<long long> ev((size_t)NCOUNT * T);
+          HIP_TRY(hipMemcpy(ev.data(), devals, sizeof(long long) * ev.size(), hipMemcpyDeviceToHost));
+          fwrite(ev.data(), sizeof(long long), ev.size(), f);
+        }
+        fclose(f);
+      }
+    }
   }
 #endif
 #ifdef MRBO_STAMPS

@@ -3036,9 +3036,15 @@ __global__ void __launch_bounds__((KBounds<D, RPL, HW>::threads), (KBounds<D, RP
       tr = (id >= 0 && id < kp.T) ? id : tr;
     }
     if (kp.skip_active && kp.skip_active[tr / kp.M] == 0) continue;   // a stopped restart (outer ascent)
+#ifdef MRBO_TAIL
+    const unsigned long long t_tr = __builtin_amdgcn_s_memrealtime();
+#endif
     trajectory<D, RPL, HW>(W, kp, tr);
 #ifdef MRBO_TAIL
     ++n_taken;
+    // per-trajectory wall time after the per-wave records (3 per wave of the grid)
+    if (kp.stamps && (W.lane & 31) == 0)
+      kp.stamps[3ll * gridDim.x * (blockDim.x / WAVE) + tr] = __builtin_amdgcn_s_memrealtime() - t_tr;
 #endif
   }
 #ifdef MRBO_TAIL
