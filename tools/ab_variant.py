@@ -47,7 +47,8 @@ def main():
         for d in dims:
             obj = os.path.join(vdir, f"{name}_k{d}_f{fmax}.o")
             defs = [f"-DMRBO_D={d}", "-DMRBO_AB_MIN", f"-DMRBO_AB_RPL={rpl}"] + ([f"-DMRBO_FMAX={fmax}"] if fmax != 6 else [])
-            cmd = [hipcc] + g.HIPCC_FLAGS + g.UNIT_FLAGS + shlex.split(flags) + defs + \
+            unit = g.UNIT_FLAGS + (g.F4_FLAGS if fmax == 4 else [])   # as the main build's units
+            cmd = [hipcc] + g.HIPCC_FLAGS + unit + shlex.split(flags) + defs + \
                   ["-c", "-o", obj, os.path.join(g.CSRC, "mrbo_kernels.hip")]
             procs.append((subprocess.Popen(cmd, stderr=subprocess.DEVNULL), name))
             objs.append(obj)
