@@ -716,7 +716,10 @@ int mrbo_plan_create(const mrbo_surrogate_t* s, const mrbo_params_t* p, int32_t 
   const size_t fixed = linv_bytes + (P->xs_lds ? xs_bytes : 0);
   int wpg0 = 0, blocks0 = 0;
   size_t smem0 = 0;
-  const int maxw = ks.max_threads / WAVE;
+  int maxw = ks.max_threads / WAVE;
+  // MRBO_MAX_WPG (A/B runs only): at most this many waves per rollout workgroup -- fewer resident
+  // waves per XCD, a smaller L2 footprint of their work slots and scratch
+  if (const char* mw = getenv("MRBO_MAX_WPG")) maxw = std::max(1, std::min(maxw, atoi(mw)));
   // Matérn-5/2 + EI: the compile-time specialised rollout kernel
   // (MRBO_GENERIC_KERNEL=1 forces the generic instantiation, for A/B runs and tests)
   const char* gen = getenv("MRBO_GENERIC_KERNEL");
