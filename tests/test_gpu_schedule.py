@@ -109,3 +109,14 @@ def test_library_longest_first_order(gpu, name, M, R):
             assert torch.equal(out[k], v), f"{name}: output {k} differs under the library's order"
     finally:
         plan.set_order(None)
+
+
+def test_library_longest_first_order_rejects_null_counters(gpu):
+    """mrbo_plan_order_longest_first refuses a null work-counter array (MRBO_ERR_ARG) and leaves the
+    plan's schedule as it was: the next launch's outputs equal an index-order launch's."""
+    torch, plan, args = _setup("C2", 32, 2)
+    ref = _launch(torch, plan, args)
+    assert plan.lib.mrbo_plan_order_longest_first(plan.handle, None, None, None) == -1   # MRBO_ERR_ARG
+    out = _launch(torch, plan, args)
+    for k, v in ref.items():
+        assert torch.equal(out[k], v)
