@@ -247,7 +247,6 @@ def main():
     T = pb.T
     plan = _plan_for(T.s, h, hi - lo, R, pb.es.get_starts().shape[1], pb.lbs, pb.ubs, T.θ[0], local,
                      dict(sample_offset=lo, samples_total=M_total, **pb.plan_opts()))
-    geo = plan.info()   # resident persistent waves: workgroups x waves per workgroup
     longest_first = args.longest_first or args.schedule in ("auto", "longest-first")
     dev = f"cuda:{local}"
     drn = to_device(np.asfortranarray(pb.tp.rnstream_sequence[lo:hi]), dev)   # resident in HBM
